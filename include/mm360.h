@@ -1,0 +1,142 @@
+/* mm360.h -- C-ABI of the MI355X-native 360-degree multi-model motion-compensation path.
+ *
+ * Drop-in boundary for the MM branch of VTM-17.2 + MM extension (FAU-LMS/vvc-extension-mm).
+ * The reference has no plugin/FFI API; these entry points replace the C++ method surface
+ * listed in SURVEY.md section 8(b).  Paths are relative to
+ * /root/reference/source/Lib/CommonLib (SRC) or /root/reference/source/Lib.
+ *
+ *   mm_create        <- MVReprojection::init              SRC/MVReprojection.h:32
+ *                       (+ EquirectangularProjection ctor SRC/Projection.h:127-130,
+ *                          MMConfig active-model list     SRC/MMConfig.cpp:7-39)
+ *   mm_set_epipole   <- EpipoleList::addEpipole           SRC/EpipoleList.cpp:8-11
+ *   mm_upload_ref    <- Picture reconstruction planes     SRC/Picture.cpp:84-95 (+ extendPicBorder :988-1048)
+ *   mm_reproject     <- MVReprojection::reprojectMotionVectorSubblocks
+ *                                                         SRC/MVReprojection.h:54-58
+ *   mm_pred          <- InterPrediction::xPredInterBlkMM  SRC/InterPrediction.h:151-154,
+ *                       batched over a picture's PU list together with xWeightedAverage
+ *                       (addAvg / copyClip)               SRC/InterPrediction.cpp:1584-1679
+ *   mm_filter        <- InterpolationFilter::filterHor/filterVer  SRC/InterpolationFilter.h:123-128
+ *   mm_destroy       <- (MVReprojection / InterPrediction destructors)
+ *
+ * Conventions: plain C, int status return (MM_OK = 0), one opaque context per
+ * decoder instance, explicit HIP stream, no exceptions across the ABI.  Samples are `Pel`
+ * (int16), planes are caller-owned; reprojection results are fixed-point sub-block origins
+ * (1/16 pel luma, 1/32 pel 4:2:0 chroma) in Eigen column-major order (element (row, col) of the
+ * reference's ArrayXXi at index col*rows + row).  NaN reprojections fall back to zero motion and
+ * out-of-range sub-blocks predict zeros, exactly as the reference (these are results, not errors).
+ */
+#ifndef MM360_H
+#define MM360_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MM_OK 0
+#define MM_ERR_ARG 1        /* invalid argument (reference: CHECK -> Exception) */
+#define MM_ERR_HIP 2        /* HIP runtime error */
+#define MM_ERR_NOREF 3      /* reference POC not uploaded */
+#define MM_ERR_NOEPIPOLE 4  /* no epipole for (curPOC, refPOC) -- EpipoleList.cpp:31 CHECK */
+#define MM_ERR_MODEL 5      /* motion model not active / CLASSIC passed to reprojection */
+#define MM_ERR_NODEV 6      /* no HIP device */
+
+/* MotionModelID, SRC/TypeDef.h:865-879 */
+enum mm_model_id {
+  MM_CLASSIC = 0,
+  MM_MPA_FRONT_BACK = 1,
+  MM_MPA_LEFT_RIGHT = 2,
+  MM_MPA_TOP_BOTTOM = 3,
+  MM_TANGENTIAL = 4,
+  MM_THREE_D_TRANSLATIONAL = 5,
+  MM_ROTATIONAL = 6,
+  MM_GEODESIC_X = 7,
+  MM_GEODESIC_Y = 8,
+  MM_GEODESIC_Z = 9,
+  MM_GEODESIC_CAMPOSE = 10
+};
+
+/* Sequence parameters (SPS fields + hard-coded MM settings, EncApp.cpp:754-768) */
+typedef struct mm_seq_params {
+  int32_t width, height;       /* luma picture size of the ERP picture */
+  int32_t chroma_format;       /* 0 = 4:0:0, 1 = 4:2:0 (ChromaFormat CHROMA_400 / CHROMA_420) */
+  int32_t bit_depth;           /* internal bit depth (10 in the RA cfg) */
+  int32_t max_cu_width;        /* SPS maxCUWidth (CTU size, 128) -- out-of-range rule */
+  int32_t max_cu_height;
+  int32_t mm_offset4x4;        /* SPS MMOffset4x4 code 0..4 (4 => 1.5), MVReprojection.cpp:10 */
+  int32_t ged_flavor;          /* 0 VISHWANATH_ORIGINAL, 1 VISHWANATH_MODULATED */
+  uint32_t active_models;      /* bit i set <=> MotionModelID i active (CLASSIC always) */
+} mm_seq_params;
+
+/* One reprojection request == one call of reprojectMotionVectorSubblocks */
+typedef struct mm_block_desc {
+  int32_t x, y, w, h;          /* block position/size in COMPONENT units (pu.blocks[compID]) */
+  int32_t mv_hor, mv_ver;      /* Mv in 1/16 luma units (MV_FRACTIONAL_BITS_INTERNAL = 4) */
+  int32_t model;               /* mm_model_id, not CLASSIC */
+  int32_t comp;                /* 0 = luma, 1 = Cb, 2 = Cr */
+  int32_t cur_poc, ref_poc;    /* for GEODESIC_CAMPOSE epipole selection */
+} mm_block_desc;
+
+/* One prediction unit (or sub-PU after the host's xSubPuBio / DMVR / SbTMVP split) */
+typedef struct mm_pu_desc {
+  int32_t x, y, w, h;          /* luma area */
+  int32_t mv[2][2];            /* [list][hor, ver], 1/16 luma */
+  int32_t ref_poc[2];          /* reference POC per list, -1 = list unused */
+  int32_t model[2];            /* mm_model_id per list (non-CLASSIC for MM MC) */
+} mm_pu_desc;
+
+typedef struct mm_ctx mm_ctx;
+
+/* Lifecycle */
+int mm_create(const mm_seq_params* params, int device, mm_ctx** out_ctx);
+int mm_destroy(mm_ctx* ctx);
+int mm_set_stream(mm_ctx* ctx, void* hip_stream);     /* hipStream_t; NULL = default stream */
+int mm_synchronize(mm_ctx* ctx);
+const char* mm_last_error(mm_ctx* ctx);
+int mm_get_version(void);
+
+/* Epipoles in Q24 fixed point (EPIPOLE_PRECISION_FIXED, CommonDef.h:441).  cur/ref POC -1 are
+ * the wildcards of EpipoleList::findEpipoleFixed (exact pair, then (cur,-1), then (-1,-1)). */
+int mm_set_epipole(mm_ctx* ctx, int cur_poc, int ref_poc, const int32_t q24[3]);
+
+/* Reference picture planes (reconstruction, unpadded, picture origin at plane[0]).  `src_is_device`
+ * = 1 when the pointers are device memory.  The context keeps its own device copy; padding is
+ * implicit (edge replication == coordinate clamping, Picture.cpp:988-1048). */
+int mm_upload_ref(mm_ctx* ctx, int poc, const int16_t* y, ptrdiff_t stride_y, const int16_t* cb,
+                  const int16_t* cr, ptrdiff_t stride_c, int src_is_device);
+int mm_release_ref(mm_ctx* ctx, int poc);
+
+/* Parity API: n blocks, results written to out_xy (host memory) as int32 pairs
+ * [X0, Y0, X1, Y1, ...] block after block, N_b = (w/sbw)*(h/sbh) pairs per block. */
+int mm_reproject(mm_ctx* ctx, const mm_block_desc* blocks, int n, int32_t* out_xy);
+
+/* Batched motion compensation of one picture's PU list (host descriptor array).
+ * Writes the final prediction (bi: addAvg of both lists' 14-bit predictions; uni: clipped
+ * prediction) of every PU into the destination planes (device memory, picture-sized). */
+int mm_pred(mm_ctx* ctx, int cur_poc, const mm_pu_desc* pus, int n, int16_t* dst_y,
+            ptrdiff_t dst_stride_y, int16_t* dst_cb, int16_t* dst_cr, ptrdiff_t dst_stride_c);
+
+/* Split form for resident-input benchmarking: mm_pred_prepare uploads and plans the PU list
+ * (kept in the context); mm_pred_run executes the prepared list (all device work, no host
+ * synchronisation).  mm_pred == prepare + run. */
+int mm_pred_prepare(mm_ctx* ctx, int cur_poc, const mm_pu_desc* pus, int n);
+int mm_pred_run(mm_ctx* ctx, int16_t* dst_y, ptrdiff_t dst_stride_y, int16_t* dst_cb,
+                int16_t* dst_cr, ptrdiff_t dst_stride_c);
+
+/* Single-block interpolation (InterpolationFilter::filterHor/filterVer on the device), for
+ * parity tests of the integer pel pipeline.  comp 0 = luma 8-tap (16 phases), else chroma 4-tap
+ * (32 phases).  `src` points at the block origin inside a host buffer that holds at least
+ * (taps/2 - 1) samples of margin on every side; dst is host memory (w*h int16). */
+int mm_filter(mm_ctx* ctx, int comp, int vertical, const int16_t* src, ptrdiff_t src_stride,
+              int16_t* dst, ptrdiff_t dst_stride, int w, int h, int frac, int is_first,
+              int is_last);
+
+/* Kernel timing of the last mm_pred_run (HIP events on the context stream), milliseconds. */
+int mm_last_timing(mm_ctx* ctx, float* ms_total);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MM360_H */

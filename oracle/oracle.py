@@ -1,0 +1,100 @@
+"""ctypes binding of the CPU oracle (oracle/mm_oracle.c) -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module; the
+product (vvc-extension-mm_amd/) never does.  Parity status: UNPINNED (see mm_oracle.c header).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from ctypes import POINTER, c_int, c_int32, c_void_p
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "_build", "libmmoracle.so")
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def load():
+    if not os.path.exists(LIB):
+        build()
+    lib = ctypes.CDLL(LIB)
+    lib.orc_create.restype = c_void_p
+    lib.orc_create.argtypes = [c_void_p]
+    lib.orc_destroy.argtypes = [c_void_p]
+    lib.orc_set_epipole.argtypes = [c_void_p, c_int, c_int, POINTER(c_int32)]
+    lib.orc_reproject.argtypes = [c_void_p, c_void_p, c_int, c_void_p]
+    lib.orc_pred.argtypes = [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                             ctypes.c_ssize_t, ctypes.c_ssize_t, c_void_p, ctypes.c_ssize_t, c_void_p, c_void_p,
+                             ctypes.c_ssize_t]
+    lib.orc_filter.argtypes = [c_int, c_int, c_int, c_void_p, ctypes.c_ssize_t, c_void_p, ctypes.c_ssize_t, c_int,
+                               c_int, c_int, c_int, c_int]
+    return lib
+
+
+def _ptr_array(arrs):
+    return (c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+
+
+class Oracle:
+    """CPU restatement of MVReprojection / xPredInterBlkMM for one sequence."""
+
+    def __init__(self, params, epipoles=()):
+        self.lib = load()
+        self.params = params
+        self.h = self.lib.orc_create(ctypes.byref(params))
+        for (cur, ref, q) in epipoles:
+            self.set_epipole(cur, ref, q)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.lib.orc_destroy(self.h)
+            self.h = None
+
+    def set_epipole(self, cur, ref, q):
+        self.lib.orc_set_epipole(self.h, cur, ref, (c_int32 * 3)(*q))
+
+    def reproject(self, blocks):
+        blocks = np.ascontiguousarray(blocks)
+        sb = np.where(blocks["comp"] != 0, 2, 4)
+        total = int(((blocks["w"] // sb) * (blocks["h"] // sb)).sum())
+        out = np.zeros((max(total, 1), 2), dtype=np.int32)
+        rc = self.lib.orc_reproject(self.h, c_void_p(blocks.ctypes.data), len(blocks), c_void_p(out.ctypes.data))
+        if rc:
+            raise RuntimeError(f"oracle reproject failed: {rc}")
+        return out[:total]
+
+    def predict(self, cur_poc, pus, refs, W, H):
+        """refs: dict poc -> (Y, Cb, Cr) int16 arrays.  Returns (Y, Cb, Cr) predicted planes
+        (zero where no PU)."""
+        pus = np.ascontiguousarray(pus)
+        pocs = sorted(refs)
+        ys = [np.ascontiguousarray(refs[p][0]) for p in pocs]
+        cbs = [np.ascontiguousarray(refs[p][1]) for p in pocs]
+        crs = [np.ascontiguousarray(refs[p][2]) for p in pocs]
+        dy = np.zeros((H, W), dtype=np.int16)
+        dcb = np.zeros((H // 2, W // 2), dtype=np.int16)
+        dcr = np.zeros((H // 2, W // 2), dtype=np.int16)
+        pa = np.array(pocs, dtype=np.int32)
+        rc = self.lib.orc_pred(self.h, cur_poc, c_void_p(pus.ctypes.data), len(pus), len(pocs),
+                               c_void_p(pa.ctypes.data), _ptr_array(ys), _ptr_array(cbs), _ptr_array(crs),
+                               ys[0].shape[1], cbs[0].shape[1], c_void_p(dy.ctypes.data), W,
+                               c_void_p(dcb.ctypes.data), c_void_p(dcr.ctypes.data), W // 2)
+        if rc:
+            raise RuntimeError(f"oracle predict failed: {rc}")
+        return dy, dcb, dcr
+
+    def filter(self, comp, vertical, bd, src, x0, y0, w, h, frac, first, last):
+        src = np.ascontiguousarray(src, dtype=np.int16)
+        dst = np.zeros((h, w), dtype=np.int16)
+        base = src.ctypes.data + (y0 * src.shape[1] + x0) * 2
+        rc = self.lib.orc_filter(comp, vertical, bd, c_void_p(base), src.shape[1], c_void_p(dst.ctypes.data), w, w,
+                                 h, frac, int(first), int(last))
+        if rc:
+            raise RuntimeError(f"oracle filter failed: {rc}")
+        return dst

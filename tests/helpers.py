@@ -1,0 +1,35 @@
+"""Shared helpers for the test suites."""
+import os
+
+import numpy as np
+
+import mm360
+from mm360 import workload as W
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+EPI = [(W.CUR_POC, -1, W.GED_EPIPOLE_Q24), (-1, -1, (0, 1 << 24, 1 << 23))]
+
+
+def load_blocks(npz):
+    return np.ascontiguousarray(npz["blocks"]).view(mm360.BLOCK_DTYPE).reshape(-1)
+
+
+def load_pus(npz):
+    return np.ascontiguousarray(npz["pus"]).view(mm360.PU_DTYPE).reshape(-1)
+
+
+def block_offsets(blocks):
+    sb = np.where(blocks["comp"] != 0, 2, 4)
+    n = (blocks["w"] // sb) * (blocks["h"] // sb)
+    return np.concatenate([[0], np.cumsum(n)])
+
+
+def describe_mismatch(blocks, a, b, limit=3):
+    off = block_offsets(blocks)
+    diff = np.any(a != b, axis=1)
+    bad = [i for i in range(len(blocks)) if diff[off[i]:off[i + 1]].any()]
+    lines = [f"{len(bad)} blocks differ"]
+    for i in bad[:limit]:
+        lines.append(f"block {blocks[i]} first: {a[off[i]:off[i+1]][:2].tolist()} vs {b[off[i]:off[i+1]][:2].tolist()}")
+    return "\n".join(lines)

@@ -1,0 +1,123 @@
+// host_twin.cpp -- CPU twin of the device pipeline (TEST UTILITY).
+//
+// Runs the product's per-thread bodies (vvc-extension-mm_amd/csrc/mm_pipeline.h) and planner
+// (mm_plan.h) in host loops, compiled by g++ with the same no-contraction rules as the HIP
+// build.  The CPU test suite compares it against the oracle, which checks the device logic
+// without a GPU; the GPU suite then checks the HIP library itself.
+//   g++ -O2 -std=c++17 -ffp-contract=off -fopenmp -fPIC -shared host_twin.cpp -o libhosttwin.so
+#include <cmath>
+#include <vector>
+
+#include "mm_plan.h"
+
+using namespace mmplan;
+
+static const int8_t LUMA_T[16][8] = MM_LUMA_TAPS_INIT;
+static const int8_t CHROMA_T[32][4] = MM_CHROMA_TAPS_INIT;
+
+struct Twin {
+  SeqConst sc;
+  Geometry geo;
+  std::vector<float> px[3], py[3];
+  std::vector<uint8_t> vip[3];
+};
+
+static void make_twin(const mm_seq_params* p, Twin* t) {
+  t->sc.Wf = (float)p->width;
+  t->sc.Hf = (float)p->height;
+  t->sc.off = p->mm_offset4x4 == 4 ? 1.5f : (float)p->mm_offset4x4;
+  t->sc.focal = (float)(1. / std::tan(M_PI / p->height));
+  t->sc.res = (float)(M_PI / p->height);
+  t->sc.ged_flavor = p->ged_flavor;
+  t->geo = Geometry{p->width,        p->height,           p->width >> 1,        p->height >> 1,
+                    p->max_cu_width, p->max_cu_height,    p->max_cu_width >> 1, p->max_cu_height >> 1,
+                    p->bit_depth,    p->chroma_format == 1};
+  const int cols = p->width / 4, rows = p->height / 4, n = cols * rows;
+  for (int pl = 0; pl < 3; pl++) {
+    if (!(p->active_models & (1u << (MPA_FRONT_BACK + pl)))) continue;
+    t->px[pl].resize(n);
+    t->py[pl].resize(n);
+    t->vip[pl].resize(n);
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < n; i++)
+      mpa_cache_thread(i, t->sc, MPA_FRONT_BACK + pl, cols, rows, t->px[pl].data(), t->py[pl].data(),
+                       t->vip[pl].data());
+  }
+}
+
+static MpaCache cache_of(const Twin& t) {
+  MpaCache c{};
+  for (int pl = 0; pl < 3; pl++) {
+    c.px[pl] = t.px[pl].data();
+    c.py[pl] = t.py[pl].data();
+    c.vip[pl] = t.vip[pl].data();
+  }
+  c.cols = t.geo.W / 4;
+  c.rows = t.geo.H / 4;
+  return c;
+}
+
+static EpipoleMap epi_of(int n, const int32_t* e) {
+  EpipoleMap m;
+  for (int i = 0; i < n; i++) m[{e[5 * i], e[5 * i + 1]}] = {e[5 * i + 2], e[5 * i + 3], e[5 * i + 4]};
+  return m;
+}
+
+static void run_reproj(const Twin& t, const Plan& plan, std::vector<int32_t>* out) {
+  std::vector<BlockSetup> setups(plan.jobs.size());
+  const int nj = (int)plan.jobs.size();
+#pragma omp parallel for schedule(static)
+  for (int i = 0; i < nj; i++) setup_thread(i, t.sc, plan.jobs.data(), plan.ged.data(), setups.data());
+  out->assign(2 * (size_t)plan.n_elems, 0);
+  MpaCache c = cache_of(t);
+#pragma omp parallel for schedule(static, 256)
+  for (int g = 0; g < plan.n_elems; g++)
+    reproj_thread(g, t.sc, plan.jobs.data(), nj, plan.job_off.data(), plan.job_chunk.data(), setups.data(), c,
+                  out->data());
+}
+
+extern "C" int twin_reproject(const mm_seq_params* p, int n_epi, const int32_t* epi, const mm_block_desc* b, int n,
+                              int32_t* out) {
+  Twin t;
+  make_twin(p, &t);
+  Plan plan;
+  EpipoleMap em = epi_of(n_epi, epi);
+  Planner pl(seq_info(*p), em, &plan);
+  int rc = pl.plan_blocks(b, n);
+  if (rc) return rc;
+  std::vector<int32_t> r;
+  run_reproj(t, plan, &r);
+  std::copy(r.begin(), r.end(), out);
+  return 0;
+}
+
+extern "C" int twin_pred(const mm_seq_params* p, int n_epi, const int32_t* epi, int cur_poc, const mm_pu_desc* pus,
+                         int n, int n_refs, const int32_t* pocs, const int16_t* const* ys, const int16_t* const* cbs,
+                         const int16_t* const* crs, int stride_y, int stride_c, int16_t* dy, int sdy, int16_t* dcb,
+                         int16_t* dcr, int sdc) {
+  Twin t;
+  make_twin(p, &t);
+  Plan plan;
+  EpipoleMap em = epi_of(n_epi, epi);
+  Planner pl(seq_info(*p), em, &plan);
+  auto has = [&](int poc) {
+    for (int i = 0; i < n_refs; i++)
+      if (pocs[i] == poc) return true;
+    return false;
+  };
+  int rc = pl.plan_pus(cur_poc, pus, n, has);
+  if (rc) return rc;
+  std::vector<RefDev> refs;
+  for (int poc : plan.ref_pocs)
+    for (int i = 0; i < n_refs; i++)
+      if (pocs[i] == poc) refs.push_back(RefDev{ys[i], cbs ? cbs[i] : nullptr, crs ? crs[i] : nullptr, stride_y, stride_c});
+  std::vector<int32_t> r;
+  run_reproj(t, plan, &r);
+  const Taps taps{LUMA_T, CHROMA_T};
+  const int npu = (int)plan.pus.size();
+#pragma omp parallel for schedule(static, 256)
+  for (int g = 0; g < plan.n_sb; g++)
+    mc_thread(g, t.geo, taps, plan.pus.data(), npu, plan.pu_off.data(), plan.pu_chunk.data(), plan.jobs.data(),
+              r.data(), refs.data(), dy, sdy, dcb, dcr, sdc);
+  return 0;
+}

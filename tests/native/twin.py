@@ -1,0 +1,59 @@
+"""ctypes binding of the CPU twin (tests/native/host_twin.cpp) -- test utility."""
+import ctypes
+import os
+import subprocess
+from ctypes import c_int, c_void_p
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "_build", "libhosttwin.so")
+
+
+def load():
+    if not os.path.exists(LIB):
+        subprocess.check_call(["make", "-s", "-C", HERE])
+    lib = ctypes.CDLL(LIB)
+    lib.twin_reproject.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]
+    lib.twin_pred.argtypes = [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                              c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int]
+    return lib
+
+
+def _epi(epipoles):
+    a = np.array([[c, r, q[0], q[1], q[2]] for (c, r, q) in epipoles] or [[0] * 5], dtype=np.int32)
+    return len(epipoles), a
+
+
+def reproject(params, blocks, epipoles=()):
+    lib = load()
+    blocks = np.ascontiguousarray(blocks)
+    sb = np.where(blocks["comp"] != 0, 2, 4)
+    total = int(((blocks["w"] // sb) * (blocks["h"] // sb)).sum())
+    out = np.zeros((max(total, 1), 2), dtype=np.int32)
+    n_epi, ea = _epi(epipoles)
+    rc = lib.twin_reproject(ctypes.addressof(params), n_epi, c_void_p(ea.ctypes.data), c_void_p(blocks.ctypes.data),
+                            len(blocks), c_void_p(out.ctypes.data))
+    if rc:
+        raise RuntimeError(f"twin reproject failed: {rc}")
+    return out[:total]
+
+
+def predict(params, cur_poc, pus, refs, W, H, epipoles=()):
+    lib = load()
+    pus = np.ascontiguousarray(pus)
+    pocs = sorted(refs)
+    arrs = [[np.ascontiguousarray(refs[p][k]) for p in pocs] for k in range(3)]
+    ptrs = [(c_void_p * len(pocs))(*[a.ctypes.data for a in arrs[k]]) for k in range(3)]
+    dy = np.zeros((H, W), dtype=np.int16)
+    dcb = np.zeros((H // 2, W // 2), dtype=np.int16)
+    dcr = np.zeros((H // 2, W // 2), dtype=np.int16)
+    pa = np.array(pocs, dtype=np.int32)
+    n_epi, ea = _epi(epipoles)
+    rc = lib.twin_pred(ctypes.addressof(params), n_epi, c_void_p(ea.ctypes.data), cur_poc, c_void_p(pus.ctypes.data),
+                       len(pus), len(pocs), c_void_p(pa.ctypes.data), ptrs[0], ptrs[1], ptrs[2], arrs[0][0].shape[1],
+                       arrs[1][0].shape[1], c_void_p(dy.ctypes.data), W, c_void_p(dcb.ctypes.data),
+                       c_void_p(dcr.ctypes.data), W // 2)
+    if rc:
+        raise RuntimeError(f"twin predict failed: {rc}")
+    return dy, dcb, dcr

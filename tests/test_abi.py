@@ -1,0 +1,60 @@
+"""The C-ABI library: loads on a CPU-only host and exports every entry point of include/mm360.h.
+No compute call is made here (no GPU)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import mm360
+from helpers import ROOT
+
+
+def _header_functions():
+    text = open(os.path.join(ROOT, "include", "mm360.h")).read()
+    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(mm_\w+)\(", text, re.M)))
+
+
+def test_header_and_binding_agree():
+    assert sorted(mm360.EXPORTED_SYMBOLS) == _header_functions()
+
+
+def test_library_exports_every_symbol():
+    lib = mm360.load_library()
+    for name in _header_functions():
+        assert hasattr(lib, name), name
+
+
+def test_version():
+    assert mm360.load_library().mm_get_version() >= 100
+
+
+def test_create_without_gpu_fails_loudly():
+    try:
+        import torch
+        if torch.cuda.is_available():
+            pytest.skip("a GPU is present")
+    except ImportError:
+        pass
+    with pytest.raises(mm360.MMError) as e:
+        mm360.MMContext(mm360.seq_params(256, 128, [1]))
+    assert e.value.code in (mm360.MM_ERR_NODEV, mm360.MM_ERR_HIP)
+
+
+def test_struct_layouts_match_header():
+    text = open(os.path.join(ROOT, "include", "mm360.h")).read()
+    body = re.search(r"typedef struct mm_seq_params \{(.*?)\}", text, re.S).group(1)
+    n_fields = sum(len(re.findall(r"\w+\s*(?:,|;)", l.split("/*")[0])) for l in body.splitlines() if ";" in l)
+    assert ctypes.sizeof(mm360.SeqParams) == 4 * n_fields == 36
+    assert mm360.BLOCK_DTYPE.itemsize == 40 and mm360.PU_DTYPE.itemsize == 48
+
+
+def test_product_has_no_oracle_dependency():
+    """The product never imports, links or includes the oracle."""
+    pkg = os.path.join(ROOT, "vvc-extension-mm_amd")
+    for dp, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".h", ".hip", ".cpp", "Makefile")):
+                txt = open(os.path.join(dp, f)).read()
+                assert "oracle" not in txt.lower() or f == "__init__.py" and "oracle" not in txt, f

@@ -1,0 +1,201 @@
+"""Parity of the HIP path (through the C-ABI) with the CPU oracle and the golden vectors.
+
+Bit-exact everywhere: fixed-point reprojection results, filter outputs and predicted samples are
+integers.  Size-independent properties at the full 6144x3072 size: full-frame equality with the
+oracle, determinism, prepare/run == one-shot, uni/bi consistency."""
+import os
+
+import numpy as np
+import pytest
+
+import mm360
+from helpers import EPI, GOLDEN, describe_mismatch, load_blocks, load_pus
+from mm360 import workload as W
+from oracle.oracle import Oracle
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    mm360.load_library()  # raises if the HIP library is missing -- no fallback
+
+
+def _ctx(params, epipoles=EPI):
+    ctx = mm360.MMContext(params, device=0)
+    for (cur, ref, q) in epipoles:
+        ctx.set_epipole(cur, ref, q)
+    return ctx
+
+
+def _gpu_predict(ctx, params, cur_poc, pus, refs):
+    W_, H_ = params.width, params.height
+    for poc, (y, cb, cr) in refs.items():
+        ctx.upload_ref(poc, torch.from_numpy(y).cuda(), torch.from_numpy(cb).cuda(), torch.from_numpy(cr).cuda())
+    dy = torch.zeros((H_, W_), dtype=torch.int16, device="cuda")
+    dcb = torch.zeros((H_ // 2, W_ // 2), dtype=torch.int16, device="cuda")
+    dcr = torch.zeros_like(dcb)
+    ctx.predict(cur_poc, pus, dy, dcb, dcr)
+    torch.cuda.synchronize()
+    return dy.cpu().numpy(), dcb.cpu().numpy(), dcr.cpu().numpy()
+
+
+@pytest.mark.parametrize("name", ["reproject_c1_all_models.npz", "reproject_c2_all_models.npz",
+                                  "reproject_c1_offset15_original.npz"])
+def test_reproject_golden(name):
+    z = np.load(os.path.join(GOLDEN, name))
+    blocks = load_blocks(z)
+    off, flav = [int(v) for v in z["params"]]
+    params = mm360.seq_params(int(z["width"]), int(z["height"]), [int(m) for m in z["models"]], mm_offset4x4=off,
+                              ged_flavor=flav)
+    with _ctx(params) as ctx:
+        got = ctx.reproject(blocks)
+    assert np.array_equal(got, z["result"]), describe_mismatch(blocks, got, z["result"])
+
+
+@pytest.mark.parametrize("w,h,seed,off,flav", [(256, 128, 11, 1, 1), (2048, 1024, 12, 0, 1), (6144, 3072, 13, 1, 1),
+                                             (1024, 512, 14, 4, 0), (4096, 2048, 15, 3, 1)])
+def test_reproject_random_vs_oracle(w, h, seed, off, flav):
+    models = W.ALL_MODELS + (7, 8, 9)
+    params = mm360.seq_params(w, h, models, mm_offset4x4=off, ged_flavor=flav)
+    blocks = W.random_blocks(w, h, models, 4000, seed, sizes=(4, 8, 16, 32, 64, 128))
+    want = Oracle(params, EPI).reproject(blocks)
+    with _ctx(params) as ctx:
+        got = ctx.reproject(blocks)
+    assert np.array_equal(got, want), describe_mismatch(blocks, got, want)
+
+
+def test_reproject_single_call_shape():
+    params = mm360.seq_params(256, 128, W.ALL_MODELS)
+    with _ctx(params) as ctx:
+        X, Y = ctx.reproject_motion_vector_subblocks((32, 16), (16, 8), (37, -5), mm360.ROTATIONAL, 0)
+        assert X.shape == (2, 4) and Y.shape == (2, 4)
+        # zero motion with the ROT shortcut returns the grid: (4*i + off - off) * 16
+        X0, Y0 = ctx.reproject_motion_vector_subblocks((32, 16), (16, 8), (0, 0), mm360.ROTATIONAL, 0)
+        assert np.array_equal(X0[0], (32 + 4 * np.arange(4)) * 16) and np.array_equal(Y0[:, 0], (16 + 4 * np.arange(2)) * 16)
+
+
+def test_pred_golden_c1():
+    z = np.load(os.path.join(GOLDEN, "pred_c1.npz"))
+    cfg = W.CONFIGS["C1"]
+    params = mm360.seq_params(cfg.width, cfg.height, cfg.models)
+    refs = {poc: W.ref_planes(cfg.width, cfg.height, poc) for poc in W.REF_POCS}
+    with _ctx(params) as ctx:
+        y, cb, cr = _gpu_predict(ctx, params, W.CUR_POC, load_pus(z), refs)
+    assert np.array_equal(y, z["y"]) and np.array_equal(cb, z["cb"]) and np.array_equal(cr, z["cr"])
+
+
+@pytest.mark.parametrize("cfg_name,frame", [("C1", 3), ("C2", 0), ("C2", 5), ("C3", 0)])
+def test_pred_full_frame_vs_oracle(cfg_name, frame):
+    cfg = W.CONFIGS[cfg_name]
+    params = mm360.seq_params(cfg.width, cfg.height, cfg.models)
+    pus = W.pu_list(cfg, frame=frame)
+    refs = {poc: W.ref_planes(cfg.width, cfg.height, poc) for poc in W.REF_POCS}
+    want = Oracle(params, EPI).predict(W.CUR_POC, pus, refs, cfg.width, cfg.height)
+    with _ctx(params) as ctx:
+        got = _gpu_predict(ctx, params, W.CUR_POC, pus, refs)
+    for name, g, w in zip("Y Cb Cr".split(), got, want):
+        assert np.array_equal(g, w), f"{name}: {(g != w).sum()} samples differ"
+
+
+@pytest.mark.parametrize("model", W.ALL_MODELS)
+def test_pred_uniform_per_model(model):
+    cfg = W.CONFIGS["C2"]
+    params = mm360.seq_params(cfg.width, cfg.height, W.ALL_MODELS)
+    pus = W.pu_list(cfg, uniform=True, uniform_model=model)
+    refs = {poc: W.ref_planes(cfg.width, cfg.height, poc) for poc in W.REF_POCS}
+    want = Oracle(params, EPI).predict(W.CUR_POC, pus, refs, cfg.width, cfg.height)
+    with _ctx(params) as ctx:
+        got = _gpu_predict(ctx, params, W.CUR_POC, pus, refs)
+    for g, w in zip(got, want):
+        assert np.array_equal(g, w)
+
+
+def test_pred_extreme_motion_zeroing():
+    cfg = W.CONFIGS["C1"]
+    params = mm360.seq_params(cfg.width, cfg.height, W.ALL_MODELS)
+    pus = W.pu_list(cfg, frame=2)
+    rng = np.random.default_rng(9)
+    pus["model"] = rng.choice(np.array(W.ALL_MODELS), size=pus["model"].shape)
+    pus["mv"] = rng.integers(-(1 << 14), 1 << 14, size=pus["mv"].shape)
+    refs = {poc: W.ref_planes(cfg.width, cfg.height, poc) for poc in W.REF_POCS}
+    want = Oracle(params, EPI).predict(W.CUR_POC, pus, refs, cfg.width, cfg.height)
+    with _ctx(params) as ctx:
+        got = _gpu_predict(ctx, params, W.CUR_POC, pus, refs)
+    for g, w in zip(got, want):
+        assert np.array_equal(g, w)
+    assert (got[0] == 0).any(), "expected some zeroed (out-of-range) sub-blocks"
+
+
+def test_pred_deterministic_and_split_api():
+    cfg = W.CONFIGS["C2"]
+    params = mm360.seq_params(cfg.width, cfg.height, cfg.models)
+    pus = W.pu_list(cfg, frame=7)
+    refs = {poc: W.ref_planes(cfg.width, cfg.height, poc) for poc in W.REF_POCS}
+    with _ctx(params) as ctx:
+        a = _gpu_predict(ctx, params, W.CUR_POC, pus, refs)
+        dy = torch.full((cfg.height, cfg.width), -1, dtype=torch.int16, device="cuda")
+        dcb = torch.full((cfg.height // 2, cfg.width // 2), -1, dtype=torch.int16, device="cuda")
+        dcr = torch.full_like(dcb, -1)
+        ctx.prepare(W.CUR_POC, pus)
+        for _ in range(3):
+            ctx.run(dy, dcb, dcr)
+        ctx.synchronize()
+        assert ctx.last_timing_ms() > 0
+    for x, t in zip(a, (dy, dcb, dcr)):
+        assert np.array_equal(x, t.cpu().numpy())
+
+
+def _filter_cases():
+    rng = np.random.default_rng(5)
+    src = rng.integers(0, 1024, size=(40, 40)).astype(np.int16)
+    src[5:9, :] = 1023
+    src[20:24, :] = 0
+    return src
+
+
+@pytest.mark.parametrize("comp", [0, 1])
+def test_filter_all_phases_vs_oracle(comp):
+    src = _filter_cases()
+    params = mm360.seq_params(256, 128, [1])
+    orc = Oracle(params)
+    phases = 16 if comp == 0 else 32
+    with _ctx(params, []) as ctx:
+        for frac in range(phases):
+            for (w, h) in ((4, 4), (2, 2), (8, 4), (16, 16)):
+                for last in (False, True):
+                    got = ctx.filter_hor(comp, src, 8, 8, w, h, frac, last)
+                    want = orc.filter(comp, 0, 10, src, 8, 8, w, h, frac, True, last)
+                    assert np.array_equal(got, want), (comp, frac, w, h, last)
+                for first in (False, True):
+                    for last in (False, True):
+                        s = src if first else (src.astype(np.int32) * 16 - 8192).astype(np.int16)
+                        got = ctx.filter_ver(comp, s, 8, 8, w, h, frac, first, last)
+                        want = orc.filter(comp, 1, 10, s, 8, 8, w, h, frac, first, last)
+                        assert np.array_equal(got, want), (comp, frac, w, h, first, last)
+
+
+def test_error_paths():
+    cfg = W.CONFIGS["C1"]
+    params = mm360.seq_params(cfg.width, cfg.height, W.MPA3 + (mm360.GEODESIC_CAMPOSE,))
+    pus = W.pu_list(cfg)
+    with mm360.MMContext(params) as ctx:
+        with pytest.raises(mm360.MMError) as e:
+            ctx.prepare(W.CUR_POC, pus)  # no references uploaded
+        assert e.value.code == mm360.MM_ERR_NOREF
+        blk = np.array([(0, 0, 16, 16, 16, 16, mm360.GEODESIC_CAMPOSE, 0, 8, 0)], dtype=mm360.BLOCK_DTYPE)
+        with pytest.raises(mm360.MMError) as e:
+            ctx.reproject(blk)  # no epipole
+        assert e.value.code == mm360.MM_ERR_NOEPIPOLE
+        for bad_model in (mm360.CLASSIC, mm360.TANGENTIAL):
+            blk = np.array([(0, 0, 16, 16, 16, 16, bad_model, 0, 8, 0)], dtype=mm360.BLOCK_DTYPE)
+            with pytest.raises(mm360.MMError) as e:
+                ctx.reproject(blk)
+            assert e.value.code == mm360.MM_ERR_MODEL
+        blk = np.array([(250, 0, 16, 16, 16, 16, 1, 0, 8, 0)], dtype=mm360.BLOCK_DTYPE)
+        with pytest.raises(mm360.MMError) as e:
+            ctx.reproject(blk)  # outside the picture
+        assert e.value.code == mm360.MM_ERR_ARG

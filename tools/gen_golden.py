@@ -1,0 +1,51 @@
+"""Generate the committed golden vectors (tests/golden/*.npz) from the CPU oracle.
+
+The reference cannot be built or run here (Eigen 3.3.7 absent, see oracle/mm_oracle.c), so these
+vectors are the oracle's outputs -- regression pins of the oracle and the expected outputs the
+GPU tests compare against.  Numerics mode recorded in each file: glibc 2.35 libm (FMA IFUNC
+sinf/cosf), Eigen 3.3.7 SSE psin/pcos, psqrt = rsqrtps(Intel fixture table) + 1 Newton step,
+round = ties-away, 3x3 product = p0 + (p1 + p2), TAN centre = double sin/cos.
+"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path[:0] = [os.path.join(ROOT, "vvc-extension-mm_amd"), ROOT]
+import mm360  # noqa: E402
+from mm360 import workload as W  # noqa: E402
+from oracle.oracle import Oracle  # noqa: E402
+
+OUT = os.path.join(ROOT, "tests", "golden")
+MODE = "glibc2.35-fma-sincosf|eigen3.3.7-sse-psin-pcos|psqrt-rsqrtps-intel-nr1|round-away|prod3-p0+(p1+p2)|tan-centre-double"
+EPI = [(W.CUR_POC, -1, W.GED_EPIPOLE_Q24), (-1, -1, (0, 1 << 24, 1 << 23))]
+
+
+def reproject_set(name, width, height, models, n, seed, **kw):
+    params = mm360.seq_params(width, height, models, **kw)
+    blocks = W.random_blocks(width, height, models, n, seed)
+    res = Oracle(params, EPI).reproject(blocks)
+    np.savez_compressed(os.path.join(OUT, name), blocks=blocks.view(np.int32).reshape(-1, 10), result=res,
+                        width=width, height=height, models=np.array(models), mode=MODE,
+                        params=np.array([params.mm_offset4x4, params.ged_flavor]))
+    print(name, len(blocks), res.shape)
+
+
+def pred_set(name, cfg_name):
+    cfg = W.CONFIGS[cfg_name]
+    params = mm360.seq_params(cfg.width, cfg.height, cfg.models)
+    pus = W.pu_list(cfg)
+    refs = {poc: W.ref_planes(cfg.width, cfg.height, poc) for poc in W.REF_POCS}
+    y, cb, cr = Oracle(params, EPI).predict(W.CUR_POC, pus, refs, cfg.width, cfg.height)
+    np.savez_compressed(os.path.join(OUT, name), pus=pus.view(np.int32).reshape(-1, 12), y=y, cb=cb, cr=cr,
+                        mode=MODE)
+    print(name, len(pus), y.shape)
+
+
+if __name__ == "__main__":
+    reproject_set("reproject_c1_all_models.npz", 256, 128, W.ALL_MODELS, 300, 101)
+    reproject_set("reproject_c2_all_models.npz", 2048, 1024, W.ALL_MODELS + (7, 8, 9), 300, 102)
+    reproject_set("reproject_c1_offset15_original.npz", 256, 128, W.ALL_MODELS, 200, 103, mm_offset4x4=4,
+                  ged_flavor=0)
+    pred_set("pred_c1.npz", "C1")

@@ -1,0 +1,415 @@
+// mm_models.h -- per-sub-block restatement of the reference's ERP projection and the five
+// 360-degree motion models, written once for host and device.
+//
+// The reference evaluates each model on Eigen arrays holding one element per 4x4 luma
+// (2x2 chroma) sub-block (MVReprojection::reprojectMotionVectorSubblocks,
+// source/Lib/CommonLib/MVReprojection.cpp:80-166).  Element-wise every array expression is a
+// fixed sequence of float32 operations; the only cross-element effect is Eigen's packet/tail
+// split (elements [0, N - N%4) evaluated with SSE packets), which decides per expression
+// whether sin/cos/sqrt are the Cephes packet kernels or glibc scalar calls.
+// Here one call evaluates one element; the caller passes `packet` for that element.
+//
+// File:line citations are into /root/reference/source/Lib/CommonLib.
+#pragma once
+#include "mm_numerics.h"
+
+namespace mmmod {
+using namespace mmnum;
+
+// MotionModelID (TypeDef.h:865-879)
+enum ModelId : int {
+  CLASSIC = 0,
+  MPA_FRONT_BACK = 1,
+  MPA_LEFT_RIGHT = 2,
+  MPA_TOP_BOTTOM = 3,
+  TANGENTIAL = 4,
+  THREE_D_TRANSLATIONAL = 5,
+  ROTATIONAL = 6,
+  GEODESIC_X = 7,
+  GEODESIC_Y = 8,
+  GEODESIC_Z = 9,
+  GEODESIC_CAMPOSE = 10,
+  NUM_MODELS = 11
+};
+
+constexpr float PI_F = 3.14159274101257324f;     // TCoord(M_PI)
+constexpr float TWO_PI_F = 6.28318548202514648f;  // TCoord(2) * TCoord(M_PI)
+constexpr float PI_2_F = 1.57079637050628662f;    // float(M_PI_2) (double constant in array expr)
+constexpr double PI_2_D = 1.57079632679489661923;  // M_PI_2
+
+struct V3 {
+  float x, y, z;
+};
+
+// Sequence constants (MVReprojection::init, MVReprojection.cpp:7-65; Projection.h:127-130)
+struct SeqConst {
+  float Wf, Hf;    // luma picture width/height as float
+  float off;       // m_offset4x4 (code 4 -> 1.5)
+  float focal;     // float(1. / tan(M_PI / H)) -- ERP focal, reused by MPA's perspective
+  float res;       // float(M_PI / H) -- angle resolution of TAN/ROT/GED
+  int ged_flavor;  // 0 VISHWANATH_ORIGINAL, 1 VISHWANATH_MODULATED (EncApp.cpp:755 hard-codes 1)
+};
+
+// ------------------------------------------------------------------------------------------
+// Coordinate conversions (Coordinate.cpp).  `arr` selects the Eigen array form (clamp as
+// cwiseMin(1).cwiseMax(-1): NaN passes through) versus the scalar Array3 form (std::max then
+// std::min: NaN -> -1).
+// ------------------------------------------------------------------------------------------
+MM_HD float clamp_unit_(float v, bool arr) {
+  if (arr) {
+    v = (1.0f < v) ? 1.0f : v;    // std::min(v, 1)
+    v = (v < -1.0f) ? -1.0f : v;  // std::max(v, -1)
+    return v;
+  }
+  float w = (-1.0f < v) ? v : -1.0f;  // std::max(-1, v)
+  return (w < 1.0f) ? w : 1.0f;       // std::min(1, w)
+}
+
+// cartesianToSpherical (Coordinate.cpp:32-38 array / :40-45 scalar): returns R, theta, phi
+MM_HD V3 cart_to_sph(V3 p, Math m, bool arr) {
+  float R = m.sqrt((p.x * p.x + p.y * p.y) + p.z * p.z);
+  float th = g_acosf(clamp_unit_(p.z / R, arr));
+  float ph = g_atan2f(p.y, p.x);
+  return {R, th, ph};
+}
+
+// sphericalToCartesian with explicit R (Coordinate.cpp:47-53)
+MM_HD V3 sph_to_cart(float R, float th, float ph, Math m) {
+  float st = m.sin(th);
+  return {(R * st) * m.cos(ph), (R * st) * m.sin(ph), R * m.cos(th)};
+}
+
+// ------------------------------------------------------------------------------------------
+// EquirectangularProjection (Projection.cpp:213-249 in SURVEY numbering; pixelOffset = 0)
+// ------------------------------------------------------------------------------------------
+MM_HD V3 erp_to_sphere(float x, float y, const SeqConst& s, Math m) {
+  float phi = ((-((x + 0.0f) / s.Wf)) * 2.0f) * PI_F;
+  float theta = ((y + 0.0f) / s.Hf) * PI_F;
+  return sph_to_cart(1.0f, theta, phi, m);
+}
+
+MM_HD void erp_from_sphere(V3 p, const SeqConst& s, Math m, bool arr, float* ox, float* oy) {
+  V3 sp = cart_to_sph(p, m, arr);
+  float phi = sp.z > 0.0f ? sp.z - TWO_PI_F : sp.z;
+  *ox = ((-(phi / TWO_PI_F)) * s.Wf) - 0.0f;
+  *oy = ((sp.y / PI_F) * s.Hf) - 0.0f;
+}
+
+// ------------------------------------------------------------------------------------------
+// PerspectiveProjection, optical centre (0,0) (Projection.cpp:119-211 in SURVEY numbering)
+// ------------------------------------------------------------------------------------------
+MM_HD void persp_from_sphere(V3 s3, float f, Math m, float* ox, float* oy, bool* vip) {
+  V3 rot = {s3.y, -s3.z, -s3.x};
+  V3 sp = cart_to_sph(rot, m, true);
+  float polarR = f * g_tanf(sp.y);
+  *ox = polarR * m.cos(sp.z) + 0.0f;
+  *oy = polarR * m.sin(sp.z) + 0.0f;
+  *vip = polarR < 0.0f;
+}
+
+MM_HD V3 persp_to_sphere(float x, float y, bool vip, float f, Math m) {
+  x = x - 0.0f;
+  y = y - 0.0f;
+  float r = m.sqrt(x * x + y * y);
+  float phi = g_atan2f(y, x);
+  float theta = g_atanf(r / f);
+  float v = vip ? 1.0f : 0.0f;
+  theta = theta - v * (2.0f * theta - PI_F);
+  phi = phi - v * PI_F;
+  V3 c = sph_to_cart(1.0f, theta, phi, m);
+  return {-c.z, c.x, -c.y};
+}
+
+// MotionPlaneAdaptiveMotionModel::toPerspective (array, MotionPlaneAdaptiveMotionModel.cpp:111-135)
+MM_HD void mpa_to_perspective(int plane, float gx, float gy, const SeqConst& s, Math m, float* px,
+                              float* py, bool* vip) {
+  V3 sph = erp_to_sphere(gx, gy, s, m);
+  V3 q;
+  if (plane == MPA_FRONT_BACK)
+    q = sph;
+  else if (plane == MPA_LEFT_RIGHT)
+    q = {sph.y, -sph.x, sph.z};
+  else
+    q = {-sph.z, sph.y, sph.x};
+  persp_from_sphere(q, s.focal, m, px, py, vip);
+}
+
+// MotionPlaneAdaptiveMotionModel::toProjection (array, MotionPlaneAdaptiveMotionModel.cpp:163-187)
+MM_HD void mpa_to_projection(int plane, float px, float py, bool vip, const SeqConst& s, Math m,
+                             float* ox, float* oy) {
+  V3 q = persp_to_sphere(px, py, vip, s.focal, m);
+  V3 sph;
+  if (plane == MPA_FRONT_BACK)
+    sph = q;
+  else if (plane == MPA_LEFT_RIGHT)
+    sph = {-q.y, q.x, q.z};
+  else
+    sph = {q.z, q.y, -q.x};
+  erp_from_sphere(sph, s, m, true, ox, oy);
+}
+
+// ------------------------------------------------------------------------------------------
+// 3x3 products: Eigen 3.3.7 lazy coefficient-based product, coefficient = p0 + (p1 + p2)
+// (redux_novec_unroller halves).  Row-major storage m[3*i + j].
+// ------------------------------------------------------------------------------------------
+struct M3 {
+  float m[9];
+};
+MM_HD float dot3_(float a0, float b0, float a1, float b1, float a2, float b2) {
+  return a0 * b0 + (a1 * b1 + a2 * b2);
+}
+MM_HD M3 mat_mul(const M3& A, const M3& B) {
+  M3 C;
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++)
+      C.m[3 * i + j] = dot3_(A.m[3 * i], B.m[j], A.m[3 * i + 1], B.m[3 + j], A.m[3 * i + 2], B.m[6 + j]);
+  return C;
+}
+MM_HD V3 mat_vec(const M3& A, V3 v) {
+  return {dot3_(A.m[0], v.x, A.m[1], v.y, A.m[2], v.z), dot3_(A.m[3], v.x, A.m[4], v.y, A.m[5], v.z),
+          dot3_(A.m[6], v.x, A.m[7], v.y, A.m[8], v.z)};
+}
+MM_HD V3 matT_vec(const M3& A, V3 v) {
+  return {dot3_(A.m[0], v.x, A.m[3], v.y, A.m[6], v.z), dot3_(A.m[1], v.x, A.m[4], v.y, A.m[7], v.z),
+          dot3_(A.m[2], v.x, A.m[5], v.y, A.m[8], v.z)};
+}
+MM_HD M3 mat_transpose(const M3& A) {
+  return {{A.m[0], A.m[3], A.m[6], A.m[1], A.m[4], A.m[7], A.m[2], A.m[5], A.m[8]}};
+}
+
+// Eigen 3.3.7 AngleAxis<float>::toRotationMatrix (Geometry/AngleAxis.h), axis given exactly
+MM_HD M3 angle_axis(float angle, float ax, float ay, float az) {
+  float s = g_sinf(angle), c = g_cosf(angle);
+  float sx = s * ax, sy = s * ay, sz = s * az;
+  float omc = 1.0f - c;
+  float cx = omc * ax, cy = omc * ay, cz = omc * az;
+  M3 r;
+  float tmp = cx * ay;
+  r.m[1] = tmp - sz;
+  r.m[3] = tmp + sz;
+  tmp = cx * az;
+  r.m[2] = tmp + sy;
+  r.m[6] = tmp - sy;
+  tmp = cy * az;
+  r.m[5] = tmp - sx;
+  r.m[7] = tmp + sx;
+  r.m[0] = cx * ax + c;
+  r.m[4] = cy * ay + c;
+  r.m[8] = cz * az + c;
+  return r;
+}
+
+// GeodesicMotionModel::setEpipole (GeodesicMotionModel.cpp:14-46)
+MM_HD M3 ged_rotation(V3 e) {
+  float n = sqrtf_((e.x * e.x + e.y * e.y) + e.z * e.z);
+  V3 pa = {e.x / n, e.y / n, e.z / n};
+  V3 cr = {-pa.y, pa.x, 0.0f};
+  float s = sqrtf_((cr.x * cr.x + cr.y * cr.y) + cr.z * cr.z);
+  M3 R;
+  if (s == 0.0f) {
+    R = {{1, 0, 0, 0, 1, 0, 0, 0, 1}};
+    if (pa.z < 0.0f) R.m[8] = -1.0f;
+    return R;
+  }
+  float zmin = (pa.z < 1.0f) ? pa.z : 1.0f;         // std::min(TCoord(1), z)
+  float c = (-1.0f < zmin) ? zmin : -1.0f;           // std::max(TCoord(-1), .)
+  M3 K = {{0.0f, -cr.z, cr.y, cr.z, 0.0f, -cr.x, -cr.y, cr.x, 0.0f}};
+  M3 K2 = mat_mul(K, K);
+  float f = (1.0f - c) / (s * s);
+  for (int i = 0; i < 9; i++) {
+    float I = (i == 0 || i == 4 || i == 8) ? 1.0f : 0.0f;
+    R.m[i] = (I + K.m[i]) + K2.m[i] * f;
+  }
+  return mat_transpose(R);
+}
+
+// EpipoleList::findEpipole -> FloatingFixedConversion::fixedToFloating(.., 24) (Coordinate.cpp:76-80)
+MM_HD float fixed_to_float(int32_t v, int prec) {
+  return (float)(v >> prec) + (float)(v & ((1 << prec) - 1)) / (float)(1 << prec);
+}
+
+// ------------------------------------------------------------------------------------------
+// Per-block (per PU x list x component) setup: everything the reference computes once per
+// reprojectMotionVectorSubblocks call, before the per-element arrays.
+// ------------------------------------------------------------------------------------------
+struct BlockSetup {
+  int model;
+  int identity;   // model returns the input grid unchanged (zero-MV shortcut)
+  float mvx, mvy;  // motion vector as float (MVReprojection.cpp:123-124)
+  float cx, cy;    // block centre in component units (MVReprojection.cpp:133)
+  M3 M;            // GED rotation (setEpipole) or ROT rotationMatrixReally
+  float k;         // GED MODULATED parameter
+  float sE, cE, alphaC;  // TAN centre terms
+  float d0, d1, d2;      // 3DT motion vector in 3D
+};
+
+MM_HD float mv_to_float(int32_t v) { return (float)(v >> 4) + (float)(v & 15) / 16.0f; }
+
+MM_HD void block_setup(BlockSetup* b, const SeqConst& s, int model, bool luma, int pos_x, int pos_y,
+                       int size_w, int size_h, int32_t mv_hor, int32_t mv_ver, const M3* ged_rot) {
+  b->model = model;
+  b->mvx = mv_to_float(mv_hor);
+  b->mvy = mv_to_float(mv_ver);
+  b->cx = (float)pos_x + ((float)size_w - 1.0f) / 2.0f;
+  b->cy = (float)pos_y + ((float)size_h - 1.0f) / 2.0f;
+  b->identity = 0;
+  b->k = 0.0f;
+  b->sE = b->cE = b->alphaC = 0.0f;
+  b->d0 = b->d1 = b->d2 = 0.0f;
+  for (int i = 0; i < 9; i++) b->M.m[i] = 0.0f;
+  const bool zero = (b->mvx == 0.0f && b->mvy == 0.0f);
+  const Math sc{false};
+  switch (model) {
+    case MPA_FRONT_BACK:
+    case MPA_LEFT_RIGHT:
+    case MPA_TOP_BOTTOM:
+      break;  // no shortcut, no per-block constants
+    case TANGENTIAL: {  // TangentialMotionModel.cpp:8-48
+      if (zero) { b->identity = 1; break; }
+      V3 c3 = erp_to_sphere(b->cx, b->cy, s, sc);
+      V3 sp = cart_to_sph(c3, sc, false);
+      float epsC = (float)(PI_2_D - (double)sp.y);
+      b->alphaC = sp.z;
+      b->sE = sinf_via_double(epsC);   // unqualified sin(float) -> double ::sin
+      b->cE = cosf_via_double(epsC);
+    } break;
+    case THREE_D_TRANSLATIONAL: {  // ThreeDTranslationalMotionModel.cpp:7-24
+      if (zero) { b->identity = 1; break; }
+      V3 c = erp_to_sphere(b->cx, b->cy, s, sc);
+      V3 cm = erp_to_sphere(b->cx + b->mvx, b->cy + b->mvy, s, sc);
+      b->d0 = cm.x - c.x;
+      b->d1 = cm.y - c.y;
+      b->d2 = cm.z - c.z;
+    } break;
+    case ROTATIONAL: {  // RotationalMotionModel.cpp:8-78
+      if (zero) { b->identity = 1; break; }
+      V3 sp = cart_to_sph(erp_to_sphere(b->cx, b->cy, s, sc), sc, false);
+      M3 rot = mat_mul(angle_axis(-b->mvx * s.res, 0.0f, 0.0f, 1.0f),
+                       angle_axis(b->mvy * s.res, 0.0f, 1.0f, 0.0f));
+      M3 unrotPhi = angle_axis(-sp.z, 0.0f, 0.0f, 1.0f);
+      M3 unrotTheta = angle_axis((float)(PI_2_D - (double)sp.y), 0.0f, 1.0f, 0.0f);
+      M3 unrot = mat_mul(unrotTheta, unrotPhi);
+      M3 unrotT = mat_transpose(unrot);
+      b->M = mat_mul(unrotT, mat_mul(rot, unrot));
+    } break;
+    case GEODESIC_X:
+    case GEODESIC_Y:
+    case GEODESIC_Z:
+    case GEODESIC_CAMPOSE: {  // GeodesicMotionModel.cpp:101-176
+      b->M = *ged_rot;
+      if (!luma && zero) { b->identity = 1; break; }  // only modelMotion shortcuts (:130-132)
+      if (s.ged_flavor == 1) {
+        V3 c3 = erp_to_sphere(b->cx, b->cy, s, sc);
+        V3 cr = mat_vec(b->M, c3);
+        V3 sp = cart_to_sph(cr, sc, false);
+        float rm = s.res * b->mvx;
+        b->k = g_sinf(sp.y + rm) / g_sinf(rm);
+      }
+    } break;
+    default:
+      break;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// One element of <Model>::modelMotion[Cached] followed by the NaN fallback and fixed-point
+// rounding of reprojectMotionVectorSubblocks (MVReprojection.cpp:147-164).
+//   gx, gy   : the element's grid coordinate (luma-scaled, incl. the 4x4 offset)
+//   packet   : Eigen packet lane for this element within its block (N >= 4, index < N - N%4)
+//   pers*    : MPA luma only -- the frame-cache perspective coordinates of this element
+//   chroma_shift : 0 for luma, 1 for 4:2:0 chroma; fixed precision = 4 + chroma_shift bits
+// ------------------------------------------------------------------------------------------
+MM_HD void reproject_element(const SeqConst& s, const BlockSetup& b, float gx, float gy, bool packet,
+                             bool mpa_cached, float pers_x, float pers_y, bool pers_vip,
+                             int chroma_shift, int32_t* fx, int32_t* fy) {
+  const Math m{packet};
+  float mx = gx, my = gy;
+  if (!b.identity) {
+    switch (b.model) {
+      case MPA_FRONT_BACK:
+      case MPA_LEFT_RIGHT:
+      case MPA_TOP_BOTTOM: {
+        float px, py;
+        bool vip;
+        if (mpa_cached) {
+          px = pers_x;
+          py = pers_y;
+          vip = pers_vip;
+        } else {
+          mpa_to_perspective(b.model, gx, gy, s, m, &px, &py, &vip);
+        }
+        float sign = vip ? -1.0f : 1.0f;
+        px = px + b.mvx * sign;
+        py = py + b.mvy * sign;
+        mpa_to_projection(b.model, px, py, vip, s, m, &mx, &my);
+      } break;
+      case TANGENTIAL: {
+        V3 p = erp_to_sphere(gx, gy, s, m);
+        V3 sp = cart_to_sph(p, m, true);
+        float eps = PI_2_F - sp.y;
+        float alpha = sp.z;
+        float dA = alpha - b.alphaC;
+        float se = m.sin(eps), ce = m.cos(eps), cdA = m.cos(dA);
+        float cosPsi = b.sE * se + (b.cE * ce) * cdA;
+        float yP = (se * b.cE - (b.sE * ce) * cdA) / cosPsi;
+        float xP = (m.sin(dA) * ce) / cosPsi;
+        float yM = yP - b.mvy * s.res;
+        float xM = xP - b.mvx * s.res;
+        float rho = m.sqrt(xM * xM + yM * yM);
+        float eta = g_atanf(rho);
+        float gamma = (rho * b.cE) * m.cos(eta) - (yM * b.sE) * m.sin(eta);
+        float alphaM = b.alphaC + g_atanf((xM * g_sinf(eta)) / gamma);
+        float epsM = g_asinf(g_cosf(eta) * b.sE + ((yM * g_sinf(eta)) * b.cE) / rho);
+        V3 c = sph_to_cart(1.0f, PI_2_F - epsM, alphaM, m);
+        erp_from_sphere(c, s, m, true, &mx, &my);
+      } break;
+      case THREE_D_TRANSLATIONAL: {
+        V3 p = erp_to_sphere(gx, gy, s, m);
+        V3 q = {p.x + b.d0, p.y + b.d1, p.z + b.d2};
+        erp_from_sphere(q, s, m, true, &mx, &my);
+      } break;
+      case ROTATIONAL: {
+        V3 p = erp_to_sphere(gx, gy, s, m);
+        V3 q = mat_vec(b.M, p);
+        erp_from_sphere(q, s, m, true, &mx, &my);
+      } break;
+      case GEODESIC_X:
+      case GEODESIC_Y:
+      case GEODESIC_Z:
+      case GEODESIC_CAMPOSE: {
+        V3 p = erp_to_sphere(gx, gy, s, m);
+        V3 q = mat_vec(b.M, p);
+        V3 sp = cart_to_sph(q, m, true);
+        float th;
+        if (s.ged_flavor == 1)
+          th = sp.y + g_atanf(g_sinf(sp.y) / (b.k - g_cosf(sp.y)));
+        else
+          th = sp.y + s.res * b.mvx;
+        float ph = sp.z + s.res * b.mvy;
+        V3 c = sph_to_cart(sp.x, th, ph, m);
+        V3 r = matT_vec(b.M, c);
+        erp_from_sphere(r, s, m, true, &mx, &my);
+      } break;
+      default:
+        break;
+    }
+  }
+  // NaN -> unmoved (MVReprojection.cpp:151-154), remove offset, rescale, round to fixed point
+  if (isnanf_(mx) || isnanf_(my)) {
+    mx = gx;
+    my = gy;
+  }
+  mx = mx - s.off;
+  my = my - s.off;
+  if (chroma_shift) {
+    mx = mx / 2.0f;
+    my = my / 2.0f;
+  }
+  const float scale = (float)(1 << (4 + chroma_shift));
+  float rx = roundf_(mx * scale), ry = roundf_(my * scale);
+  // cast<int>: x86 cvttss2si semantics for out-of-range values
+  *fx = (fabsf_(rx) < 2147483648.0f) ? (int32_t)rx : (int32_t)0x80000000u;
+  *fy = (fabsf_(ry) < 2147483648.0f) ? (int32_t)ry : (int32_t)0x80000000u;
+}
+
+}  // namespace mmmod

@@ -1,0 +1,187 @@
+// mm_pipeline.h -- work descriptors and per-thread bodies of the MC pipeline (host + device).
+//
+// The HIP kernels in mm_kernels.hip are one-line wrappers around these bodies; the CPU twin
+// used by the CPU test suite (tests/native/host_twin.cpp) loops over the same bodies, so the
+// device logic is exercised bit-for-bit on the host before it ever reaches a GPU.
+#pragma once
+#include "mm_filter.h"
+#include "mm_models.h"
+
+namespace mmpipe {
+using namespace mmmod;
+using namespace mmflt;
+
+struct RefDev {
+  const int16_t* y;
+  const int16_t* cb;
+  const int16_t* cr;
+  int stride_y, stride_c;
+};
+
+// One reprojection job == one reprojectMotionVectorSubblocks call
+struct JobDev {
+  int x, y;    // block position in LUMA units (grid origin)
+  int cw, ch;  // block size in component units
+  int comp;    // 0 luma, 1 chroma (4:2:0)
+  int model;
+  int mv_hor, mv_ver;
+  int ged_idx;  // index into the GED rotation table (-1 if not GED)
+  int n;        // elements = (cw/sbw)*(ch/sbh)
+  int rows;     // ch/sbh (Eigen column-major rows)
+  int offset;   // first element in the result array
+};
+
+struct PuDev {
+  int x, y, w, h;
+  int ref_slot[2];  // -1 = list unused
+  int job[2][2];    // [list][comp] -> job index
+  int sb_offset;    // first luma sub-block of this PU in the k_mc enumeration
+};
+
+struct MpaCache {
+  const float* px[3];
+  const float* py[3];
+  const uint8_t* vip[3];
+  int cols, rows;  // W/4, H/4
+};
+
+struct Geometry {
+  int W, H, Wc, Hc;
+  int maxCUw, maxCUh, maxCUwc, maxCUhc;
+  int bd;
+  int chroma;  // 1 = 4:2:0
+};
+
+struct Taps {
+  const int8_t (*luma)[8];
+  const int8_t (*chroma)[4];
+};
+
+// item containing flat index g: chunk_start[g/64] is the item holding g rounded down to 64
+MM_HD int find_item(const int* offsets, const int* chunk_start, int g, int n_items) {
+  int j = chunk_start[g >> 6];
+  while (j + 1 < n_items && offsets[j + 1] <= g) j++;
+  return j;
+}
+
+// MotionPlaneAdaptiveMotionModel::fillCache on MVReprojection::fillCache's frame grid; storage
+// row-major [j][i], Eigen column-major index i*rows + j decides packet vs tail.
+MM_HD void mpa_cache_thread(int t, const SeqConst& sc, int plane, int cols, int rows, float* px, float* py,
+                            uint8_t* vip) {
+  const int n = cols * rows;
+  int j = t / cols, i = t % cols;
+  int eig = i * rows + j;
+  float gx = 4.0f * (float)i + sc.off, gy = 4.0f * (float)j + sc.off;
+  float x, y;
+  bool v;
+  mpa_to_perspective(plane, gx, gy, sc, Math{packet_lane(eig, n)}, &x, &y, &v);
+  px[t] = x;
+  py[t] = y;
+  vip[t] = v ? 1 : 0;
+}
+
+MM_HD void setup_thread(int t, const SeqConst& sc, const JobDev* jobs, const M3* ged, BlockSetup* out) {
+  const JobDev j = jobs[t];
+  const int cs = j.comp ? 1 : 0;
+  block_setup(&out[t], sc, j.model, j.comp == 0, j.x >> cs, j.y >> cs, j.cw, j.ch, j.mv_hor, j.mv_ver,
+              j.ged_idx >= 0 ? &ged[j.ged_idx] : nullptr);
+}
+
+MM_HD void reproj_thread(int g, const SeqConst& sc, const JobDev* jobs, int n_jobs, const int* job_offsets,
+                         const int* chunk_start, const BlockSetup* setups, const MpaCache& cache, int32_t* out_xy) {
+  const int ji = find_item(job_offsets, chunk_start, g, n_jobs);
+  const JobDev& j = jobs[ji];
+  const int local = g - j.offset;
+  const int col = local / j.rows, row = local - col * j.rows;
+  // grid: luma frame grid (4i + off) or chroma LinSpaced (2*xc + off + 4i) -- the same values
+  const float gx = (float)(j.x + 4 * col) + sc.off;
+  const float gy = (float)(j.y + 4 * row) + sc.off;
+  const bool mpa_cached = (j.comp == 0) && (j.model >= MPA_FRONT_BACK && j.model <= MPA_TOP_BOTTOM);
+  float px = 0.0f, py = 0.0f;
+  bool vip = false;
+  if (mpa_cached) {
+    const int ci = ((j.y >> 2) + row) * cache.cols + (j.x >> 2) + col;
+    const int pl = j.model - MPA_FRONT_BACK;
+    px = cache.px[pl][ci];
+    py = cache.py[pl][ci];
+    vip = cache.vip[pl][ci] != 0;
+  }
+  int32_t fx, fy;
+  reproject_element(sc, setups[ji], gx, gy, packet_lane(local, j.n), mpa_cached, px, py, vip, j.comp ? 1 : 0, &fx,
+                    &fy);
+  out_xy[2 * g] = fx;
+  out_xy[2 * g + 1] = fy;
+}
+
+// One luma 4x4 sub-block (and its two 4:2:0 chroma 2x2 sub-blocks) of one PU: both lists,
+// xPredInterBlkMM's per-sub-block dispatch (InterPrediction.cpp:776-828), then addAvg (bi) or the
+// rndRes uni prediction (xWeightedAverage, InterPrediction.cpp:1584-1679).
+MM_HD void mc_thread(int g, const Geometry& geo, const Taps& taps, const PuDev* pus, int n_pus,
+                     const int* pu_offsets, const int* chunk_start, const JobDev* jobs, const int32_t* reproj,
+                     const RefDev* refs, int16_t* dst_y, int dsy, int16_t* dst_cb, int16_t* dst_cr, int dsc) {
+  const int pi = find_item(pu_offsets, chunk_start, g, n_pus);
+  const PuDev pu = pus[pi];
+  const int local = g - pu.sb_offset;
+  const int rows = pu.h >> 2;
+  const int col = local / rows, row = local - col * rows;
+  const bool bi = pu.ref_slot[0] >= 0 && pu.ref_slot[1] >= 0;
+  const int uni_list = pu.ref_slot[0] >= 0 ? 0 : 1;
+
+  // ---- luma 4x4 ----
+  int16_t pl[2][16];
+  for (int l = 0; l < 2; l++) {
+    if (pu.ref_slot[l] < 0) continue;
+    const JobDev& j = jobs[pu.job[l][0]];
+    const int32_t fx = reproj[2 * (j.offset + local)], fy = reproj[2 * (j.offset + local) + 1];
+    const int xPos = fx >> 4, yPos = fy >> 4, xFrac = fx & 15, yFrac = fy & 15;
+    const RefDev r = refs[pu.ref_slot[l]];
+    if (sb_out_of_range(xPos, yPos, geo.W, geo.H, geo.maxCUw, geo.maxCUh, 4, 4)) {
+      for (int i = 0; i < 16; i++) pl[l][i] = 0;
+    } else {
+      predict_subblock<8, 4, 4>(r.y, r.stride_y, geo.W, geo.H, xPos, yPos, xFrac, yFrac, taps.luma[xFrac],
+                                taps.luma[yFrac], bi, geo.bd, pl[l]);
+    }
+  }
+  {
+    const int ox = pu.x + 4 * col, oy = pu.y + 4 * row;
+    for (int r = 0; r < 4; r++) {
+      int16_t* d = dst_y + (long)(oy + r) * dsy + ox;
+      for (int c = 0; c < 4; c++) {
+        const int i = r * 4 + c;
+        d[c] = bi ? add_avg(pl[0][i], pl[1][i], geo.bd) : pl[uni_list][i];
+      }
+    }
+  }
+  if (!geo.chroma) return;
+  // ---- chroma 2x2 (Cb and Cr share one reprojection) ----
+  int16_t pcb[2][4], pcr[2][4];
+  for (int l = 0; l < 2; l++) {
+    if (pu.ref_slot[l] < 0) continue;
+    const JobDev& j = jobs[pu.job[l][1]];
+    const int32_t fx = reproj[2 * (j.offset + local)], fy = reproj[2 * (j.offset + local) + 1];
+    const int xPos = fx >> 5, yPos = fy >> 5, xFrac = fx & 31, yFrac = fy & 31;
+    const RefDev r = refs[pu.ref_slot[l]];
+    if (sb_out_of_range(xPos, yPos, geo.Wc, geo.Hc, geo.maxCUwc, geo.maxCUhc, 2, 2)) {
+      for (int i = 0; i < 4; i++) pcb[l][i] = pcr[l][i] = 0;
+    } else {
+      predict_subblock<4, 2, 2>(r.cb, r.stride_c, geo.Wc, geo.Hc, xPos, yPos, xFrac, yFrac, taps.chroma[xFrac],
+                                taps.chroma[yFrac], bi, geo.bd, pcb[l]);
+      predict_subblock<4, 2, 2>(r.cr, r.stride_c, geo.Wc, geo.Hc, xPos, yPos, xFrac, yFrac, taps.chroma[xFrac],
+                                taps.chroma[yFrac], bi, geo.bd, pcr[l]);
+    }
+  }
+  {
+    const int ox = (pu.x >> 1) + 2 * col, oy = (pu.y >> 1) + 2 * row;
+    for (int r = 0; r < 2; r++) {
+      int16_t* db = dst_cb + (long)(oy + r) * dsc + ox;
+      int16_t* dr = dst_cr + (long)(oy + r) * dsc + ox;
+      for (int c = 0; c < 2; c++) {
+        const int i = r * 2 + c;
+        db[c] = bi ? add_avg(pcb[0][i], pcb[1][i], geo.bd) : pcb[uni_list][i];
+        dr[c] = bi ? add_avg(pcr[0][i], pcr[1][i], geo.bd) : pcr[uni_list][i];
+      }
+    }
+  }
+}
+
+}  // namespace mmpipe

@@ -1,0 +1,274 @@
+"""Python host interface of the MI355X 360-degree multi-model motion-compensation path.
+
+Mirrors the reference's C++ call surface for this path:
+
+    MVReprojection::init                          -> MMContext(...)          (mm_create)
+    EpipoleList::addEpipole                       -> MMContext.set_epipole   (mm_set_epipole)
+    Picture reconstruction planes                 -> MMContext.upload_ref    (mm_upload_ref)
+    MVReprojection::reprojectMotionVectorSubblocks-> MMContext.reproject_motion_vector_subblocks
+    InterPrediction::xPredInterBlkMM (+ addAvg)   -> MMContext.predict       (mm_pred)
+    InterpolationFilter::filterHor / filterVer    -> MMContext.filter_hor / filter_ver
+
+Everything runs through the HIP C-ABI library ``lib/libmm360.so`` (include/mm360.h).  There is
+no CPU fallback: constructing a context without the library or without a GPU raises.
+Reference citations are into /root/reference/source/Lib/CommonLib.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, byref, c_int, c_int32, c_uint32, c_void_p, c_float
+from typing import Optional, Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libmm360.so")
+
+# MotionModelID (TypeDef.h:865-879)
+CLASSIC, MPA_FRONT_BACK, MPA_LEFT_RIGHT, MPA_TOP_BOTTOM = 0, 1, 2, 3
+TANGENTIAL, THREE_D_TRANSLATIONAL, ROTATIONAL = 4, 5, 6
+GEODESIC_X, GEODESIC_Y, GEODESIC_Z, GEODESIC_CAMPOSE = 7, 8, 9, 10
+MODEL_NAMES = {
+    CLASSIC: "CLASSIC", MPA_FRONT_BACK: "MPA_FRONT_BACK", MPA_LEFT_RIGHT: "MPA_LEFT_RIGHT",
+    MPA_TOP_BOTTOM: "MPA_TOP_BOTTOM", TANGENTIAL: "TANGENTIAL",
+    THREE_D_TRANSLATIONAL: "THREE_D_TRANSLATIONAL", ROTATIONAL: "ROTATIONAL",
+    GEODESIC_X: "GEODESIC_X", GEODESIC_Y: "GEODESIC_Y", GEODESIC_Z: "GEODESIC_Z",
+    GEODESIC_CAMPOSE: "GEODESIC_CAMPOSE",
+}
+
+MM_OK, MM_ERR_ARG, MM_ERR_HIP, MM_ERR_NOREF, MM_ERR_NOEPIPOLE, MM_ERR_MODEL, MM_ERR_NODEV = range(7)
+ERROR_NAMES = {
+    MM_ERR_ARG: "MM_ERR_ARG", MM_ERR_HIP: "MM_ERR_HIP", MM_ERR_NOREF: "MM_ERR_NOREF",
+    MM_ERR_NOEPIPOLE: "MM_ERR_NOEPIPOLE", MM_ERR_MODEL: "MM_ERR_MODEL", MM_ERR_NODEV: "MM_ERR_NODEV",
+}
+
+# Every entry point declared in include/mm360.h (checked by the CPU test suite)
+EXPORTED_SYMBOLS = (
+    "mm_create", "mm_destroy", "mm_set_stream", "mm_synchronize", "mm_last_error", "mm_get_version",
+    "mm_set_epipole", "mm_upload_ref", "mm_release_ref", "mm_reproject", "mm_pred",
+    "mm_pred_prepare", "mm_pred_run", "mm_filter", "mm_last_timing",
+)
+
+
+class MMError(RuntimeError):
+    """Status != MM_OK from the C-ABI (the reference would throw from CHECK, TypeDef.h:1120-1148)."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{ERROR_NAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+class SeqParams(ctypes.Structure):
+    _fields_ = [
+        ("width", c_int32), ("height", c_int32), ("chroma_format", c_int32), ("bit_depth", c_int32),
+        ("max_cu_width", c_int32), ("max_cu_height", c_int32), ("mm_offset4x4", c_int32),
+        ("ged_flavor", c_int32), ("active_models", c_uint32),
+    ]
+
+
+# numpy views of mm_block_desc / mm_pu_desc (all int32, packed)
+BLOCK_DTYPE = np.dtype([("x", "<i4"), ("y", "<i4"), ("w", "<i4"), ("h", "<i4"), ("mv_hor", "<i4"),
+                        ("mv_ver", "<i4"), ("model", "<i4"), ("comp", "<i4"), ("cur_poc", "<i4"),
+                        ("ref_poc", "<i4")])
+PU_DTYPE = np.dtype([("x", "<i4"), ("y", "<i4"), ("w", "<i4"), ("h", "<i4"), ("mv", "<i4", (2, 2)),
+                     ("ref_poc", "<i4", (2,)), ("model", "<i4", (2,))])
+assert BLOCK_DTYPE.itemsize == 40 and PU_DTYPE.itemsize == 48
+
+
+def active_mask(models: Sequence[int]) -> int:
+    """MMConfig active-model list as a bit mask; CLASSIC is always active (MMConfig.cpp:7-39)."""
+    m = 1 << CLASSIC
+    for x in models:
+        m |= 1 << int(x)
+    return m
+
+
+def seq_params(width: int, height: int, models: Sequence[int], chroma_format: int = 1,
+               bit_depth: int = 10, max_cu: int = 128, mm_offset4x4: int = 1,
+               ged_flavor: int = 1) -> SeqParams:
+    """Defaults are the reference's hard-coded MM settings (EncApp.cpp:754-768) and RA cfg."""
+    return SeqParams(width, height, chroma_format, bit_depth, max_cu, max_cu, mm_offset4x4,
+                     ged_flavor, active_mask(models))
+
+
+_lib = None
+
+
+def load_library() -> ctypes.CDLL:
+    """Load the HIP library; raise if it has not been built (no fallback path exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise FileNotFoundError(f"{LIB_PATH} missing: build it with `make -C vvc-extension-mm_amd` "
+                                "or __graft_entry__.build()")
+    lib = ctypes.CDLL(LIB_PATH)
+    vp = c_void_p
+    sig = {
+        "mm_create": (c_int, [POINTER(SeqParams), c_int, POINTER(vp)]),
+        "mm_destroy": (c_int, [vp]),
+        "mm_set_stream": (c_int, [vp, vp]),
+        "mm_synchronize": (c_int, [vp]),
+        "mm_last_error": (ctypes.c_char_p, [vp]),
+        "mm_get_version": (c_int, []),
+        "mm_set_epipole": (c_int, [vp, c_int, c_int, POINTER(c_int32)]),
+        "mm_upload_ref": (c_int, [vp, c_int, vp, ctypes.c_ssize_t, vp, vp, ctypes.c_ssize_t, c_int]),
+        "mm_release_ref": (c_int, [vp, c_int]),
+        "mm_reproject": (c_int, [vp, vp, c_int, vp]),
+        "mm_pred": (c_int, [vp, c_int, vp, c_int, vp, ctypes.c_ssize_t, vp, vp, ctypes.c_ssize_t]),
+        "mm_pred_prepare": (c_int, [vp, c_int, vp, c_int]),
+        "mm_pred_run": (c_int, [vp, vp, ctypes.c_ssize_t, vp, vp, ctypes.c_ssize_t]),
+        "mm_filter": (c_int, [vp, c_int, c_int, vp, ctypes.c_ssize_t, vp, ctypes.c_ssize_t, c_int, c_int,
+                              c_int, c_int, c_int]),
+        "mm_last_timing": (c_int, [vp, POINTER(c_float)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _ptr(a) -> int:
+    """Address of a numpy array or a torch tensor (host or device)."""
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    return int(a.data_ptr())
+
+
+def _is_device(a) -> bool:
+    return not isinstance(a, np.ndarray) and getattr(a, "is_cuda", False)
+
+
+def subblock_count(w: int, h: int, comp: int) -> int:
+    sb = 2 if comp else 4
+    return (w // sb) * (h // sb)
+
+
+class MMContext:
+    """One decoder instance's MM motion-compensation context on one GPU."""
+
+    def __init__(self, params: SeqParams, device: int = 0):
+        self.lib = load_library()
+        self.params = params
+        h = c_void_p()
+        rc = self.lib.mm_create(byref(params), device, byref(h))
+        if rc != MM_OK:
+            raise MMError(rc, "mm_create failed (no HIP device, or invalid parameters)")
+        self.h = h
+        self.device = device
+
+    # -- lifecycle ---------------------------------------------------------------------------
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.mm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, rc: int):
+        if rc != MM_OK:
+            msg = self.lib.mm_last_error(self.h)
+            raise MMError(rc, msg.decode() if msg else "")
+
+    def set_stream(self, stream_handle: int):
+        self._check(self.lib.mm_set_stream(self.h, c_void_p(stream_handle)))
+
+    def synchronize(self):
+        self._check(self.lib.mm_synchronize(self.h))
+
+    # -- EpipoleList -------------------------------------------------------------------------
+    def set_epipole(self, cur_poc: int, ref_poc: int, q24: Sequence[int]):
+        arr = (c_int32 * 3)(*[int(v) for v in q24])
+        self._check(self.lib.mm_set_epipole(self.h, cur_poc, ref_poc, arr))
+
+    # -- reference pictures ------------------------------------------------------------------
+    def upload_ref(self, poc: int, y, cb=None, cr=None):
+        """Planes: 2-D int16 numpy arrays (host) or torch int16 CUDA tensors (device)."""
+        dev = _is_device(y)
+        sy = y.strides[0] // 2 if isinstance(y, np.ndarray) else y.stride(0)
+        sc = 0
+        if cb is not None:
+            sc = cb.strides[0] // 2 if isinstance(cb, np.ndarray) else cb.stride(0)
+        self._check(self.lib.mm_upload_ref(self.h, poc, c_void_p(_ptr(y)), sy,
+                                           c_void_p(_ptr(cb)) if cb is not None else None,
+                                           c_void_p(_ptr(cr)) if cr is not None else None, sc, int(dev)))
+
+    def release_ref(self, poc: int):
+        self._check(self.lib.mm_release_ref(self.h, poc))
+
+    # -- MVReprojection ----------------------------------------------------------------------
+    def reproject(self, blocks: np.ndarray) -> np.ndarray:
+        """Batched reprojectMotionVectorSubblocks: BLOCK_DTYPE array -> int32 [sum N_b, 2]."""
+        blocks = np.ascontiguousarray(blocks, dtype=BLOCK_DTYPE)
+        total = int(sum(subblock_count(int(b["w"]), int(b["h"]), int(b["comp"])) for b in blocks))
+        out = np.zeros((max(total, 1), 2), dtype=np.int32)
+        self._check(self.lib.mm_reproject(self.h, c_void_p(blocks.ctypes.data), len(blocks),
+                                          c_void_p(out.ctypes.data)))
+        return out[:total]
+
+    def reproject_motion_vector_subblocks(self, position, size, mv, model, comp, cur_poc=0, ref_poc=0):
+        """Single-call twin of MVReprojection::reprojectMotionVectorSubblocks
+        (MVReprojection.h:54-58): returns the fixed-point X and Y arrays shaped (rows, cols) like
+        the reference's Eigen::ArrayXXi pair."""
+        b = np.zeros(1, dtype=BLOCK_DTYPE)
+        b[0] = (position[0], position[1], size[0], size[1], mv[0], mv[1], model, comp, cur_poc, ref_poc)
+        r = self.reproject(b)
+        sb = 2 if comp else 4
+        rows, cols = size[1] // sb, size[0] // sb
+        return (r[:, 0].reshape(cols, rows).T.copy(), r[:, 1].reshape(cols, rows).T.copy())
+
+    # -- InterPrediction ---------------------------------------------------------------------
+    def predict(self, cur_poc: int, pus: np.ndarray, dst_y, dst_cb=None, dst_cr=None):
+        """Batched xPredInterBlkMM + xWeightedAverage over a picture's PU list into device planes."""
+        pus = np.ascontiguousarray(pus, dtype=PU_DTYPE)
+        self._check(self.lib.mm_pred(self.h, cur_poc, c_void_p(pus.ctypes.data), len(pus),
+                                     c_void_p(_ptr(dst_y)), dst_y.stride(0),
+                                     c_void_p(_ptr(dst_cb)) if dst_cb is not None else None,
+                                     c_void_p(_ptr(dst_cr)) if dst_cr is not None else None,
+                                     dst_cb.stride(0) if dst_cb is not None else 0))
+
+    def prepare(self, cur_poc: int, pus: np.ndarray):
+        pus = np.ascontiguousarray(pus, dtype=PU_DTYPE)
+        self._check(self.lib.mm_pred_prepare(self.h, cur_poc, c_void_p(pus.ctypes.data), len(pus)))
+
+    def run(self, dst_y, dst_cb=None, dst_cr=None):
+        self._check(self.lib.mm_pred_run(self.h, c_void_p(_ptr(dst_y)), dst_y.stride(0),
+                                         c_void_p(_ptr(dst_cb)) if dst_cb is not None else None,
+                                         c_void_p(_ptr(dst_cr)) if dst_cr is not None else None,
+                                         dst_cb.stride(0) if dst_cb is not None else 0))
+
+    def last_timing_ms(self) -> float:
+        ms = c_float()
+        self._check(self.lib.mm_last_timing(self.h, byref(ms)))
+        return float(ms.value)
+
+    # -- InterpolationFilter -----------------------------------------------------------------
+    def _filter(self, comp, vertical, src, x0, y0, w, h, frac, is_first, is_last):
+        src = np.ascontiguousarray(src, dtype=np.int16)
+        dst = np.zeros((h, w), dtype=np.int16)
+        base = src.ctypes.data + (y0 * src.shape[1] + x0) * 2
+        self._check(self.lib.mm_filter(self.h, comp, vertical, c_void_p(base), src.shape[1],
+                                       c_void_p(dst.ctypes.data), w, w, h, frac, int(is_first),
+                                       int(is_last)))
+        return dst
+
+    def filter_hor(self, comp, src, x0, y0, w, h, frac, is_last):
+        """InterpolationFilter::filterHor (always isFirst, InterpolationFilter.cpp:658)."""
+        return self._filter(comp, 0, src, x0, y0, w, h, frac, True, is_last)
+
+    def filter_ver(self, comp, src, x0, y0, w, h, frac, is_first, is_last):
+        """InterpolationFilter::filterVer."""
+        return self._filter(comp, 1, src, x0, y0, w, h, frac, is_first, is_last)

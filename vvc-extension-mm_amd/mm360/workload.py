@@ -1,0 +1,193 @@
+"""Seeded synthetic ERP workloads.
+
+No MM bitstreams exist and none can be produced offline, so every "decode" configuration is a
+synthetic per-picture PU list over synthetic 10-bit 4:2:0 ERP reference planes:
+
+* planes: clip(512 + 300 sin(3 phi) sin(2 theta) + 120 sin(17 phi + 5 theta) + U(-16, 16)),
+  seed 0x4D4D0000 + poc;
+* PU lists: every 128x128 CTU split by a seeded random QT/BT into PUs of 8x8 .. 64x64 plus
+  8x4 / 4x8 (uni only); per PU a model uniform over the active non-CLASSIC ids, 60 % bi /
+  40 % uni, MV integer part U[-32, 32] px and fraction U{0..15}/16, curPOC 8, refPOCs {0, 16};
+* the host applies the reference's sub-PU split for bi PUs (motionCompensation ->
+  xSubPuBio, InterPrediction.cpp:1786-1789 + :361-453): with refs 0 and 16 around POC 8 every
+  bi PU >= 8x8 with area >= 128 is BDOF-eligible by the pre-check, so a bi PU wider or taller
+  than 16 becomes min(16, w) x min(16, h) sub-PUs (the reprojection block centre moves).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import List, Sequence, Tuple
+
+import numpy as np
+
+from . import (GEODESIC_CAMPOSE, MPA_FRONT_BACK, MPA_LEFT_RIGHT, MPA_TOP_BOTTOM, PU_DTYPE,
+               ROTATIONAL, TANGENTIAL, THREE_D_TRANSLATIONAL)
+
+MPA3 = (MPA_FRONT_BACK, MPA_LEFT_RIGHT, MPA_TOP_BOTTOM)
+ALL_MODELS = MPA3 + (TANGENTIAL, THREE_D_TRANSLATIONAL, ROTATIONAL, GEODESIC_CAMPOSE)
+
+CUR_POC = 8
+REF_POCS = (0, 16)
+GED_EPIPOLE_Q24 = (1 << 24, 0, 0)  # epipole (1, 0, 0) in Q24 (README.md:59)
+
+
+@dataclass(frozen=True)
+class Config:
+    name: str
+    width: int
+    height: int
+    models: Tuple[int, ...]
+    frames: int
+    description: str
+
+
+CONFIGS = {
+    "C1": Config("C1", 256, 128, MPA3, 4, "256x128 ERP, MPA=1 only (CPU plumbing case)"),
+    "C2": Config("C2", 2048, 1024, MPA3 + (GEODESIC_CAMPOSE, ROTATIONAL), 32,
+                 "2048x1024 ERP decode, MPA+GED+ROT"),
+    "C3": Config("C3", 6144, 3072, ALL_MODELS, 1, "6144x3072 ERP decode, all 5 motion models"),
+}
+
+
+def ref_planes(width: int, height: int, poc: int, bit_depth: int = 10):
+    """Synthetic 10-bit ERP content (int16 Y, Cb, Cr; 4:2:0)."""
+    rng = np.random.default_rng(0x4D4D0000 + poc)
+
+    def plane(w, h, phase):
+        x = (np.arange(w, dtype=np.float64) + 0.5) / w * 2.0 * math.pi
+        y = (np.arange(h, dtype=np.float64) + 0.5) / h * math.pi
+        phi, theta = np.meshgrid(x + phase, y)
+        v = 512 + 300 * np.sin(3 * phi) * np.sin(2 * theta) + 120 * np.sin(17 * phi + 5 * theta)
+        v = v + rng.integers(-16, 17, size=v.shape)
+        return np.clip(np.rint(v), 0, (1 << bit_depth) - 1).astype(np.int16)
+
+    return plane(width, height, 0.0), plane(width // 2, height // 2, 0.7), plane(width // 2, height // 2, 1.9)
+
+
+def _split_ctu(rng, x0, y0, w, h, out):
+    """Seeded random QT/BT split down to 8x8 .. 64x64 leaves (plus occasional 8x4 / 4x8)."""
+    options = []
+    if w <= 64 and h <= 64 and w >= 8 and h >= 8:
+        options += ["leaf"] * 3
+    if w >= 16 and h >= 16:
+        options += ["qt"] * (4 if (w > 64 or h > 64) else 2)
+    if w >= 16 and h <= 64:
+        options.append("btv")
+    if h >= 16 and w <= 64:
+        options.append("bth")
+    if w == 8 and h == 8:
+        options.append("small")
+    choice = options[int(rng.integers(0, len(options)))] if options else "leaf"
+    if choice == "leaf":
+        out.append((x0, y0, w, h))
+    elif choice == "qt":
+        for dy in (0, h // 2):
+            for dx in (0, w // 2):
+                _split_ctu(rng, x0 + dx, y0 + dy, w // 2, h // 2, out)
+    elif choice == "btv":
+        _split_ctu(rng, x0, y0, w // 2, h, out)
+        _split_ctu(rng, x0 + w // 2, y0, w // 2, h, out)
+    elif choice == "bth":
+        _split_ctu(rng, x0, y0, w, h // 2, out)
+        _split_ctu(rng, x0, y0 + h // 2, w, h // 2, out)
+    else:  # 8x8 -> two 4x8 or two 8x4 (uni-only PUs)
+        if rng.random() < 0.5:
+            out += [(x0, y0, 4, 8), (x0 + 4, y0, 4, 8)]
+        else:
+            out += [(x0, y0, 8, 4), (x0, y0 + 4, 8, 4)]
+
+
+def pu_list(cfg: Config, frame: int = 0, uniform: bool = False, uniform_model: int = None,
+            ctu: int = 128) -> np.ndarray:
+    """Per-picture PU list (after the host's sub-PU split), PU_DTYPE."""
+    rng = np.random.default_rng(0x4D4D1000 + 977 * frame + cfg.width)
+    models = cfg.models
+    leaves: List[Tuple[int, int, int, int]] = []
+    if uniform:
+        for y in range(0, cfg.height, 16):
+            for x in range(0, cfg.width, 16):
+                leaves.append((x, y, 16, 16))
+    else:
+        for y0 in range(0, cfg.height, ctu):
+            for x0 in range(0, cfg.width, ctu):
+                _split_ctu(rng, x0, y0, min(ctu, cfg.width - x0), min(ctu, cfg.height - y0), leaves)
+    rows = []
+    for (x, y, w, h) in leaves:
+        small = (w * h) < 64  # 8x4 / 4x8: uni only
+        bi = (not small) and rng.random() < 0.6
+        if uniform:
+            m0 = m1 = uniform_model if uniform_model is not None else models[0]
+        else:
+            m0 = int(models[rng.integers(0, len(models))])
+            m1 = int(models[rng.integers(0, len(models))])
+        mvs = []
+        for _ in range(2):
+            mvs.append([int(rng.integers(-32, 33)) * 16 + int(rng.integers(0, 16)),
+                        int(rng.integers(-32, 33)) * 16 + int(rng.integers(0, 16))])
+        if bi:
+            refs = (REF_POCS[0], REF_POCS[1])
+        else:
+            lst = int(rng.integers(0, 2))
+            refs = (REF_POCS[0], -1) if lst == 0 else (-1, REF_POCS[1])
+        if bi and (w > 16 or h > 16):
+            sw, sh = min(16, w), min(16, h)
+            for yy in range(y, y + h, sh):
+                for xx in range(x, x + w, sw):
+                    rows.append((xx, yy, sw, sh, mvs, refs, (m0, m1)))
+        else:
+            rows.append((x, y, w, h, mvs, refs, (m0, m1)))
+    out = np.zeros(len(rows), dtype=PU_DTYPE)
+    for i, (x, y, w, h, mvs, refs, ms) in enumerate(rows):
+        out[i]["x"], out[i]["y"], out[i]["w"], out[i]["h"] = x, y, w, h
+        out[i]["mv"] = np.array(mvs, dtype=np.int32)
+        out[i]["ref_poc"] = refs
+        out[i]["model"] = ms
+    return out
+
+
+def luma_area(pus: np.ndarray) -> int:
+    return int((pus["w"].astype(np.int64) * pus["h"]).sum())
+
+
+def algorithmic_bytes(pus: np.ndarray) -> int:
+    """uni 6 B / bi 9 B per output luma pixel (int16 samples, 4:2:0)."""
+    area = pus["w"].astype(np.int64) * pus["h"]
+    bi = (pus["ref_poc"][:, 0] >= 0) & (pus["ref_poc"][:, 1] >= 0)
+    return int((area * np.where(bi, 9, 6)).sum())
+
+
+def random_blocks(width: int, height: int, models: Sequence[int], n: int, seed: int,
+                  comps=(0, 1), sizes=(4, 8, 16, 32, 64), mv_range: int = 32, cur_poc: int = CUR_POC,
+                  ref_pocs=REF_POCS) -> np.ndarray:
+    """Random reprojection requests covering every model / component / N in {1,2,4,...}."""
+    from . import BLOCK_DTYPE
+    rng = np.random.default_rng(seed)
+    out = np.zeros(n, dtype=BLOCK_DTYPE)
+    for i in range(n):
+        comp = int(comps[rng.integers(0, len(comps))])
+        cs = 1 if comp else 0
+        w = int(sizes[rng.integers(0, len(sizes))])
+        h = int(sizes[rng.integers(0, len(sizes))])
+        if comp == 0 and (w < 4 or h < 4):
+            w, h = max(w, 4), max(h, 4)
+        wc, hc = w >> cs, h >> cs
+        if comp and (wc < 2 or hc < 2):
+            wc, hc = max(wc, 2), max(hc, 2)
+        sb = 2 if comp else 4
+        Wc, Hc = width >> cs, height >> cs
+        x = int(rng.integers(0, (Wc - wc) // sb + 1)) * sb
+        y = int(rng.integers(0, (Hc - hc) // sb + 1)) * sb
+        kind = rng.random()
+        if kind < 0.1:
+            mvh = mvv = 0
+        elif kind < 0.2:
+            mvh = int(rng.integers(-2000, 2001))
+            mvv = int(rng.integers(-2000, 2001))
+        else:
+            mvh = int(rng.integers(-mv_range * 16, mv_range * 16 + 1))
+            mvv = int(rng.integers(-mv_range * 16, mv_range * 16 + 1))
+        model = int(models[rng.integers(0, len(models))])
+        out[i] = (x, y, wc, hc, mvh, mvv, model, comp if comp == 0 else int(rng.integers(1, 3)),
+                  cur_poc, int(ref_pocs[rng.integers(0, len(ref_pocs))]))
+    return out
