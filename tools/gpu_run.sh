@@ -1,0 +1,30 @@
+#!/bin/bash
+# GPU-box driver: runs the named steps in order, each under its own time limit, and stops at the
+# first failure (no further GPU work after a fault / abort / timeout).
+#   tools/gpu_run.sh tests smoke bench prof pmc
+set -u
+mkdir -p gpurun_out
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+run() {  # name limit cmd...
+  local name=$1 lim=$2; shift 2
+  echo "[gpu_run] $name: $*"
+  timeout -k 10 "$lim" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "[gpu_run] $name rc=$rc"
+  tail -3 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ]; then exit $rc; fi
+}
+for step in "$@"; do
+  case $step in
+    tests) run gpu_tests 900 python -m pytest tests -x -q -m gpu ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 600 python bench.py ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
+    pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 ;;
+    pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 ;;
+    pmc_valu) run pmc_valu 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES -d gpurun_out/pmc_valu -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "[gpu_run] all steps ok"
