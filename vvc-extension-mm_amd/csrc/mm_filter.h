@@ -65,69 +65,135 @@ MM_HD bool sb_out_of_range(int xPos, int yPos, int Wc, int Hc, int maxCUw, int m
 
 MM_HD int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
-// Predict one sub-block (sbw x sbh, NT taps) from a clamped-address reference plane.
-//   bi: keep 14-bit intermediate (rndRes = !bi), else clip to bit depth.
-//   coef: tap row for xFrac / yFrac.  out: row-major sbw*sbh.
+// Every case of xPredInterBlkMM's per-sub-block dispatch (InterPrediction.cpp:785-826) --
+// filterCopy (both fractions 0), filterHor only (yFrac == 0), filterVer only (xFrac == 0) and the
+// 2-D filterHor(isFirst, !isLast) + filterVer(!isFirst, rndRes) -- yields exactly the 2-D result
+// computed with the phase-0 tap row ({.., 64, ..}) for the zero fraction(s): with taps summing to
+// 64 and IF_INTERNAL_OFFS = 8192 the extra stage only adds and removes exact multiples of the
+// shift (verified for bit depths 8..12 by tests/test_filter_identity.py).  The kernels therefore
+// run the branch-free 2-D form for every sub-block (no divergence between the four cases).
+
+// Predict one sub-block (SBW x SBH, NT taps) from a clamped-address reference plane.
+//   bi: keep the 14-bit intermediate (rndRes = !bi), else clip to the bit depth.
+//   cx, cy: tap rows for xFrac / yFrac.  out: row-major SBW*SBH.
 template <int NT, int SBW, int SBH>
 MM_HD void predict_subblock(const int16_t* __restrict__ ref, int stride, int Wc, int Hc, int xPos, int yPos,
-                            int xFrac, int yFrac, const int8_t* cx, const int8_t* cy, bool bi, int bd,
-                            int16_t* out) {
+                            const int8_t* cx, const int8_t* cy, bool bi, int bd, int16_t* out) {
+  constexpr int R = SBH + NT - 1, H0 = NT / 2 - 1;
   const int maxv = (1 << bd) - 1;
-  const bool rndRes = !bi;
-  if (yFrac == 0) {
-    // filterHor(xFrac, isLast = rndRes) -> filterCopy[true][rndRes] or filter<NT,false,true,rndRes>
-    for (int r = 0; r < SBH; r++) {
-      const int16_t* row = ref + (long)clampi(yPos + r, 0, Hc - 1) * stride;
-      for (int c = 0; c < SBW; c++) {
-        int v;
-        if (xFrac == 0) {
-          int s = row[clampi(xPos + c, 0, Wc - 1)];
-          if (rndRes)
-            v = s;  // isFirst == isLast: plain copy
-          else
-            v = (int16_t)((int16_t)(s << if_internal_frac_bits(bd)) - (int16_t)IF_INTERNAL_OFFS);
-        } else {
-          FiltParam fp = filt_param(true, rndRes, bd);
-          int sum = 0;
-          for (int t = 0; t < NT; t++) sum += row[clampi(xPos + c + t - (NT / 2 - 1), 0, Wc - 1)] * cx[t];
-          v = (int16_t)((sum + fp.offset) >> fp.shift);
-          if (fp.clip) v = clip_pel(v, maxv);
-        }
-        out[r * SBW + c] = (int16_t)v;
-      }
-    }
-    return;
-  }
-  if (xFrac == 0) {
-    // filterVer(yFrac, isFirst = true, isLast = rndRes)
-    FiltParam fp = filt_param(true, rndRes, bd);
-    for (int r = 0; r < SBH; r++)
-      for (int c = 0; c < SBW; c++) {
-        const int xx = clampi(xPos + c, 0, Wc - 1);
-        int sum = 0;
-        for (int t = 0; t < NT; t++) sum += ref[(long)clampi(yPos + r + t - (NT / 2 - 1), 0, Hc - 1) * stride + xx] * cy[t];
-        int v = (int16_t)((sum + fp.offset) >> fp.shift);
-        if (fp.clip) v = clip_pel(v, maxv);
-        out[r * SBW + c] = (int16_t)v;
-      }
-    return;
-  }
-  // 2-D: filterHor on (SBH + NT - 1) rows into tmp (isFirst, !isLast), then filterVer (!isFirst, rndRes)
-  int16_t tmp[(SBH + NT - 1) * SBW];
-  FiltParam fh = filt_param(true, false, bd);
-  for (int r = 0; r < SBH + NT - 1; r++) {
-    const int16_t* row = ref + (long)clampi(yPos + r - (NT / 2 - 1), 0, Hc - 1) * stride;
+  const FiltParam fh = filt_param(true, false, bd);
+  const FiltParam fv = filt_param(false, !bi, bd);
+  int tmp[R][SBW];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const int16_t* row = ref + (long)clampi(yPos + r - H0, 0, Hc - 1) * stride;
+#pragma unroll
     for (int c = 0; c < SBW; c++) {
       int sum = 0;
-      for (int t = 0; t < NT; t++) sum += row[clampi(xPos + c + t - (NT / 2 - 1), 0, Wc - 1)] * cx[t];
-      tmp[r * SBW + c] = (int16_t)((sum + fh.offset) >> fh.shift);
+#pragma unroll
+      for (int t = 0; t < NT; t++) sum += row[clampi(xPos + c + t - H0, 0, Wc - 1)] * cx[t];
+      tmp[r][c] = (int16_t)((sum + fh.offset) >> fh.shift);
     }
   }
-  FiltParam fv = filt_param(false, rndRes, bd);
+#pragma unroll
   for (int r = 0; r < SBH; r++)
+#pragma unroll
     for (int c = 0; c < SBW; c++) {
       int sum = 0;
-      for (int t = 0; t < NT; t++) sum += tmp[(r + t) * SBW + c] * cy[t];
+#pragma unroll
+      for (int t = 0; t < NT; t++) sum += tmp[r + t][c] * cy[t];
+      int v = (int16_t)((sum + fv.offset) >> fv.shift);
+      if (fv.clip) v = clip_pel(v, maxv);
+      out[r * SBW + c] = (int16_t)v;
+    }
+}
+
+// Window fully inside the picture (plus one spare sample to the right): the fast path reads
+// whole window rows with dword-aligned loads and needs no clamping.
+template <int NT, int SBW, int SBH>
+MM_HD bool window_interior(int xPos, int yPos, int Wc, int Hc) {
+  return xPos - (NT / 2 - 1) >= 0 && xPos + SBW + NT / 2 + 1 <= Wc && yPos - (NT / 2 - 1) >= 0 &&
+         yPos + SBH + NT / 2 <= Hc;
+}
+
+// Row segment of L = SBW + NT - 1 samples starting at x, read as dwords from the even index
+// below x (planes are 4-byte aligned, stride even).
+typedef uint32_t u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
+typedef uint32_t u32x3_a4 __attribute__((ext_vector_type(3), aligned(4)));
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+
+// ND dwords from a 4-byte aligned address as few wide loads as possible (global_load_dwordx4 /
+// x3 / x2 only need dword alignment on CDNA)
+template <int ND>
+MM_HD void load_dwords(const uint32_t* p, uint32_t* d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (ND == 6) {
+    u32x4_a4 a = *reinterpret_cast<const u32x4_a4*>(p);
+    u32x2_a4 b = *reinterpret_cast<const u32x2_a4*>(p + 4);
+    d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w; d[4] = b.x; d[5] = b.y;
+  } else if constexpr (ND == 3) {
+    u32x3_a4 a = *reinterpret_cast<const u32x3_a4*>(p);
+    d[0] = a.x; d[1] = a.y; d[2] = a.z;
+  } else {
+#pragma unroll
+    for (int k = 0; k < ND; k++) d[k] = p[k];
+  }
+#else
+  for (int k = 0; k < ND; k++) d[k] = p[k];
+#endif
+}
+
+template <int L>
+MM_HD void load_row(const int16_t* __restrict__ row, int x, int* v) {
+  constexpr int ND = (L + 2) / 2;
+  const uint32_t* p = reinterpret_cast<const uint32_t*>(row + (x & ~1));
+  uint32_t d[ND];
+  load_dwords<ND>(p, d);
+  // odd start: funnel-shift the dword stream by one sample (value selects, no indexed array)
+  const bool odd = (x & 1) != 0;
+#pragma unroll
+  for (int m = 0; m < (L + 1) / 2; m++) {
+    const uint32_t nxt = (m + 1 < ND) ? (d[m + 1] << 16) : 0u;
+    const uint32_t w = odd ? ((d[m] >> 16) | nxt) : d[m];
+    v[2 * m] = (int16_t)(w & 0xffffu);
+    if (2 * m + 1 < L) v[2 * m + 1] = (int16_t)(w >> 16);
+  }
+}
+
+// predict_subblock for an interior window: same arithmetic, window rows read with wide loads
+template <int NT, int SBW, int SBH>
+MM_HD void predict_subblock_interior(const int16_t* __restrict__ ref, int stride, int xPos, int yPos,
+                                     const int8_t* cx, const int8_t* cy, bool bi, int bd, int16_t* out) {
+  constexpr int L = SBW + NT - 1, R = SBH + NT - 1, H0 = NT / 2 - 1;
+  const int maxv = (1 << bd) - 1;
+  const FiltParam fh = filt_param(true, false, bd);
+  const FiltParam fv = filt_param(false, !bi, bd);
+  int cxv[NT], cyv[NT];
+#pragma unroll
+  for (int t = 0; t < NT; t++) {
+    cxv[t] = cx[t];
+    cyv[t] = cy[t];
+  }
+  int tmp[R][SBW];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    int v[L];
+    load_row<L>(ref + (long)(yPos + r - H0) * stride, xPos - H0, v);
+#pragma unroll
+    for (int c = 0; c < SBW; c++) {
+      int sum = 0;
+#pragma unroll
+      for (int t = 0; t < NT; t++) sum += v[c + t] * cxv[t];
+      tmp[r][c] = (int16_t)((sum + fh.offset) >> fh.shift);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < SBH; r++)
+#pragma unroll
+    for (int c = 0; c < SBW; c++) {
+      int sum = 0;
+#pragma unroll
+      for (int t = 0; t < NT; t++) sum += tmp[r + t][c] * cyv[t];
       int v = (int16_t)((sum + fv.offset) >> fv.shift);
       if (fv.clip) v = clip_pel(v, maxv);
       out[r * SBW + c] = (int16_t)v;

@@ -18,7 +18,7 @@
 #include <stdint.h>
 
 #if defined(__HIPCC__) || defined(__HIP__)
-#define MM_HD __host__ __device__ inline
+#define MM_HD __host__ __device__ __forceinline__
 #define MM_HD_CONST __device__ __constant__
 #else
 #define MM_HD inline
@@ -118,12 +118,19 @@ MM_HD double reduce_fast_(double x, int* np) {
 }
 
 // 4/pi bits (glibc sysdeps/ieee754/flt-32/s_sincosf_data.c __inv_pio4)
+// (entry i is bits 8*(i-3) .. 8*i+31 of 2/pi's fraction; written as a switch so that no
+// per-thread table is materialised)
 MM_HD uint32_t inv_pio4_(int i) {
-  const uint32_t t[24] = {0xa2,       0xa2f9,     0xa2f983,   0xa2f9836e, 0xf9836e4e, 0x836e4e44,
-                          0x6e4e4415, 0x4e441529, 0x441529fc, 0x1529fc27, 0x29fc2757, 0xfc2757d1,
-                          0x2757d1f5, 0x57d1f534, 0xd1f534dd, 0xf534ddc0, 0x34ddc0db, 0xddc0db62,
-                          0xc0db6295, 0xdb629599, 0x6295993c, 0x95993c43, 0x993c4390, 0x3c439041};
-  return t[i];
+  switch (i) {
+    case 0: return 0xa2u;          case 1: return 0xa2f9u;        case 2: return 0xa2f983u;
+    case 3: return 0xa2f9836eu;    case 4: return 0xf9836e4eu;    case 5: return 0x836e4e44u;
+    case 6: return 0x6e4e4415u;    case 7: return 0x4e441529u;    case 8: return 0x441529fcu;
+    case 9: return 0x1529fc27u;    case 10: return 0x29fc2757u;   case 11: return 0xfc2757d1u;
+    case 12: return 0x2757d1f5u;   case 13: return 0x57d1f534u;   case 14: return 0xd1f534ddu;
+    case 15: return 0xf534ddc0u;   case 16: return 0x34ddc0dbu;   case 17: return 0xddc0db62u;
+    case 18: return 0xc0db6295u;   case 19: return 0xdb629599u;   case 20: return 0x6295993cu;
+    case 21: return 0x95993c43u;   case 22: return 0x993c4390u;   default: return 0x3c439041u;
+  }
 }
 
 MM_HD double reduce_large_(uint32_t xi, int* np) {
@@ -691,7 +698,7 @@ MM_HD float e_psqrt(float x) {
 // Packet-or-scalar selection (Eigen LinearVectorizedTraversal on a 16-byte aligned
 // destination: elements [0, n - n%4) use packets, the tail uses the scalar functors).
 struct Math {
-  bool packet;
+  int packet;  // int, not bool: an i1 member defeats SROA and lands in LDS
   MM_HD float sin(float x) const { return packet ? e_psin(x) : g_sinf(x); }
   MM_HD float cos(float x) const { return packet ? e_pcos(x) : g_cosf(x); }
   MM_HD float sqrt(float x) const { return packet ? e_psqrt(x) : sqrtf_(x); }

@@ -91,7 +91,7 @@ MM_HD void reproj_thread(int g, const SeqConst& sc, const JobDev* jobs, int n_jo
                          const int* chunk_start, const BlockSetup* setups, const MpaCache& cache, int32_t* out_xy) {
   const int ji = find_item(job_offsets, chunk_start, g, n_jobs);
   const JobDev& j = jobs[ji];
-  const int local = g - j.offset;
+  const int local = g - job_offsets[ji];  // enumeration order; results go to j.offset + local
   const int col = local / j.rows, row = local - col * j.rows;
   // grid: luma frame grid (4i + off) or chroma LinSpaced (2*xc + off + 4i) -- the same values
   const float gx = (float)(j.x + 4 * col) + sc.off;
@@ -109,8 +109,8 @@ MM_HD void reproj_thread(int g, const SeqConst& sc, const JobDev* jobs, int n_jo
   int32_t fx, fy;
   reproject_element(sc, setups[ji], gx, gy, packet_lane(local, j.n), mpa_cached, px, py, vip, j.comp ? 1 : 0, &fx,
                     &fy);
-  out_xy[2 * g] = fx;
-  out_xy[2 * g + 1] = fy;
+  out_xy[2 * (j.offset + local)] = fx;
+  out_xy[2 * (j.offset + local) + 1] = fy;
 }
 
 // One luma 4x4 sub-block (and its two 4:2:0 chroma 2x2 sub-blocks) of one PU: both lists,
@@ -121,14 +121,18 @@ MM_HD void mc_thread(int g, const Geometry& geo, const Taps& taps, const PuDev* 
                      const RefDev* refs, int16_t* dst_y, int dsy, int16_t* dst_cb, int16_t* dst_cr, int dsc) {
   const int pi = find_item(pu_offsets, chunk_start, g, n_pus);
   const PuDev pu = pus[pi];
-  const int local = g - pu.sb_offset;
-  const int rows = pu.h >> 2;
-  const int col = local / rows, row = local - col * rows;
+  // lanes walk the PU row-major (horizontally adjacent sub-blocks in adjacent lanes share the
+  // reference cache lines of each window row); reprojection results are Eigen column-major
+  const int lin = g - pu.sb_offset;
+  const int rows = pu.h >> 2, cols = pu.w >> 2;
+  const int row = lin / cols, col = lin - row * cols;
+  const int local = col * rows + row;
   const bool bi = pu.ref_slot[0] >= 0 && pu.ref_slot[1] >= 0;
   const int uni_list = pu.ref_slot[0] >= 0 ? 0 : 1;
 
   // ---- luma 4x4 ----
   int16_t pl[2][16];
+#pragma unroll
   for (int l = 0; l < 2; l++) {
     if (pu.ref_slot[l] < 0) continue;
     const JobDev& j = jobs[pu.job[l][0]];
@@ -137,8 +141,11 @@ MM_HD void mc_thread(int g, const Geometry& geo, const Taps& taps, const PuDev* 
     const RefDev r = refs[pu.ref_slot[l]];
     if (sb_out_of_range(xPos, yPos, geo.W, geo.H, geo.maxCUw, geo.maxCUh, 4, 4)) {
       for (int i = 0; i < 16; i++) pl[l][i] = 0;
+    } else if (window_interior<8, 4, 4>(xPos, yPos, geo.W, geo.H)) {
+      predict_subblock_interior<8, 4, 4>(r.y, r.stride_y, xPos, yPos, taps.luma[xFrac],
+                                         taps.luma[yFrac], bi, geo.bd, pl[l]);
     } else {
-      predict_subblock<8, 4, 4>(r.y, r.stride_y, geo.W, geo.H, xPos, yPos, xFrac, yFrac, taps.luma[xFrac],
+      predict_subblock<8, 4, 4>(r.y, r.stride_y, geo.W, geo.H, xPos, yPos, taps.luma[xFrac],
                                 taps.luma[yFrac], bi, geo.bd, pl[l]);
     }
   }
@@ -148,13 +155,14 @@ MM_HD void mc_thread(int g, const Geometry& geo, const Taps& taps, const PuDev* 
       int16_t* d = dst_y + (long)(oy + r) * dsy + ox;
       for (int c = 0; c < 4; c++) {
         const int i = r * 4 + c;
-        d[c] = bi ? add_avg(pl[0][i], pl[1][i], geo.bd) : pl[uni_list][i];
+        d[c] = bi ? add_avg(pl[0][i], pl[1][i], geo.bd) : (uni_list == 0 ? pl[0][i] : pl[1][i]);
       }
     }
   }
   if (!geo.chroma) return;
   // ---- chroma 2x2 (Cb and Cr share one reprojection) ----
   int16_t pcb[2][4], pcr[2][4];
+#pragma unroll
   for (int l = 0; l < 2; l++) {
     if (pu.ref_slot[l] < 0) continue;
     const JobDev& j = jobs[pu.job[l][1]];
@@ -163,10 +171,15 @@ MM_HD void mc_thread(int g, const Geometry& geo, const Taps& taps, const PuDev* 
     const RefDev r = refs[pu.ref_slot[l]];
     if (sb_out_of_range(xPos, yPos, geo.Wc, geo.Hc, geo.maxCUwc, geo.maxCUhc, 2, 2)) {
       for (int i = 0; i < 4; i++) pcb[l][i] = pcr[l][i] = 0;
+    } else if (window_interior<4, 2, 2>(xPos, yPos, geo.Wc, geo.Hc)) {
+      predict_subblock_interior<4, 2, 2>(r.cb, r.stride_c, xPos, yPos, taps.chroma[xFrac],
+                                         taps.chroma[yFrac], bi, geo.bd, pcb[l]);
+      predict_subblock_interior<4, 2, 2>(r.cr, r.stride_c, xPos, yPos, taps.chroma[xFrac],
+                                         taps.chroma[yFrac], bi, geo.bd, pcr[l]);
     } else {
-      predict_subblock<4, 2, 2>(r.cb, r.stride_c, geo.Wc, geo.Hc, xPos, yPos, xFrac, yFrac, taps.chroma[xFrac],
+      predict_subblock<4, 2, 2>(r.cb, r.stride_c, geo.Wc, geo.Hc, xPos, yPos, taps.chroma[xFrac],
                                 taps.chroma[yFrac], bi, geo.bd, pcb[l]);
-      predict_subblock<4, 2, 2>(r.cr, r.stride_c, geo.Wc, geo.Hc, xPos, yPos, xFrac, yFrac, taps.chroma[xFrac],
+      predict_subblock<4, 2, 2>(r.cr, r.stride_c, geo.Wc, geo.Hc, xPos, yPos, taps.chroma[xFrac],
                                 taps.chroma[yFrac], bi, geo.bd, pcr[l]);
     }
   }
@@ -177,8 +190,8 @@ MM_HD void mc_thread(int g, const Geometry& geo, const Taps& taps, const PuDev* 
       int16_t* dr = dst_cr + (long)(oy + r) * dsc + ox;
       for (int c = 0; c < 2; c++) {
         const int i = r * 2 + c;
-        db[c] = bi ? add_avg(pcb[0][i], pcb[1][i], geo.bd) : pcb[uni_list][i];
-        dr[c] = bi ? add_avg(pcr[0][i], pcr[1][i], geo.bd) : pcr[uni_list][i];
+        db[c] = bi ? add_avg(pcb[0][i], pcb[1][i], geo.bd) : (uni_list == 0 ? pcb[0][i] : pcb[1][i]);
+        dr[c] = bi ? add_avg(pcr[0][i], pcr[1][i], geo.bd) : (uni_list == 0 ? pcr[0][i] : pcr[1][i]);
       }
     }
   }

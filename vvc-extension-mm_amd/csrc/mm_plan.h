@@ -8,6 +8,7 @@
 // (EpipoleList::findEpipole + GeodesicMotionModel::setEpipole).  Shared by the C-ABI
 // (mm_kernels.hip) and the CPU twin of the test suite.
 #pragma once
+#include <algorithm>
 #include <array>
 #include <map>
 #include <string>
@@ -183,18 +184,53 @@ class Planner {
         }
       }
       if (!used) return fail(MM_ERR_ARG, "PU " + std::to_string(i) + " uses no reference list");
-      d.sb_offset = plan_->n_sb;
-      plan_->n_sb += (u.w / 4) * (u.h / 4);
       plan_->pus.push_back(d);
-      plan_->pu_off.push_back(d.sb_offset);
     }
     finish_jobs();
+    // k_mc enumeration grouped by prediction class (bi, uni L0, uni L1): a wave then runs one
+    // class's code path instead of both lists masked
+    auto cls = [](const PuDev& d) { return d.ref_slot[0] >= 0 && d.ref_slot[1] >= 0 ? 0 : (d.ref_slot[0] >= 0 ? 1 : 2); };
+    std::stable_sort(plan_->pus.begin(), plan_->pus.end(),
+                     [&](const PuDev& a, const PuDev& b) { return cls(a) < cls(b); });
+    for (auto& d : plan_->pus) {
+      d.sb_offset = plan_->n_sb;
+      plan_->n_sb += (d.w / 4) * (d.h / 4);
+      plan_->pu_off.push_back(d.sb_offset);
+    }
     build_chunks(plan_->pu_off, plan_->n_sb, &plan_->pu_chunk);
     return MM_OK;
   }
 
  private:
+  // Enumerate jobs grouped by (component, model, packet/scalar) so that the waves of k_setup and
+  // k_reproj run one model path each instead of every model's path (divergence).  j.offset keeps
+  // each job's place in the result array; job_off is the prefix over the enumeration order.
   void finish_jobs() {
+    const int n = (int)plan_->jobs.size();
+    std::vector<int> order(n);
+    for (int i = 0; i < n; i++) order[i] = i;
+    auto key = [&](int i) {
+      const JobDev& j = plan_->jobs[i];
+      return (j.comp * 64 + j.model) * 2 + (j.n < 4 ? 1 : 0);
+    };
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return key(a) < key(b); });
+    std::vector<int> inv(n);
+    std::vector<JobDev> sorted(n);
+    for (int i = 0; i < n; i++) {
+      sorted[i] = plan_->jobs[order[i]];
+      inv[order[i]] = i;
+    }
+    plan_->jobs.swap(sorted);
+    for (auto& d : plan_->pus)
+      for (int l = 0; l < 2; l++)
+        for (int c = 0; c < 2; c++)
+          if (d.job[l][c] >= 0) d.job[l][c] = inv[d.job[l][c]];
+    plan_->job_off.resize(n);
+    int acc = 0;
+    for (int i = 0; i < n; i++) {
+      plan_->job_off[i] = acc;
+      acc += plan_->jobs[i].n;
+    }
     build_chunks(plan_->job_off, plan_->n_elems, &plan_->job_chunk);
     if (plan_->ged.empty()) plan_->ged.push_back(M3{});
   }
