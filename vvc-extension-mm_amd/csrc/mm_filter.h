@@ -160,7 +160,75 @@ MM_HD void load_row(const int16_t* __restrict__ row, int x, int* v) {
   }
 }
 
-// predict_subblock for an interior window: same arithmetic, window rows read with wide loads
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef short mm_short2 __attribute__((ext_vector_type(2)));
+// a.lo*b.lo + a.hi*b.hi + c, exact (v_dot2c_i32_i16; int16 samples x taps, int32 sums)
+__device__ __forceinline__ int dot2_(uint32_t a, uint32_t b, int c) {
+  return __builtin_amdgcn_sdot2(__builtin_bit_cast(mm_short2, a), __builtin_bit_cast(mm_short2, b), c, false);
+}
+__device__ __forceinline__ uint32_t pack2_(int lo, int hi) {
+  return ((uint32_t)lo & 0xffffu) | ((uint32_t)hi << 16);
+}
+// predict_subblock for an interior window (device): same arithmetic, samples handled as packed
+// int16 pairs -- each tap pair is one v_dot2c_i32_i16.
+template <int NT, int SBW, int SBH>
+__device__ __forceinline__ void predict_subblock_interior(const int16_t* __restrict__ ref, int stride, int xPos, int yPos,
+                                                          const int8_t* cx, const int8_t* cy, bool bi, int bd,
+                                                          int16_t* out) {
+  constexpr int L = SBW + NT - 1, R = SBH + NT - 1, H0 = NT / 2 - 1;
+  constexpr int ND = (L + 2) / 2;  // dwords loaded per row
+  constexpr int NP = NT / 2;       // tap pairs
+  const int maxv = (1 << bd) - 1;
+  const FiltParam fh = filt_param(true, false, bd);
+  const FiltParam fv = filt_param(false, !bi, bd);
+  uint32_t ch[NP], cv[NP];
+#pragma unroll
+  for (int k = 0; k < NP; k++) {
+    ch[k] = pack2_(cx[2 * k], cx[2 * k + 1]);
+    cv[k] = pack2_(cy[2 * k], cy[2 * k + 1]);
+  }
+  const int x0 = xPos - H0;
+  const uint32_t sh = (x0 & 1) ? 16u : 0u;
+  int tmp[R][SBW];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(ref + (long)(yPos + r - H0) * stride + (x0 & ~1));
+    uint32_t d[ND];
+    load_dwords<ND>(p, d);
+    // e[m] = window samples (2m, 2m+1), o[m] = (2m+1, 2m+2); the last e only needs its low half
+    uint32_t e[ND], o[ND - 1];
+#pragma unroll
+    for (int m = 0; m < ND; m++) e[m] = __builtin_amdgcn_alignbit(m + 1 < ND ? d[m + 1] : 0u, d[m], sh);
+#pragma unroll
+    for (int m = 0; m < ND - 1; m++) o[m] = __builtin_amdgcn_alignbit(e[m + 1], e[m], 16u);
+#pragma unroll
+    for (int c = 0; c < SBW; c++) {
+      int sum = 0;
+#pragma unroll
+      for (int k = 0; k < NP; k++) sum = dot2_((c & 1) ? o[(c >> 1) + k] : e[(c >> 1) + k], ch[k], sum);
+      tmp[r][c] = (int16_t)((sum + fh.offset) >> fh.shift);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < SBW; c++) {
+    uint32_t pe[(R + 1) / 2], po[R / 2];  // row pairs (2m, 2m+1) and (2m+1, 2m+2)
+#pragma unroll
+    for (int m = 0; m < (R + 1) / 2; m++) pe[m] = pack2_(tmp[2 * m][c], 2 * m + 1 < R ? tmp[2 * m + 1][c] : 0);
+#pragma unroll
+    for (int m = 0; m < R / 2; m++) po[m] = pack2_(tmp[2 * m + 1][c], 2 * m + 2 < R ? tmp[2 * m + 2][c] : 0);
+#pragma unroll
+    for (int r = 0; r < SBH; r++) {
+      int sum = 0;
+#pragma unroll
+      for (int k = 0; k < NP; k++) sum = dot2_((r & 1) ? po[(r >> 1) + k] : pe[(r >> 1) + k], cv[k], sum);
+      int v = (int16_t)((sum + fv.offset) >> fv.shift);
+      if (fv.clip) v = clip_pel(v, maxv);
+      out[r * SBW + c] = (int16_t)v;
+    }
+  }
+}
+#else
+// predict_subblock for an interior window (host): same arithmetic, window rows read with wide loads
 template <int NT, int SBW, int SBH>
 MM_HD void predict_subblock_interior(const int16_t* __restrict__ ref, int stride, int xPos, int yPos,
                                      const int8_t* cx, const int8_t* cy, bool bi, int bd, int16_t* out) {
@@ -168,37 +236,26 @@ MM_HD void predict_subblock_interior(const int16_t* __restrict__ ref, int stride
   const int maxv = (1 << bd) - 1;
   const FiltParam fh = filt_param(true, false, bd);
   const FiltParam fv = filt_param(false, !bi, bd);
-  int cxv[NT], cyv[NT];
-#pragma unroll
-  for (int t = 0; t < NT; t++) {
-    cxv[t] = cx[t];
-    cyv[t] = cy[t];
-  }
   int tmp[R][SBW];
-#pragma unroll
   for (int r = 0; r < R; r++) {
     int v[L];
     load_row<L>(ref + (long)(yPos + r - H0) * stride, xPos - H0, v);
-#pragma unroll
     for (int c = 0; c < SBW; c++) {
       int sum = 0;
-#pragma unroll
-      for (int t = 0; t < NT; t++) sum += v[c + t] * cxv[t];
+      for (int t = 0; t < NT; t++) sum += v[c + t] * cx[t];
       tmp[r][c] = (int16_t)((sum + fh.offset) >> fh.shift);
     }
   }
-#pragma unroll
   for (int r = 0; r < SBH; r++)
-#pragma unroll
     for (int c = 0; c < SBW; c++) {
       int sum = 0;
-#pragma unroll
-      for (int t = 0; t < NT; t++) sum += tmp[r + t][c] * cyv[t];
+      for (int t = 0; t < NT; t++) sum += tmp[r + t][c] * cy[t];
       int v = (int16_t)((sum + fv.offset) >> fv.shift);
       if (fv.clip) v = clip_pel(v, maxv);
       out[r * SBW + c] = (int16_t)v;
     }
 }
+#endif
 
 // AreaBuf<Pel>::addAvg (Buffer.cpp:551-582): clip((p0 + p1 + offset) >> shiftNum)
 MM_HD int16_t add_avg(int p0, int p1, int bd) {
