@@ -111,3 +111,32 @@ def test_epipole_lookup_order():
     assert np.array_equal(o, t)
     n = 16
     assert not np.array_equal(o[:n], o[n:2 * n]) and not np.array_equal(o[n:2 * n], o[2 * n:])
+
+
+@pytest.mark.parametrize("w,h", [(256, 128), (2048, 1024), (6144, 3072)])
+def test_mpa_chroma_equals_luma_for_packet_blocks(w, h):
+    """The planner's MPA chroma->luma aliasing (mm_plan.h chroma_aliases_luma) restated on the
+    oracle: for N >= 4 the 1/32-pel chroma result equals the 1/16-pel luma result."""
+    params = mm360.seq_params(w, h, W.MPA3)
+    rng = np.random.default_rng(w)
+    rows = []
+    for i in range(400):
+        bw, bh = [int(v) for v in rng.choice([4, 8, 16, 32, 64], size=2)]
+        if (bw // 4) * (bh // 4) < 4:
+            bw, bh = 8, 8
+        x = int(rng.integers(0, (w - bw) // 8 + 1)) * 8
+        y = int(rng.integers(0, (h - bh) // 8 + 1)) * 8
+        mvh, mvv = [int(v) for v in rng.integers(-4000, 4000, size=2)]
+        m = int(rng.choice(W.MPA3))
+        rows.append((x, y, bw, bh, mvh, mvv, m, 0, 8, 0))
+        rows.append((x // 2, y // 2, bw // 2, bh // 2, mvh, mvv, m, 1, 8, 0))
+    blocks = np.array(rows, dtype=mm360.BLOCK_DTYPE)
+    r = Oracle(params, EPI).reproject(blocks)
+    off = helpers_offsets(blocks)
+    for i in range(0, len(blocks), 2):
+        assert np.array_equal(r[off[i]:off[i + 1]], r[off[i + 1]:off[i + 2]]), blocks[i]
+
+
+def helpers_offsets(blocks):
+    from helpers import block_offsets
+    return block_offsets(blocks)

@@ -146,6 +146,21 @@ class Planner {
     return MM_OK;
   }
 
+  // MPA chroma reprojection == luma reprojection, element for element, when every element of the
+  // block is a packet lane both in the luma frame cache and in the chroma block:
+  //  * the chroma grid (LinSpaced 2*xc + off + 4i) holds the luma grid values (4i + off);
+  //  * the chroma block's toPerspective (packet for N % 4 == 0) equals the frame cache entry
+  //    (packet for frame index < Nf - Nf % 4) -- same function, same inputs, same packet mode;
+  //  * the motion (mv * sign), toProjection and NaN fallback are identical;
+  //  * (x - off) * 16 == ((x - off) / 2) * 32 exactly (power-of-two scalings).
+  // So the 1/32-pel chroma result equals the 1/16-pel luma result and k_mc reads the luma job.
+  bool chroma_aliases_luma(int model, int w, int h) const {
+    if (model < MPA_FRONT_BACK || model > MPA_TOP_BOTTOM) return false;
+    const long nf = (long)(seq_.W / 4) * (seq_.H / 4);
+    const int n = (w / 4) * (h / 4);
+    return n >= 4 && n % 4 == 0 && nf % 4 == 0;
+  }
+
   // has_ref(poc) -> bool: is the reference uploaded
   template <typename HasRef>
   int plan_pus(int cur_poc, const mm_pu_desc* pus, int n, HasRef has_ref) {
@@ -177,6 +192,10 @@ class Planner {
         }
         d.ref_slot[l] = sit->second;
         for (int comp = 0; comp < (seq_.chroma ? 2 : 1); comp++) {
+          if (comp == 1 && chroma_aliases_luma(u.model[l], u.w, u.h)) {
+            d.job[l][1] = d.job[l][0];
+            continue;
+          }
           d.job[l][comp] = (int)plan_->jobs.size();
           rc = add_job(u.x, u.y, u.w >> comp, u.h >> comp, comp, u.model[l], u.mv[l][0], u.mv[l][1], cur_poc,
                        u.ref_poc[l]);
