@@ -1,10 +1,15 @@
 """Benchmark: MC+reprojection Mpixels/s on 6144x3072 ERP (BASELINE.json metric, config C3).
 
-One step = one pass of the MM motion-compensation path over one picture's PU list: the per-block
-setup, the per-sub-block reprojection of every (PU, list, component) and the 8-tap / 4-tap
-interpolation + bi-averaging of every predicted sample, for a synthetic 6144x3072 10-bit 4:2:0
-ERP picture whose PU list uses all five motion models (MPA x3, TAN, 3DT, ROT, GED_CAMPOSE).
-Inputs (reference planes, planned PU list) are resident in HBM before the timed region.
+One step = one pass of the MM motion-compensation path over one picture's PU list: device-side
+planning (PU classification + validation, job bucketing), the per-block setup, the per-sub-block
+reprojection of every (PU, list, component) and the 8-tap / 4-tap interpolation + bi-averaging
+of every predicted sample, for a synthetic 6144x3072 10-bit 4:2:0 ERP picture whose PU list uses
+all five motion models (MPA x3, TAN, 3DT, ROT, GED_CAMPOSE).  Inputs (reference planes, the PU
+descriptor list) are resident in HBM before the timed region; nothing is planned on the host.
+
+roofline: the dominant kernel is k_mc (interpolation + averaging); its algorithmic bytes (SURVEY
+8(d): 6 B uni / 9 B bi per luma pixel) over its per-launch device time, measured with HIP events
+on the context stream (mm_last_stage_timing).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
@@ -64,9 +69,7 @@ def main():
     dy = torch.zeros((cfg.height, cfg.width), dtype=torch.int16, device="cuda")
     dcb = torch.zeros((cfg.height // 2, cfg.width // 2), dtype=torch.int16, device="cuda")
     dcr = torch.zeros_like(dcb)
-    t = time.perf_counter()
-    ctx.prepare(W.CUR_POC, pus)  # host planning + descriptor upload (outside the timed region)
-    plan_ms = (time.perf_counter() - t) * 1e3
+    ctx.prepare(W.CUR_POC, pus)  # PU descriptors -> HBM (outside the timed region)
 
     for _ in range(args.warmup):
         ctx.run(dy, dcb, dcr)
@@ -92,12 +95,17 @@ def main():
     else:
         total_area = float(area)
 
-    # per-launch device time of the MC pipeline (HIP events on the context stream)
-    kms = []
+    ctx.synchronize()  # raises if the device planner rejected a PU
+    # per-launch device time of each stage (HIP events between the launches on the context stream)
+    ctx.set_stage_timing(True)
+    stages = []
     for _ in range(args.kernel_steps):
         ctx.run(dy, dcb, dcr)
-        kms.append(ctx.last_timing_ms())
-    kernel_ms = float(np.mean(kms))
+        stages.append(ctx.last_stage_timing_ms())
+    ctx.set_stage_timing(False)
+    st = np.mean(np.array(stages), axis=0)
+    kernel_ms = float(st[3])
+    pipeline_ms = float(st.sum())
 
     ms_per_step = elapsed / args.steps * 1e3
     value = total_area * args.steps / elapsed / 1e6
@@ -135,10 +143,12 @@ def main():
                        "parallelism": f"replicas x{world} (one picture per GPU)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                         "kernel": "mm_pred_run pipeline (k_setup + k_reproj + k_mc)",
-                         "kernel_ms": round(kernel_ms, 4), "algorithmic_bytes": int(alg_bytes)},
+                         "kernel": "k_mc_dev", "kernel_ms": round(kernel_ms, 4),
+                         "algorithmic_bytes": int(alg_bytes)},
+            "stages_ms": {"plan": round(float(st[0]), 4), "setup": round(float(st[1]), 4),
+                          "reproj": round(float(st[2]), 4), "mc": round(float(st[3]), 4),
+                          "pipeline": round(pipeline_ms, 4)},
             "cpu_baseline": cpu,
-            "plan_ms": round(plan_ms, 2),
         }
         print(json.dumps(line), flush=True)
     ctx.close()

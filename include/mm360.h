@@ -13,7 +13,8 @@
  *   mm_reproject     <- MVReprojection::reprojectMotionVectorSubblocks
  *                                                         SRC/MVReprojection.h:54-58
  *   mm_pred          <- InterPrediction::xPredInterBlkMM  SRC/InterPrediction.h:151-154,
- *                       batched over a picture's PU list together with xWeightedAverage
+ *   mm_pred_device      batched over a picture's PU list together with the MM dispatch of
+ *                       xPredInterUni (InterPrediction.cpp:455-533) and xWeightedAverage
  *                       (addAvg / copyClip)               SRC/InterPrediction.cpp:1584-1679
  *   mm_filter        <- InterpolationFilter::filterHor/filterVer  SRC/InterpolationFilter.h:123-128
  *   mm_destroy       <- (MVReprojection / InterPrediction destructors)
@@ -93,7 +94,7 @@ typedef struct mm_ctx mm_ctx;
 int mm_create(const mm_seq_params* params, int device, mm_ctx** out_ctx);
 int mm_destroy(mm_ctx* ctx);
 int mm_set_stream(mm_ctx* ctx, void* hip_stream);     /* hipStream_t; NULL = default stream */
-int mm_synchronize(mm_ctx* ctx);
+int mm_synchronize(mm_ctx* ctx);                      /* also reports a deferred mm_pred_device status */
 const char* mm_last_error(mm_ctx* ctx);
 int mm_get_version(void);
 
@@ -118,9 +119,23 @@ int mm_reproject(mm_ctx* ctx, const mm_block_desc* blocks, int n, int32_t* out_x
 int mm_pred(mm_ctx* ctx, int cur_poc, const mm_pu_desc* pus, int n, int16_t* dst_y,
             ptrdiff_t dst_stride_y, int16_t* dst_cb, int16_t* dst_cr, ptrdiff_t dst_stride_c);
 
-/* Split form for resident-input benchmarking: mm_pred_prepare uploads and plans the PU list
- * (kept in the context); mm_pred_run executes the prepared list (all device work, no host
- * synchronisation).  mm_pred == prepare + run. */
+/* The same with the PU list already in device memory: the whole per-picture path runs on the
+ * device -- planning (PU classification, job bucketing, prefix offsets), per-block setup,
+ * reprojection, interpolation and averaging -- as one asynchronous launch sequence on the
+ * context stream, with no host synchronisation.  Descriptor validation (the reference's CHECKs:
+ * geometry, model, reference, epipole) happens on the device; failing PUs are skipped and the
+ * lowest failing PU's code is reported by the next mm_pred_status / mm_synchronize. */
+int mm_pred_device(mm_ctx* ctx, int cur_poc, const mm_pu_desc* d_pus, int n, int16_t* dst_y,
+                   ptrdiff_t dst_stride_y, int16_t* dst_cb, int16_t* dst_cr,
+                   ptrdiff_t dst_stride_c);
+
+/* Waits for the context stream and returns the deferred status of the last device-planned
+ * call (MM_OK or the code of the lowest failing PU, whose index goes to *first_bad_pu). */
+int mm_pred_status(mm_ctx* ctx, int* first_bad_pu);
+
+/* Split form for resident-input benchmarking: mm_pred_prepare copies the PU list into the
+ * context's device buffer; mm_pred_run runs mm_pred_device on it (all device work, no host
+ * synchronisation).  mm_pred == prepare + run + mm_pred_status. */
 int mm_pred_prepare(mm_ctx* ctx, int cur_poc, const mm_pu_desc* pus, int n);
 int mm_pred_run(mm_ctx* ctx, int16_t* dst_y, ptrdiff_t dst_stride_y, int16_t* dst_cb,
                 int16_t* dst_cr, ptrdiff_t dst_stride_c);
@@ -133,8 +148,15 @@ int mm_filter(mm_ctx* ctx, int comp, int vertical, const int16_t* src, ptrdiff_t
               int16_t* dst, ptrdiff_t dst_stride, int w, int h, int frac, int is_first,
               int is_last);
 
-/* Kernel timing of the last mm_pred_run (HIP events on the context stream), milliseconds. */
+/* Device time of the last mm_pred_device / mm_pred_run launch sequence (HIP events on the
+ * context stream around all of its launches), milliseconds. */
 int mm_last_timing(mm_ctx* ctx, float* ms_total);
+
+/* Per-stage device time of the last launch sequence, recorded only while stage timing is on
+ * (extra events between the launches): ms[0] planning (memset + k_plan_count + k_plan_place),
+ * ms[1] k_setup, ms[2] k_reproj, ms[3] k_mc. */
+int mm_set_stage_timing(mm_ctx* ctx, int on);
+int mm_last_stage_timing(mm_ctx* ctx, float ms[4]);
 
 #ifdef __cplusplus
 }

@@ -1,11 +1,13 @@
 // host_twin.cpp -- CPU twin of the device pipeline (TEST UTILITY).
 //
-// Runs the product's per-thread bodies (vvc-extension-mm_amd/csrc/mm_pipeline.h) and planner
-// (mm_plan.h) in host loops, compiled by g++ with the same no-contraction rules as the HIP
+// Runs the product's per-thread bodies (vvc-extension-mm_amd/csrc/mm_pipeline.h) and planners
+// (mm_plan.h host plan of mm_reproject, mm_devplan.h device plan of mm_pred) in host loops, compiled by g++ with the same no-contraction rules as the HIP
 // build.  The CPU test suite compares it against the oracle, which checks the device logic
 // without a GPU; the GPU suite then checks the HIP library itself.
 //   g++ -O2 -std=c++17 -ffp-contract=off -fopenmp -fPIC -shared host_twin.cpp -o libhosttwin.so
+#include <algorithm>
 #include <cmath>
+#include <string>
 #include <vector>
 
 #include "mm_plan.h"
@@ -91,33 +93,67 @@ extern "C" int twin_reproject(const mm_seq_params* p, int n_epi, const int32_t* 
   return 0;
 }
 
+// Device-planned prediction (mm_pred_device), run sequentially: classify every PU, count per
+// bucket, place PUs/jobs with per-bucket cursors (arrival order = list order), then the setup /
+// reprojection / MC bodies over the planned lists.
 extern "C" int twin_pred(const mm_seq_params* p, int n_epi, const int32_t* epi, int cur_poc, const mm_pu_desc* pus,
                          int n, int n_refs, const int32_t* pocs, const int16_t* const* ys, const int16_t* const* cbs,
                          const int16_t* const* crs, int stride_y, int stride_c, int16_t* dy, int sdy, int16_t* dcb,
                          int16_t* dcr, int sdc) {
+  using namespace mmdev;
   Twin t;
   make_twin(p, &t);
-  Plan plan;
   EpipoleMap em = epi_of(n_epi, epi);
-  Planner pl(seq_info(*p), em, &plan);
-  auto has = [&](int poc) {
-    for (int i = 0; i < n_refs; i++)
-      if (pocs[i] == poc) return true;
-    return false;
-  };
-  int rc = pl.plan_pus(cur_poc, pus, n, has);
+  std::vector<std::pair<int, RefDev>> refs;
+  for (int i = 0; i < n_refs; i++)
+    refs.emplace_back(pocs[i], RefDev{ys[i], cbs ? cbs[i] : nullptr, crs ? crs[i] : nullptr, stride_y, stride_c});
+  std::sort(refs.begin(), refs.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+  PicTables tab;
+  std::string err;
+  int rc = build_pic_tables(seq_info(*p), em, cur_poc, refs, &tab, &err);
   if (rc) return rc;
-  std::vector<RefDev> refs;
-  for (int poc : plan.ref_pocs)
-    for (int i = 0; i < n_refs; i++)
-      if (pocs[i] == poc) refs.push_back(RefDev{ys[i], cbs ? cbs[i] : nullptr, crs ? crs[i] : nullptr, stride_y, stride_c});
-  std::vector<int32_t> r;
-  run_reproj(t, plan, &r);
-  const Taps taps{LUMA_T, CHROMA_T};
-  const int npu = (int)plan.pus.size();
+  std::vector<PuPlan> plans(n);
+  PlanCounters cnt{};
+  for (int i = 0; i < n; i++) {
+    classify_pu(pus[i], tab, &plans[i]);
+    if (plans[i].code) return plans[i].code;
+    cnt.pu_tot[plans[i].cls] += pack_count(1, plans[i].n_sb);
+    for (int k = 0; k < 4; k++)
+      if (plans[i].job[k].valid) cnt.job_tot[plans[i].job[k].key] += pack_count(1, plans[i].job[k].n);
+  }
+  PlanMeta m;
+  plan_meta(cnt, &m);
+  std::vector<PuDev> dpus(m.n_pus);
+  std::vector<int> pu_off(m.n_pus), pu_chunk(m.n_sb / 64 + 1);
+  std::vector<JobDev> jobs(m.n_jobs);
+  std::vector<int> job_off(m.n_jobs), job_chunk(m.n_elems / 64 + 1);
+  for (int i = 0; i < n; i++) {
+    const PuPlan& pp = plans[i];
+    const unsigned long long bp = cnt.pu_cur[pp.cls];
+    cnt.pu_cur[pp.cls] += pack_count(1, pp.n_sb);
+    int jidx[4] = {0, 0, 0, 0}, joff[4] = {0, 0, 0, 0};
+    for (int k = 0; k < 4; k++) {
+      if (!pp.job[k].valid) continue;
+      const int key = pp.job[k].key;
+      jidx[k] = m.job_base[key] + packed_items(cnt.job_cur[key]);
+      joff[k] = m.elem_base[key] + packed_elems(cnt.job_cur[key]);
+      cnt.job_cur[key] += pack_count(1, pp.job[k].n);
+    }
+    emit_pu(pus[i], pp, m.pu_base[pp.cls] + packed_items(bp), m.sb_base[pp.cls] + packed_elems(bp), jidx, joff,
+            dpus.data(), pu_off.data(), pu_chunk.data(), jobs.data(), job_off.data(), job_chunk.data());
+  }
+  std::vector<BlockSetup> setups(m.n_jobs);
+#pragma omp parallel for schedule(static)
+  for (int i = 0; i < m.n_jobs; i++) setup_thread(i, t.sc, jobs.data(), tab.ged, setups.data());
+  std::vector<int32_t> r(2 * (size_t)std::max(m.n_elems, 1));
+  MpaCache c = cache_of(t);
 #pragma omp parallel for schedule(static, 256)
-  for (int g = 0; g < plan.n_sb; g++)
-    mc_thread(g, t.geo, taps, plan.pus.data(), npu, plan.pu_off.data(), plan.pu_chunk.data(), plan.jobs.data(),
-              r.data(), refs.data(), dy, sdy, dcb, dcr, sdc);
+  for (int g = 0; g < m.n_elems; g++)
+    reproj_thread(g, t.sc, jobs.data(), m.n_jobs, job_off.data(), job_chunk.data(), setups.data(), c, r.data());
+  const Taps taps{LUMA_T, CHROMA_T};
+#pragma omp parallel for schedule(static, 256)
+  for (int g = 0; g < m.n_sb; g++)
+    mc_thread(g, t.geo, taps, dpus.data(), m.n_pus, pu_off.data(), pu_chunk.data(), jobs.data(), r.data(), tab.ref,
+              dy, sdy, dcb, dcr, sdc);
   return 0;
 }

@@ -185,8 +185,10 @@ def test_error_paths():
     params = mm360.seq_params(cfg.width, cfg.height, W.MPA3 + (mm360.GEODESIC_CAMPOSE,))
     pus = W.pu_list(cfg)
     with mm360.MMContext(params) as ctx:
+        dy = torch.zeros((cfg.height, cfg.width), dtype=torch.int16, device="cuda")
+        dc = torch.zeros((cfg.height // 2, cfg.width // 2), dtype=torch.int16, device="cuda")
         with pytest.raises(mm360.MMError) as e:
-            ctx.prepare(W.CUR_POC, pus)  # no references uploaded
+            ctx.predict(W.CUR_POC, pus, dy, dc, dc.clone())  # no references uploaded
         assert e.value.code == mm360.MM_ERR_NOREF
         blk = np.array([(0, 0, 16, 16, 16, 16, mm360.GEODESIC_CAMPOSE, 0, 8, 0)], dtype=mm360.BLOCK_DTYPE)
         with pytest.raises(mm360.MMError) as e:
@@ -201,3 +203,94 @@ def test_error_paths():
         with pytest.raises(mm360.MMError) as e:
             ctx.reproject(blk)  # outside the picture
         assert e.value.code == mm360.MM_ERR_ARG
+
+
+def _planes(cfg, fill=0):
+    dy = torch.full((cfg.height, cfg.width), fill, dtype=torch.int16, device="cuda")
+    dcb = torch.full((cfg.height // 2, cfg.width // 2), fill, dtype=torch.int16, device="cuda")
+    return dy, dcb, torch.full_like(dcb, fill)
+
+
+@pytest.mark.parametrize("cfg_name", ["C2", "C3"])
+def test_pred_device_resident_list_vs_oracle(cfg_name):
+    """mm_pred_device on a PU list already in HBM (device planning) == the oracle, bit-exact."""
+    cfg = W.CONFIGS[cfg_name]
+    params = mm360.seq_params(cfg.width, cfg.height, cfg.models)
+    pus = W.pu_list(cfg, frame=3)
+    refs = {poc: W.ref_planes(cfg.width, cfg.height, poc) for poc in W.REF_POCS}
+    orc = Oracle(params, EPI)
+    want = orc.predict(W.CUR_POC, pus, refs, cfg.width, cfg.height)
+    with _ctx(params) as ctx:
+        for poc, (y, cb, cr) in refs.items():
+            ctx.upload_ref(poc, torch.from_numpy(y).cuda(), torch.from_numpy(cb).cuda(), torch.from_numpy(cr).cuda())
+        d_pus = mm360.pus_to_device(pus)
+        dst = _planes(cfg, -7)
+        ctx.predict_device(W.CUR_POC, d_pus, *dst)
+        assert ctx.status() == (mm360.MM_OK, -1)
+    for x, t, name in zip(want, dst, ("y", "cb", "cr")):
+        got = t.cpu().numpy()
+        assert np.array_equal(got, x), describe_mismatch(name, got, x)
+
+
+def test_device_validation_reports_lowest_failing_pu():
+    """Device-side CHECKs: a bad PU is skipped and reported (lowest index first); the rest of the
+    picture is still predicted exactly."""
+    cfg = W.CONFIGS["C1"]
+    params = mm360.seq_params(cfg.width, cfg.height, W.MPA3 + (mm360.GEODESIC_CAMPOSE,))
+    pus = W.pu_list(cfg)
+    refs = {poc: W.ref_planes(cfg.width, cfg.height, poc) for poc in W.REF_POCS}
+    orc = Oracle(params, EPI)
+    want = orc.predict(W.CUR_POC, pus, refs, cfg.width, cfg.height)
+
+    def broken(k, field, value, ctx_epi=True):
+        bad = pus.copy()
+        if field == "x":
+            bad[k]["x"] = value
+        elif field == "model":
+            bad[k]["model"][0] = value
+            bad[k]["ref_poc"][0] = 0
+        elif field == "ref_poc":
+            bad[k]["ref_poc"][0] = value
+            bad[k]["model"][0] = 1
+        elif field == "nolist":
+            bad[k]["ref_poc"][:] = -1
+        return bad
+
+    cases = [(37, "x", 2, mm360.MM_ERR_ARG), (11, "model", mm360.CLASSIC, mm360.MM_ERR_MODEL),
+             (5, "model", mm360.TANGENTIAL, mm360.MM_ERR_MODEL), (20, "ref_poc", 99, mm360.MM_ERR_NOREF),
+             (3, "nolist", 0, mm360.MM_ERR_ARG)]
+    with _ctx(params) as ctx:
+        for poc, (y, cb, cr) in refs.items():
+            ctx.upload_ref(poc, torch.from_numpy(y).cuda(), torch.from_numpy(cb).cuda(), torch.from_numpy(cr).cuda())
+        for k, field, value, code in cases:
+            bad = broken(k, field, value)
+            bad2 = broken(k + 40, field, value) if k + 40 < len(pus) else bad
+            both = bad.copy()
+            both[k + 40:k + 41] = bad2[k + 40:k + 41]
+            dst = _planes(cfg)
+            ctx.predict_device(W.CUR_POC, mm360.pus_to_device(both), *dst)
+            rc, first = ctx.status()
+            assert (rc, first) == (code, k), (field, rc, first)
+            # every PU except the broken ones is predicted exactly
+            got = dst[0].cpu().numpy()
+            mask = np.ones_like(got, dtype=bool)
+            for j in (k, k + 40):
+                u = pus[j]
+                mask[u["y"]:u["y"] + u["h"], u["x"]:u["x"] + u["w"]] = False
+            assert np.array_equal(got[mask], want[0][mask])
+        # GED camera pose without an epipole for (8, 0)
+        g = pus.copy()
+        g[9]["model"][:] = mm360.GEODESIC_CAMPOSE
+    with mm360.MMContext(params) as ctx:  # no epipoles set
+        for poc, (y, cb, cr) in refs.items():
+            ctx.upload_ref(poc, y, cb, cr)
+        dst = _planes(cfg)
+        ctx.predict_device(W.CUR_POC, mm360.pus_to_device(g), *dst)
+        assert ctx.status() == (mm360.MM_ERR_NOEPIPOLE, 9)
+        # over capacity: the same list three times covers the picture 3x
+        ctx.predict_device(W.CUR_POC, mm360.pus_to_device(np.concatenate([pus] * 3)), *dst)
+        rc, _ = ctx.status()
+        assert rc == mm360.MM_ERR_ARG
+        # empty list is a no-op
+        ctx.predict_device(W.CUR_POC, mm360.pus_to_device(pus[:0]), *dst)
+        assert ctx.status() == (mm360.MM_OK, -1)

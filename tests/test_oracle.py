@@ -115,7 +115,7 @@ def test_epipole_lookup_order():
 
 @pytest.mark.parametrize("w,h", [(256, 128), (2048, 1024), (6144, 3072)])
 def test_mpa_chroma_equals_luma_for_packet_blocks(w, h):
-    """The planner's MPA chroma->luma aliasing (mm_plan.h chroma_aliases_luma) restated on the
+    """The planner's MPA chroma->luma aliasing (mm_devplan.h mpa_chroma_aliases) restated on the
     oracle: for N >= 4 the 1/32-pel chroma result equals the 1/16-pel luma result."""
     params = mm360.seq_params(w, h, W.MPA3)
     rng = np.random.default_rng(w)

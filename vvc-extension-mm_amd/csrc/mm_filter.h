@@ -169,59 +169,86 @@ __device__ __forceinline__ int dot2_(uint32_t a, uint32_t b, int c) {
 __device__ __forceinline__ uint32_t pack2_(int lo, int hi) {
   return ((uint32_t)lo & 0xffffu) | ((uint32_t)hi << 16);
 }
-// predict_subblock for an interior window (device): same arithmetic, samples handled as packed
-// int16 pairs -- each tap pair is one v_dot2c_i32_i16.
+__device__ __forceinline__ uint32_t pack_lo16_(uint32_t lo, uint32_t hi) {
+  return __builtin_amdgcn_perm(hi, lo, 0x05040100u);  // (lo & 0xffff) | (hi << 16), one v_perm_b32
+}
+// predict_subblock for an interior window (device): the same integer sums, regrouped as packed
+// int16 pairs so that each pair of taps is one v_dot2c_i32_i16:
+//  * a window row is loaded as dwords from the even sample below it; e[m] = samples (2m, 2m+1)
+//    (one v_alignbit when the window starts on an odd sample);
+//  * even outputs use the sample pairs e[] with the tap pairs (f0,f1), (f2,f3), ...; odd outputs
+//    use the same sample pairs with the shifted tap pairs (0,f0), (f1,f2), ..., (f_{N-1},0);
+//  * the rounding offsets seed the dot2 accumulators; the H outputs (Pel, 16 bits) are packed
+//    row pairs (one v_perm each) for the vertical pass, which uses the same even/odd tap trick.
 template <int NT, int SBW, int SBH>
 __device__ __forceinline__ void predict_subblock_interior(const int16_t* __restrict__ ref, int stride, int xPos, int yPos,
                                                           const int8_t* cx, const int8_t* cy, bool bi, int bd,
                                                           int16_t* out) {
   constexpr int L = SBW + NT - 1, R = SBH + NT - 1, H0 = NT / 2 - 1;
-  constexpr int ND = (L + 2) / 2;  // dwords loaded per row
-  constexpr int NP = NT / 2;       // tap pairs
+  constexpr int ND = (L + 2) / 2;  // dwords loaded per row (L + 1 samples from the even base)
+  constexpr int NP = NT / 2;       // tap pairs of an even output
+  constexpr int NQ = NP + 1;       // shifted tap pairs of an odd output
+  constexpr int RP = (R + 1) / 2;  // packed H-output row pairs
   const int maxv = (1 << bd) - 1;
   const FiltParam fh = filt_param(true, false, bd);
   const FiltParam fv = filt_param(false, !bi, bd);
-  uint32_t ch[NP], cv[NP];
+  uint32_t he[NP], ho[NQ], ve[NP], vo[NQ];
 #pragma unroll
   for (int k = 0; k < NP; k++) {
-    ch[k] = pack2_(cx[2 * k], cx[2 * k + 1]);
-    cv[k] = pack2_(cy[2 * k], cy[2 * k + 1]);
+    he[k] = pack2_(cx[2 * k], cx[2 * k + 1]);
+    ve[k] = pack2_(cy[2 * k], cy[2 * k + 1]);
   }
+  ho[0] = pack2_(0, cx[0]);
+  vo[0] = pack2_(0, cy[0]);
+#pragma unroll
+  for (int k = 1; k < NP; k++) {
+    ho[k] = pack2_(cx[2 * k - 1], cx[2 * k]);
+    vo[k] = pack2_(cy[2 * k - 1], cy[2 * k]);
+  }
+  ho[NP] = pack2_(cx[NT - 1], 0);
+  vo[NP] = pack2_(cy[NT - 1], 0);
   const int x0 = xPos - H0;
   const uint32_t sh = (x0 & 1) ? 16u : 0u;
-  int tmp[R][SBW];
+  uint32_t tmp[R + 1][SBW];  // H outputs; only the low 16 bits are used
+#pragma unroll
+  for (int c = 0; c < SBW; c++) tmp[R][c] = 0u;
 #pragma unroll
   for (int r = 0; r < R; r++) {
     const uint32_t* p = reinterpret_cast<const uint32_t*>(ref + (long)(yPos + r - H0) * stride + (x0 & ~1));
     uint32_t d[ND];
     load_dwords<ND>(p, d);
-    // e[m] = window samples (2m, 2m+1), o[m] = (2m+1, 2m+2); the last e only needs its low half
-    uint32_t e[ND], o[ND - 1];
+    uint32_t e[ND];
 #pragma unroll
     for (int m = 0; m < ND; m++) e[m] = __builtin_amdgcn_alignbit(m + 1 < ND ? d[m + 1] : 0u, d[m], sh);
 #pragma unroll
-    for (int m = 0; m < ND - 1; m++) o[m] = __builtin_amdgcn_alignbit(e[m + 1], e[m], 16u);
-#pragma unroll
     for (int c = 0; c < SBW; c++) {
-      int sum = 0;
+      int sum = fh.offset;
+      if (c & 1) {
 #pragma unroll
-      for (int k = 0; k < NP; k++) sum = dot2_((c & 1) ? o[(c >> 1) + k] : e[(c >> 1) + k], ch[k], sum);
-      tmp[r][c] = (int16_t)((sum + fh.offset) >> fh.shift);
+        for (int k = 0; k < NQ; k++) sum = dot2_(e[(c >> 1) + k], ho[k], sum);
+      } else {
+#pragma unroll
+        for (int k = 0; k < NP; k++) sum = dot2_(e[(c >> 1) + k], he[k], sum);
+      }
+      tmp[r][c] = (uint32_t)(sum >> fh.shift);
     }
   }
 #pragma unroll
   for (int c = 0; c < SBW; c++) {
-    uint32_t pe[(R + 1) / 2], po[R / 2];  // row pairs (2m, 2m+1) and (2m+1, 2m+2)
+    uint32_t pr[RP];  // rows (2m, 2m+1)
 #pragma unroll
-    for (int m = 0; m < (R + 1) / 2; m++) pe[m] = pack2_(tmp[2 * m][c], 2 * m + 1 < R ? tmp[2 * m + 1][c] : 0);
-#pragma unroll
-    for (int m = 0; m < R / 2; m++) po[m] = pack2_(tmp[2 * m + 1][c], 2 * m + 2 < R ? tmp[2 * m + 2][c] : 0);
+    for (int m = 0; m < RP; m++) pr[m] = pack_lo16_(tmp[2 * m][c], tmp[2 * m + 1][c]);
 #pragma unroll
     for (int r = 0; r < SBH; r++) {
-      int sum = 0;
+      int sum = fv.offset;
+      if (r & 1) {
 #pragma unroll
-      for (int k = 0; k < NP; k++) sum = dot2_((r & 1) ? po[(r >> 1) + k] : pe[(r >> 1) + k], cv[k], sum);
-      int v = (int16_t)((sum + fv.offset) >> fv.shift);
+        for (int k = 0; k < NQ; k++) sum = dot2_(pr[(r >> 1) + k], vo[k], sum);
+      } else {
+#pragma unroll
+        for (int k = 0; k < NP; k++) sum = dot2_(pr[(r >> 1) + k], ve[k], sum);
+      }
+      int v = (int16_t)(sum >> fv.shift);
       if (fv.clip) v = clip_pel(v, maxv);
       out[r * SBW + c] = (int16_t)v;
     }

@@ -1,7 +1,9 @@
 // mm_kernels.hip -- gfx950 kernels and the C-ABI (include/mm360.h) of the 360-degree
 // multi-model motion-compensation path.
 //
-// Pipeline of one mm_pred_run (one picture's PU list, all device work, one stream):
+// Pipeline of one mm_pred_device (one picture's PU list, all device work, one stream):
+//   k_plan_count / k_plan_place   device planning (mm_devplan.h): PU classification and
+//              validation, class-sorted PUs, (component, model, packet)-sorted jobs.
 //   k_setup    thread per reprojection job (PU x list x {luma, chroma}): the per-block part of
 //              reprojectMotionVectorSubblocks (centre transforms, rotation matrices, k, ...).
 //   k_reproj   thread per sub-block element of every job: <Model>::modelMotion[Cached] + NaN
@@ -9,6 +11,8 @@
 //   k_mc       thread per luma 4x4 sub-block of every PU: for each used list, the 8-tap luma and
 //              4-tap 4:2:0 chroma sub-block predictions (xPredInterBlkMM :776-828) and the
 //              addAvg / uni output (xWeightedAverage), written straight into the picture planes.
+// (k_setup / k_reproj also serve the parity API mm_reproject on a host-planned block list; the
+// _dev variants read their sizes from the device plan.)
 // Reference planes stay resident in HBM, unpadded; the edge-replication margin of the reference
 // is realised by address clamping (identical results, no padded copies).
 #include <hip/hip_runtime.h>
@@ -57,15 +61,151 @@ __global__ void __launch_bounds__(256) k_reproj(SeqConst sc, const JobDev* __res
   reproj_thread(g, sc, jobs, n_jobs, job_offsets, chunk_start, setups, cache, out);
 }
 
-__global__ void __launch_bounds__(256) k_mc(Geometry geo, const PuDev* __restrict__ pus, int n_pus,
-                                            const int* __restrict__ pu_offsets, const int* __restrict__ chunk_start,
-                                            int n_sb, const JobDev* __restrict__ jobs, const int32_t* __restrict__ reproj,
-                                            const RefDev* __restrict__ refs, int16_t* __restrict__ dst_y, int dsy,
-                                            int16_t* __restrict__ dst_cb, int16_t* __restrict__ dst_cr, int dsc) {
-  int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= n_sb) return;
+// --------------------------------------------------------------------------------------------
+// Device-planned picture path (mm_pred_device): k_plan_count -> k_plan_place -> k_setup_dev ->
+// k_reproj_dev -> k_mc_dev, sizes from PlanMeta (mm_devplan.h).
+// --------------------------------------------------------------------------------------------
+using namespace mmdev;
+
+// Buffer capacities of the device plan (the host sizes them; k_plan_place enforces them).
+struct PlanCaps {
+  int pus, sb, jobs, elems;
+};
+
+// Workgroups are dispatched round-robin over the 8 XCDs, each with its own L2.  Within every
+// group of 8 * XCD_RUN consecutive workgroups, renumbering them XCD-major hands each XCD a run of
+// XCD_RUN adjacent workgroups, so neighbouring PUs (overlapping reference windows) share one L2.
+// Groups stay small so that the work of every region still spreads over all XCDs (a static
+// 1/8 split of the whole grid would load one XCD with the most expensive model bucket).
+// Requires gridDim.x % (8 * XCD_RUN) == 0; the grids are sized by the plan capacities and
+// workgroups past the device-known totals exit at once.
+constexpr int XCD_RUN = 4;
+__device__ __forceinline__ int xcd_block() {
+  const int b = blockIdx.x, grp = b / (8 * XCD_RUN), r = b % (8 * XCD_RUN);
+  return grp * (8 * XCD_RUN) + (r & 7) * XCD_RUN + (r >> 3);
+}
+
+__global__ void __launch_bounds__(256) k_plan_count(const mm_pu_desc* __restrict__ pus, int n, const PicTables t,
+                                                    PlanCounters* __restrict__ cnt) {
+  __shared__ unsigned long long s_pu[N_PU_KEYS], s_job[N_JOB_KEYS], s_status;
+  const int tid = threadIdx.x;
+  if (tid < N_PU_KEYS) s_pu[tid] = 0;
+  if (tid < N_JOB_KEYS) s_job[tid] = 0;
+  if (tid == 0) s_status = 0;
+  __syncthreads();
+  const int i = blockIdx.x * blockDim.x + tid;
+  if (i < n) {
+    const mm_pu_desc u = pus[i];
+    PuPlan p;
+    classify_pu(u, t, &p);
+    if (p.code != MM_OK) {
+      atomicMax(&s_status, status_word(i, p.code));
+    } else {
+      atomicAdd(&s_pu[p.cls], pack_count(1, p.n_sb));
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if (p.job[k].valid) atomicAdd(&s_job[p.job[k].key], pack_count(1, p.job[k].n));
+    }
+  }
+  __syncthreads();
+  if (tid < N_PU_KEYS && s_pu[tid]) atomicAdd(&cnt->pu_tot[tid], s_pu[tid]);
+  if (tid < N_JOB_KEYS && s_job[tid]) atomicAdd(&cnt->job_tot[tid], s_job[tid]);
+  if (tid == 0 && s_status) atomicMax(&cnt->status, s_status);
+}
+
+__global__ void __launch_bounds__(256) k_plan_place(const mm_pu_desc* __restrict__ pus, int n, const PicTables t,
+                                                    PlanCounters* __restrict__ cnt, PlanMeta* __restrict__ meta,
+                                                    PlanCaps caps, PuDev* __restrict__ d_pus, int* __restrict__ pu_off,
+                                                    int* __restrict__ pu_chunk, JobDev* __restrict__ jobs,
+                                                    int* __restrict__ job_off, int* __restrict__ job_chunk) {
+  __shared__ unsigned long long s_pu[N_PU_KEYS], s_job[N_JOB_KEYS];
+  __shared__ unsigned long long g_pu[N_PU_KEYS], g_job[N_JOB_KEYS];
+  __shared__ PlanMeta s_meta;
+  __shared__ int s_ok;
+  const int tid = threadIdx.x;
+  if (tid < N_PU_KEYS) s_pu[tid] = 0;
+  if (tid < N_JOB_KEYS) s_job[tid] = 0;
+  if (tid == 0) {
+    plan_meta(*cnt, &s_meta);
+    s_ok = s_meta.n_pus <= caps.pus && s_meta.n_sb <= caps.sb && s_meta.n_jobs <= caps.jobs &&
+           s_meta.n_elems <= caps.elems;
+    if (blockIdx.x == 0) {
+      PlanMeta m = s_meta;
+      if (!s_ok) {  // over capacity (overlapping PUs): nothing is predicted, the call fails
+        m.n_pus = m.n_sb = m.n_jobs = m.n_elems = 0;
+        atomicMax(&cnt->status, status_word(0, MM_ERR_ARG));
+      }
+      *meta = m;
+    }
+  }
+  __syncthreads();
+  if (!s_ok) return;
+  const int i = blockIdx.x * blockDim.x + tid;
+  PuPlan p;
+  p.code = MM_ERR_ARG;
+  mm_pu_desc u;
+  unsigned long long lp = 0, lj[4] = {0, 0, 0, 0};
+  if (i < n) {
+    u = pus[i];
+    classify_pu(u, t, &p);
+    if (p.code == MM_OK) {
+      lp = atomicAdd(&s_pu[p.cls], pack_count(1, p.n_sb));
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if (p.job[k].valid) lj[k] = atomicAdd(&s_job[p.job[k].key], pack_count(1, p.job[k].n));
+    }
+  }
+  __syncthreads();
+  if (tid < N_PU_KEYS && s_pu[tid]) g_pu[tid] = atomicAdd(&cnt->pu_cur[tid], s_pu[tid]);
+  if (tid < N_JOB_KEYS && s_job[tid]) g_job[tid] = atomicAdd(&cnt->job_cur[tid], s_job[tid]);
+  __syncthreads();
+  if (p.code != MM_OK) return;
+  const unsigned long long bp = g_pu[p.cls] + lp;
+  const int pu_idx = s_meta.pu_base[p.cls] + packed_items(bp);
+  const int sb_off = s_meta.sb_base[p.cls] + packed_elems(bp);
+  int jidx[4], joff[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    jidx[k] = joff[k] = 0;
+    if (p.job[k].valid) {
+      const int key = p.job[k].key;
+      const unsigned long long bj = g_job[key] + lj[k];
+      jidx[k] = s_meta.job_base[key] + packed_items(bj);
+      joff[k] = s_meta.elem_base[key] + packed_elems(bj);
+    }
+  }
+  emit_pu(u, p, pu_idx, sb_off, jidx, joff, d_pus, pu_off, pu_chunk, jobs, job_off, job_chunk);
+}
+
+__global__ void __launch_bounds__(256) k_setup_dev(SeqConst sc, const PlanMeta* __restrict__ meta,
+                                                   const JobDev* __restrict__ jobs, const PicTables t,
+                                                   BlockSetup* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= meta->n_jobs) return;
+  setup_thread(i, sc, jobs, t.ged, out);
+}
+
+__global__ void __launch_bounds__(256) k_reproj_dev(SeqConst sc, const PlanMeta* __restrict__ meta,
+                                                    const JobDev* __restrict__ jobs, const int* __restrict__ job_offsets,
+                                                    const int* __restrict__ chunk_start,
+                                                    const BlockSetup* __restrict__ setups, MpaCache cache,
+                                                    int32_t* __restrict__ out) {
+  const int g = xcd_block() * blockDim.x + threadIdx.x;
+  if (g >= meta->n_elems) return;
+  reproj_thread(g, sc, jobs, meta->n_jobs, job_offsets, chunk_start, setups, cache, out);
+}
+
+__global__ void __launch_bounds__(256) k_mc_dev(Geometry geo, const PlanMeta* __restrict__ meta,
+                                                const PuDev* __restrict__ pus, const int* __restrict__ pu_offsets,
+                                                const int* __restrict__ chunk_start, const JobDev* __restrict__ jobs,
+                                                const int32_t* __restrict__ reproj, const PicTables t,
+                                                int16_t* __restrict__ dst_y, int dsy, int16_t* __restrict__ dst_cb,
+                                                int16_t* __restrict__ dst_cr, int dsc) {
+  const int g = xcd_block() * blockDim.x + threadIdx.x;
+  if (g >= meta->n_sb) return;
   const Taps taps{c_luma_taps, c_chroma_taps};
-  mc_thread(g, geo, taps, pus, n_pus, pu_offsets, chunk_start, jobs, reproj, refs, dst_y, dsy, dst_cb, dst_cr, dsc);
+  mc_thread(g, geo, taps, pus, meta->n_pus, pu_offsets, chunk_start, jobs, reproj, t.ref, dst_y, dsy, dst_cb, dst_cr,
+            dsc);
 }
 
 // InterpolationFilter::filter<N, isVertical, isFirst, isLast> / filterCopy on a raw block
@@ -147,17 +287,27 @@ struct mm_ctx {
   float* mpa_px[3] = {nullptr, nullptr, nullptr};
   float* mpa_py[3] = {nullptr, nullptr, nullptr};
   uint8_t* mpa_vip[3] = {nullptr, nullptr, nullptr};
-  Plan plan;
+  Plan plan;  // host plan of the parity API mm_reproject
   DevBuf<JobDev> d_jobs;
   DevBuf<int> d_job_off, d_job_chunk, d_pu_off, d_pu_chunk;
   DevBuf<BlockSetup> d_setup;
   DevBuf<int32_t> d_reproj;
   DevBuf<PuDev> d_pus;
-  DevBuf<RefDev> d_refs;
   DevBuf<M3> d_ged;
+  // device-planned prediction (mm_pred_device / mm_pred_run)
+  DevBuf<mm_pu_desc> d_pu_in;  // PU list copied in by mm_pred / mm_pred_prepare
+  DevBuf<PlanCounters> d_cnt;
+  DevBuf<PlanMeta> d_meta;
+  PlanCaps caps{};
+  int prep_poc = 0, prep_n = 0;
   bool prepared = false;
+  bool status_pending = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool stage_timing = false;
+  hipEvent_t ev_stage[3] = {nullptr, nullptr, nullptr};  // after planning, setup, reprojection
 };
+
+static int read_status(mm_ctx* c, int* first_bad);
 
 static int fail(mm_ctx* c, int code, const std::string& msg) {
   if (c) c->err = msg;
@@ -251,7 +401,9 @@ int mm_create(const mm_seq_params* p, int device, mm_ctx** out_ctx) {
   c->geo.maxCUwc = p->max_cu_width >> 1;
   c->geo.maxCUhc = p->max_cu_height >> 1;
   c->geo.bd = p->bit_depth;
-  if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+  if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+      hipEventCreate(&c->ev_stage[0]) != hipSuccess || hipEventCreate(&c->ev_stage[1]) != hipSuccess ||
+      hipEventCreate(&c->ev_stage[2]) != hipSuccess) {
     mm_destroy(c);
     return MM_ERR_HIP;
   }
@@ -297,8 +449,12 @@ int mm_destroy(mm_ctx* c) {
   c->d_setup.release();
   c->d_reproj.release();
   c->d_pus.release();
-  c->d_refs.release();
+  c->d_pu_in.release();
+  c->d_cnt.release();
+  c->d_meta.release();
   c->d_ged.release();
+  for (auto& e : c->ev_stage)
+    if (e) (void)hipEventDestroy(e);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   delete c;
@@ -313,8 +469,7 @@ int mm_set_stream(mm_ctx* c, void* s) {
 
 int mm_synchronize(mm_ctx* c) {
   if (!c) return MM_ERR_ARG;
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  return MM_OK;
+  return read_status(c, nullptr);
 }
 
 int mm_set_epipole(mm_ctx* c, int cur, int ref, const int32_t q24[3]) {
@@ -346,7 +501,6 @@ int mm_upload_ref(mm_ctx* c, int poc, const int16_t* y, ptrdiff_t sy, const int1
     HIPCHK(c, hipMemcpy2DAsync(r.cr, r.stride_c * 2, cr, sc_ * 2, Wc * 2, Hc, k, c->stream));
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  c->prepared = false;  // slot pointers may have changed
   return MM_OK;
 }
 
@@ -359,14 +513,12 @@ int mm_release_ref(mm_ctx* c, int poc) {
   (void)hipFree(it->second.cb);
   (void)hipFree(it->second.cr);
   c->refs.erase(it);
-  c->prepared = false;
   return MM_OK;
 }
 
 int mm_reproject(mm_ctx* c, const mm_block_desc* blocks, int n, int32_t* out_xy) {
   if (!c || n < 0 || (n > 0 && (!blocks || !out_xy))) return MM_ERR_ARG;
   HIPCHK(c, hipSetDevice(c->device));
-  c->prepared = false;
   Planner pl(seq_info(c->prm), c->epipoles, &c->plan);
   int rc = pl.plan_blocks(blocks, n);
   if (rc) return fail(c, rc, c->plan.err);
@@ -379,24 +531,112 @@ int mm_reproject(mm_ctx* c, const mm_block_desc* blocks, int n, int32_t* out_xy)
   return MM_OK;
 }
 
+// ---- device-planned prediction ----------------------------------------------------------
+
+static int round_grid(long v) { return (int)((v + 8 * XCD_RUN - 1) / (8 * XCD_RUN) * (8 * XCD_RUN)); }
+
+// Buffers for a PU list of n entries: a PU list predicts each luma sample of the picture at most
+// once, so sub-blocks are bounded by the picture's sub-block count (and by n * 1024, 128x128
+// PUs); a PU has at most 4 jobs and 4 reprojection elements per luma sub-block (2 lists x
+// {luma, chroma}).  k_plan_place refuses a list beyond these capacities (overlapping PUs).
+static int ensure_plan_buffers(mm_ctx* c, int n) {
+  PlanCaps k;
+  k.pus = n;
+  k.jobs = 4 * n;
+  const long area_sb = (long)(c->geo.W / 4) * (c->geo.H / 4);
+  k.sb = (int)std::min<long>((long)n * 1024, area_sb);
+  k.elems = 4 * k.sb;
+  c->caps = k;
+  HIPCHK(c, c->d_pus.ensure(k.pus));
+  HIPCHK(c, c->d_pu_off.ensure(k.pus));
+  HIPCHK(c, c->d_pu_chunk.ensure(k.sb / 64 + 1));
+  HIPCHK(c, c->d_jobs.ensure(k.jobs));
+  HIPCHK(c, c->d_job_off.ensure(k.jobs));
+  HIPCHK(c, c->d_job_chunk.ensure(k.elems / 64 + 1));
+  HIPCHK(c, c->d_setup.ensure(k.jobs));
+  HIPCHK(c, c->d_reproj.ensure(2 * (size_t)k.elems));
+  HIPCHK(c, c->d_cnt.ensure(1));
+  HIPCHK(c, c->d_meta.ensure(1));
+  return MM_OK;
+}
+
+// One picture: memset + k_plan_count + k_plan_place + k_setup_dev + k_reproj_dev + k_mc_dev on
+// the context stream, bracketed by ev0/ev1.  Validation errors are deferred to mm_pred_status.
+static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, int n, int16_t* dy, ptrdiff_t sdy,
+                              int16_t* dcb, int16_t* dcr, ptrdiff_t sdc) {
+  std::vector<std::pair<int, RefDev>> refs;
+  for (auto& kv : c->refs)
+    refs.emplace_back(kv.first, RefDev{kv.second.y, kv.second.cb, kv.second.cr, kv.second.stride_y, kv.second.stride_c});
+  PicTables t;
+  std::string err;
+  int rc = build_pic_tables(seq_info(c->prm), c->epipoles, cur_poc, refs, &t, &err);
+  if (rc) return fail(c, rc, err);
+  RCCHK(ensure_plan_buffers(c, n));
+  const PlanCaps& k = c->caps;
+  const int gp = (n + 255) / 256;
+  const int gs = (k.jobs + 255) / 256;
+  const int gr = round_grid((k.elems + 255) / 256);
+  const int gm = round_grid((k.sb + 255) / 256);
+  HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->d_cnt.p, 0, sizeof(PlanCounters), c->stream));
+  hipLaunchKernelGGL(k_plan_count, dim3(gp), dim3(256), 0, c->stream, d_in, n, t, c->d_cnt.p);
+  hipLaunchKernelGGL(k_plan_place, dim3(gp), dim3(256), 0, c->stream, d_in, n, t, c->d_cnt.p, c->d_meta.p, k,
+                     c->d_pus.p, c->d_pu_off.p, c->d_pu_chunk.p, c->d_jobs.p, c->d_job_off.p, c->d_job_chunk.p);
+  if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[0], c->stream));
+  hipLaunchKernelGGL(k_setup_dev, dim3(gs), dim3(256), 0, c->stream, c->sc, c->d_meta.p, c->d_jobs.p, t,
+                     c->d_setup.p);
+  if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[1], c->stream));
+  hipLaunchKernelGGL(k_reproj_dev, dim3(gr), dim3(256), 0, c->stream, c->sc, c->d_meta.p, c->d_jobs.p,
+                     c->d_job_off.p, c->d_job_chunk.p, c->d_setup.p, make_cache(c), c->d_reproj.p);
+  if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[2], c->stream));
+  hipLaunchKernelGGL(k_mc_dev, dim3(gm), dim3(256), 0, c->stream, c->geo, c->d_meta.p, c->d_pus.p, c->d_pu_off.p,
+                     c->d_pu_chunk.p, c->d_jobs.p, c->d_reproj.p, t, dy, (int)sdy, dcb, dcr, (int)sdc);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+  c->status_pending = true;
+  return MM_OK;
+}
+
+// Synchronise and decode the deferred validation status of the last device-planned call.
+static int read_status(mm_ctx* c, int* first_bad) {
+  if (first_bad) *first_bad = -1;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (!c->status_pending) return MM_OK;
+  c->status_pending = false;
+  unsigned long long w = 0;
+  HIPCHK(c, hipMemcpy(&w, &c->d_cnt.p->status, sizeof(w), hipMemcpyDeviceToHost));
+  if (!w) return MM_OK;
+  const unsigned long long v = ~w;
+  const int code = (int)(v & 0xff), pu = (int)(v >> 8);
+  if (first_bad) *first_bad = pu;
+  static const char* what[] = {"ok", "PU outside the picture, not 4x4 aligned or using no list, or the list covers more than the picture",
+                               "HIP error", "reference POC not uploaded", "no epipole for (curPOC, refPOC)",
+                               "invalid, CLASSIC or inactive motion model", "no device"};
+  return fail(c, code, "PU " + std::to_string(pu) + ": " + (code >= 0 && code <= 6 ? what[code] : "error"));
+}
+
+int mm_pred_device(mm_ctx* c, int cur_poc, const mm_pu_desc* d_pus, int n, int16_t* dy, ptrdiff_t sdy, int16_t* dcb,
+                   int16_t* dcr, ptrdiff_t sdc) {
+  if (!c || n < 0 || (n > 0 && !d_pus) || !dy || (c->geo.chroma && (!dcb || !dcr))) return MM_ERR_ARG;
+  if (n == 0) return MM_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  return launch_device_plan(c, cur_poc, d_pus, n, dy, sdy, dcb, dcr, sdc);
+}
+
+int mm_pred_status(mm_ctx* c, int* first_bad_pu) {
+  if (!c) return MM_ERR_ARG;
+  return read_status(c, first_bad_pu);
+}
+
 int mm_pred_prepare(mm_ctx* c, int cur_poc, const mm_pu_desc* pus, int n) {
   if (!c || n < 0 || (n > 0 && !pus)) return MM_ERR_ARG;
   HIPCHK(c, hipSetDevice(c->device));
   c->prepared = false;
-  Planner pl(seq_info(c->prm), c->epipoles, &c->plan);
-  int rc = pl.plan_pus(cur_poc, pus, n, [c](int poc) { return c->refs.count(poc) != 0; });
-  if (rc) return fail(c, rc, c->plan.err);
-  std::vector<RefDev> refs;
-  for (int poc : c->plan.ref_pocs) {
-    const RefHost& r = c->refs[poc];
-    refs.push_back(RefDev{r.y, r.cb, r.cr, r.stride_y, r.stride_c});
-  }
-  RCCHK(upload_jobs(c));
-  RCCHK(upload(c, c->d_pus, c->plan.pus));
-  RCCHK(upload(c, c->d_pu_off, c->plan.pu_off));
-  RCCHK(upload(c, c->d_pu_chunk, c->plan.pu_chunk));
-  RCCHK(upload(c, c->d_refs, refs));
+  HIPCHK(c, c->d_pu_in.ensure(n));
+  if (n) HIPCHK(c, hipMemcpyAsync(c->d_pu_in.p, pus, (size_t)n * sizeof(mm_pu_desc), hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->prep_poc = cur_poc;
+  c->prep_n = n;
   c->prepared = true;
   return MM_OK;
 }
@@ -404,29 +644,35 @@ int mm_pred_prepare(mm_ctx* c, int cur_poc, const mm_pu_desc* pus, int n) {
 int mm_pred_run(mm_ctx* c, int16_t* dy, ptrdiff_t sdy, int16_t* dcb, int16_t* dcr, ptrdiff_t sdc) {
   if (!c || !dy || (c->geo.chroma && (!dcb || !dcr))) return MM_ERR_ARG;
   if (!c->prepared) return fail(c, MM_ERR_ARG, "mm_pred_run without a valid mm_pred_prepare");
-  const int n_pus = (int)c->plan.pus.size(), n_sb = c->plan.n_sb;
-  if (n_pus == 0) return MM_OK;
-  HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-  RCCHK(run_reproj_kernels(c));
-  hipLaunchKernelGGL(k_mc, dim3((n_sb + 255) / 256), dim3(256), 0, c->stream, c->geo, c->d_pus.p, n_pus, c->d_pu_off.p,
-                     c->d_pu_chunk.p, n_sb, c->d_jobs.p, c->d_reproj.p, c->d_refs.p, dy, (int)sdy, dcb, dcr, (int)sdc);
-  HIPCHK(c, hipGetLastError());
-  HIPCHK(c, hipEventRecord(c->ev1, c->stream));
-  return MM_OK;
+  return mm_pred_device(c, c->prep_poc, c->d_pu_in.p, c->prep_n, dy, sdy, dcb, dcr, sdc);
 }
 
 int mm_pred(mm_ctx* c, int cur_poc, const mm_pu_desc* pus, int n, int16_t* dy, ptrdiff_t sdy, int16_t* dcb,
             int16_t* dcr, ptrdiff_t sdc) {
   RCCHK(mm_pred_prepare(c, cur_poc, pus, n));
   RCCHK(mm_pred_run(c, dy, sdy, dcb, dcr, sdc));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  return MM_OK;
+  return read_status(c, nullptr);
 }
 
 int mm_last_timing(mm_ctx* c, float* ms) {
   if (!c || !ms) return MM_ERR_ARG;
   HIPCHK(c, hipEventSynchronize(c->ev1));
   HIPCHK(c, hipEventElapsedTime(ms, c->ev0, c->ev1));
+  return MM_OK;
+}
+
+int mm_set_stage_timing(mm_ctx* c, int on) {
+  if (!c) return MM_ERR_ARG;
+  c->stage_timing = on != 0;
+  return MM_OK;
+}
+
+int mm_last_stage_timing(mm_ctx* c, float ms[4]) {
+  if (!c || !ms) return MM_ERR_ARG;
+  if (!c->stage_timing) return fail(c, MM_ERR_ARG, "stage timing is off (mm_set_stage_timing)");
+  HIPCHK(c, hipEventSynchronize(c->ev1));
+  hipEvent_t e[5] = {c->ev0, c->ev_stage[0], c->ev_stage[1], c->ev_stage[2], c->ev1};
+  for (int i = 0; i < 4; i++) HIPCHK(c, hipEventElapsedTime(&ms[i], e[i], e[i + 1]));
   return MM_OK;
 }
 

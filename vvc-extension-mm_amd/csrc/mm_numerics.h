@@ -37,6 +37,7 @@ MM_HD float asf(uint32_t u) { return __builtin_bit_cast(float, u); }
 MM_HD uint64_t asu64(double d) { return __builtin_bit_cast(uint64_t, d); }
 MM_HD double asd(uint64_t u) { return __builtin_bit_cast(double, u); }
 MM_HD float fabsf_(float x) { return asf(asu(x) & 0x7fffffffu); }
+MM_HD double fabs_d_(double x) { return __builtin_fabs(x); }
 MM_HD double fabs_(double x) { return asd(asu64(x) & 0x7fffffffffffffffull); }
 MM_HD bool isnanf_(float x) { return (asu(x) & 0x7fffffffu) > 0x7f800000u; }
 MM_HD float sqrtf_(float x) { return __builtin_sqrtf(x); }   // IEEE correctly rounded
@@ -559,7 +560,7 @@ MM_HD dd_ dd_reduce_pio2_(double x, int* q) {
   s = dd_add_(s, {-k * pio2_3, 0.0});
   return s;
 }
-MM_HD float sinf_via_double(float xf) {
+MM_HD float sinf_via_double_dd(float xf) {
   double x = xf;
   if (xf == 0.0f) return xf;
   int q;
@@ -573,7 +574,7 @@ MM_HD float sinf_via_double(float xf) {
   }
   return (float)(v.hi + v.lo);
 }
-MM_HD float cosf_via_double(float xf) {
+MM_HD float cosf_via_double_dd(float xf) {
   double x = xf;
   int q;
   dd_ r = dd_reduce_pio2_(x, &q);
@@ -585,6 +586,72 @@ MM_HD float cosf_via_double(float xf) {
     default: v = dd_sin_small_(r); break;
   }
   return (float)(v.hi + v.lo);
+}
+
+// Fast path: plain-double sin/cos (Cody-Waite pi/2 reduction with FMA, Taylor polynomials in
+// Horner form, a few double ulps) rounded to float.  glibc's double result is within a few
+// double ulps of it, so both round to the same float unless the value lies near a float
+// rounding midpoint; those (rare) inputs take the double-double path above.  The combination is
+// checked against glibc over every float in [-4, 4] (tools/check_numerics.cpp); TAN's angles
+// epsC = pi/2 - thetaC lie in [-pi/2, pi/2].
+MM_HD double d_sin_poly_(double r) {
+  const double z = r * r;
+  double p = 1.0 / 121645100408832000.0;          // 1/19!  (|r| <= pi/4 + eps: next term < 2^-60)
+  p = fma_(p, -z, 1.0 / 355687428096000.0);       // 1/17!
+  p = fma_(p, -z, 1.0 / 1307674368000.0);         // 1/15!
+  p = fma_(p, -z, 1.0 / 6227020800.0);            // 1/13!
+  p = fma_(p, -z, 1.0 / 39916800.0);              // 1/11!
+  p = fma_(p, -z, 1.0 / 362880.0);                // 1/9!
+  p = fma_(p, -z, 1.0 / 5040.0);                  // 1/7!
+  p = fma_(p, -z, 1.0 / 120.0);                   // 1/5!
+  p = fma_(p, -z, 1.0 / 6.0);                     // 1/3!
+  return fma_(-r * z, p, r);
+}
+MM_HD double d_cos_poly_(double r) {
+  const double z = r * r;
+  double p = 1.0 / 2432902008176640000.0;         // 1/20!
+  p = fma_(p, -z, 1.0 / 6402373705728000.0);      // 1/18!
+  p = fma_(p, -z, 1.0 / 20922789888000.0);        // 1/16!
+  p = fma_(p, -z, 1.0 / 87178291200.0);           // 1/14!
+  p = fma_(p, -z, 1.0 / 479001600.0);             // 1/12!
+  p = fma_(p, -z, 1.0 / 3628800.0);               // 1/10!
+  p = fma_(p, -z, 1.0 / 40320.0);                 // 1/8!
+  p = fma_(p, -z, 1.0 / 720.0);                   // 1/6!
+  p = fma_(p, -z, 1.0 / 24.0);                    // 1/4!
+  const double hz = 0.5 * z;
+  const double w = 1.0 - hz;
+  return w + (((1.0 - w) - hz) + z * z * p);
+}
+// true when RN_float(v) is the same for every double within 2^-48 |v| of v
+MM_HD bool float_rounding_robust_(double v, float f) {
+  const uint32_t b = asu(f);
+  const double up = (double)asf(b + 1u), dn = (double)asf(b - 1u);
+  const double mid_hi = ((double)f + up) * 0.5, mid_lo = ((double)f + dn) * 0.5;
+  const double tol = fabs_d_(v) * 0x1p-48;
+  return fabs_d_(v - mid_hi) > tol && fabs_d_(v - mid_lo) > tol;
+}
+MM_HD double d_reduce_pio2_fast_(double x, int* q) {
+  const double pio2_1 = 0x1.921fb54442d18p0, pio2_2 = 0x1.1a62633145c07p-54;
+  const double k = __builtin_rint(x * 0x1.45f306dc9c883p-1);
+  *q = (int)k;
+  return fma_(-k, pio2_2, fma_(-k, pio2_1, x));
+}
+MM_HD float sinf_via_double(float xf) {
+  if (xf == 0.0f) return xf;
+  int q;
+  const double r = d_reduce_pio2_fast_((double)xf, &q);
+  double v = (q & 1) ? d_cos_poly_(r) : d_sin_poly_(r);
+  if (q & 2) v = -v;
+  const float f = (float)v;
+  return (f != 0.0f && float_rounding_robust_(v, f)) ? f : sinf_via_double_dd(xf);
+}
+MM_HD float cosf_via_double(float xf) {
+  int q;
+  const double r = d_reduce_pio2_fast_((double)xf, &q);
+  double v = (q & 1) ? d_sin_poly_(r) : d_cos_poly_(r);
+  if ((q + 1) & 2) v = -v;
+  const float f = (float)v;
+  return (f != 0.0f && float_rounding_robust_(v, f)) ? f : cosf_via_double_dd(xf);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -1,12 +1,13 @@
-// mm_plan.h -- host-side planning of one mm_reproject / mm_pred call (C++ host code).
+// mm_plan.h -- host-side planning (C++ host code).
 //
-// Turns the caller's block / PU descriptors into the flat work lists the kernels walk:
-//   jobs   one per reprojectMotionVectorSubblocks call (PU x list x {luma, chroma})
-//   pus    one per PU, with its reference slots and job indices
-// plus prefix offsets and 64-element chunk starts for O(1) item lookup in the kernels.  It also
-// resolves reference POCs to slots and GED epipoles to rotation matrices
-// (EpipoleList::findEpipole + GeodesicMotionModel::setEpipole).  Shared by the C-ABI
-// (mm_kernels.hip) and the CPU twin of the test suite.
+//  * Planner::plan_blocks: the parity API mm_reproject -- one job per
+//    reprojectMotionVectorSubblocks call, prefix offsets and 64-element chunk starts for O(1)
+//    item lookup in the kernels, GED epipoles resolved to rotation matrices
+//    (EpipoleList::findEpipole + GeodesicMotionModel::setEpipole).
+//  * build_pic_tables: the per-picture constants of the device-planned prediction path
+//    (mm_devplan.h): reference slots, and for each slot the GEODESIC_CAMPOSE rotation of its
+//    (curPOC, refPOC) epipole.
+// Shared by the C-ABI (mm_kernels.hip) and the CPU twin of the test suite.
 #pragma once
 #include <algorithm>
 #include <array>
@@ -16,6 +17,7 @@
 #include <vector>
 
 #include "../../include/mm360.h"
+#include "mm_devplan.h"
 #include "mm_pipeline.h"
 
 namespace mmplan {
@@ -146,80 +148,6 @@ class Planner {
     return MM_OK;
   }
 
-  // MPA chroma reprojection == luma reprojection, element for element, when every element of the
-  // block is a packet lane both in the luma frame cache and in the chroma block:
-  //  * the chroma grid (LinSpaced 2*xc + off + 4i) holds the luma grid values (4i + off);
-  //  * the chroma block's toPerspective (packet for N % 4 == 0) equals the frame cache entry
-  //    (packet for frame index < Nf - Nf % 4) -- same function, same inputs, same packet mode;
-  //  * the motion (mv * sign), toProjection and NaN fallback are identical;
-  //  * (x - off) * 16 == ((x - off) / 2) * 32 exactly (power-of-two scalings).
-  // So the 1/32-pel chroma result equals the 1/16-pel luma result and k_mc reads the luma job.
-  bool chroma_aliases_luma(int model, int w, int h) const {
-    if (model < MPA_FRONT_BACK || model > MPA_TOP_BOTTOM) return false;
-    const long nf = (long)(seq_.W / 4) * (seq_.H / 4);
-    const int n = (w / 4) * (h / 4);
-    return n >= 4 && n % 4 == 0 && nf % 4 == 0;
-  }
-
-  // has_ref(poc) -> bool: is the reference uploaded
-  template <typename HasRef>
-  int plan_pus(int cur_poc, const mm_pu_desc* pus, int n, HasRef has_ref) {
-    std::map<int, int> slot_of;
-    for (int i = 0; i < n; i++) {
-      const mm_pu_desc& u = pus[i];
-      if (u.w < 4 || u.h < 4 || u.w > 128 || u.h > 128 || (u.w & 3) || (u.h & 3) || (u.x & 3) || (u.y & 3) ||
-          u.x < 0 || u.y < 0 || u.x + u.w > seq_.W || u.y + u.h > seq_.H)
-        return fail(MM_ERR_ARG, "PU " + std::to_string(i) + " outside the picture or not 4x4 aligned");
-      PuDev d{};
-      d.x = u.x;
-      d.y = u.y;
-      d.w = u.w;
-      d.h = u.h;
-      int used = 0;
-      for (int l = 0; l < 2; l++) {
-        d.ref_slot[l] = -1;
-        d.job[l][0] = d.job[l][1] = -1;
-        if (u.ref_poc[l] < 0) continue;
-        used++;
-        int rc = model_ok(u.model[l]);
-        if (rc) return rc;
-        if (!has_ref(u.ref_poc[l]))
-          return fail(MM_ERR_NOREF, "reference POC " + std::to_string(u.ref_poc[l]) + " not uploaded");
-        auto sit = slot_of.find(u.ref_poc[l]);
-        if (sit == slot_of.end()) {
-          plan_->ref_pocs.push_back(u.ref_poc[l]);
-          sit = slot_of.emplace(u.ref_poc[l], (int)plan_->ref_pocs.size() - 1).first;
-        }
-        d.ref_slot[l] = sit->second;
-        for (int comp = 0; comp < (seq_.chroma ? 2 : 1); comp++) {
-          if (comp == 1 && chroma_aliases_luma(u.model[l], u.w, u.h)) {
-            d.job[l][1] = d.job[l][0];
-            continue;
-          }
-          d.job[l][comp] = (int)plan_->jobs.size();
-          rc = add_job(u.x, u.y, u.w >> comp, u.h >> comp, comp, u.model[l], u.mv[l][0], u.mv[l][1], cur_poc,
-                       u.ref_poc[l]);
-          if (rc) return rc;
-        }
-      }
-      if (!used) return fail(MM_ERR_ARG, "PU " + std::to_string(i) + " uses no reference list");
-      plan_->pus.push_back(d);
-    }
-    finish_jobs();
-    // k_mc enumeration grouped by prediction class (bi, uni L0, uni L1): a wave then runs one
-    // class's code path instead of both lists masked
-    auto cls = [](const PuDev& d) { return d.ref_slot[0] >= 0 && d.ref_slot[1] >= 0 ? 0 : (d.ref_slot[0] >= 0 ? 1 : 2); };
-    std::stable_sort(plan_->pus.begin(), plan_->pus.end(),
-                     [&](const PuDev& a, const PuDev& b) { return cls(a) < cls(b); });
-    for (auto& d : plan_->pus) {
-      d.sb_offset = plan_->n_sb;
-      plan_->n_sb += (d.w / 4) * (d.h / 4);
-      plan_->pu_off.push_back(d.sb_offset);
-    }
-    build_chunks(plan_->pu_off, plan_->n_sb, &plan_->pu_chunk);
-    return MM_OK;
-  }
-
  private:
   // Enumerate jobs grouped by (component, model, packet/scalar) so that the waves of k_setup and
   // k_reproj run one model path each instead of every model's path (divergence).  j.offset keeps
@@ -262,5 +190,39 @@ class Planner {
   Plan* plan_;
   std::map<std::tuple<int, int, int>, int> ged_map_;
 };
+
+// Per-picture tables of mm_pred_device: slots = the resident references (POC order), GED X/Y/Z
+// fixed epipoles (MVReprojection.cpp:44-52) and the camera-pose epipole of (cur_poc, slot POC)
+// when the epipole list has one (EpipoleList.cpp:19-36; a PU that needs a missing one raises
+// MM_ERR_NOEPIPOLE on the device).
+inline int build_pic_tables(const SeqInfo& s, const EpipoleMap& epi, int cur_poc,
+                            const std::vector<std::pair<int, RefDev>>& refs, mmdev::PicTables* t,
+                            std::string* err) {
+  if ((int)refs.size() > mmdev::MAX_SLOTS) {
+    *err = "more than " + std::to_string(mmdev::MAX_SLOTS) + " resident reference pictures";
+    return MM_ERR_ARG;
+  }
+  *t = mmdev::PicTables{};
+  t->n_slots = (int)refs.size();
+  t->W = s.W;
+  t->H = s.H;
+  t->chroma = s.chroma ? 1 : 0;
+  t->active = s.prm.active_models;
+  t->nf_mod4 = (int)(((long)(s.W / 4) * (s.H / 4)) % 4);
+  const V3 fixed[3] = {{1.0f, 0.0f, 0.0f}, {0.0f, 1.0f, 0.0f}, {0.0f, 0.0f, 1.0f}};
+  for (int i = 0; i < 3; i++) t->ged[i] = ged_rotation(fixed[i]);
+  for (int k = 0; k < t->n_slots; k++) {
+    t->poc[k] = refs[k].first;
+    t->ref[k] = refs[k].second;
+    std::array<int32_t, 3> q;
+    t->ged_cam[k] = -1;
+    if (find_epipole(epi, cur_poc, refs[k].first, &q)) {
+      V3 e = {fixed_to_float(q[0], 24), fixed_to_float(q[1], 24), fixed_to_float(q[2], 24)};
+      t->ged[3 + k] = ged_rotation(e);
+      t->ged_cam[k] = 3 + k;
+    }
+  }
+  return MM_OK;
+}
 
 }  // namespace mmplan

@@ -7,6 +7,7 @@ Mirrors the reference's C++ call surface for this path:
     Picture reconstruction planes                 -> MMContext.upload_ref    (mm_upload_ref)
     MVReprojection::reprojectMotionVectorSubblocks-> MMContext.reproject_motion_vector_subblocks
     InterPrediction::xPredInterBlkMM (+ addAvg)   -> MMContext.predict       (mm_pred)
+      same, PU list resident in HBM               -> MMContext.predict_device (mm_pred_device)
     InterpolationFilter::filterHor / filterVer    -> MMContext.filter_hor / filter_ver
 
 Everything runs through the HIP C-ABI library ``lib/libmm360.so`` (include/mm360.h).  There is
@@ -47,7 +48,8 @@ ERROR_NAMES = {
 EXPORTED_SYMBOLS = (
     "mm_create", "mm_destroy", "mm_set_stream", "mm_synchronize", "mm_last_error", "mm_get_version",
     "mm_set_epipole", "mm_upload_ref", "mm_release_ref", "mm_reproject", "mm_pred",
-    "mm_pred_prepare", "mm_pred_run", "mm_filter", "mm_last_timing",
+    "mm_pred_device", "mm_pred_status", "mm_pred_prepare", "mm_pred_run", "mm_filter", "mm_last_timing",
+    "mm_set_stage_timing", "mm_last_stage_timing",
 )
 
 
@@ -117,11 +119,15 @@ def load_library() -> ctypes.CDLL:
         "mm_release_ref": (c_int, [vp, c_int]),
         "mm_reproject": (c_int, [vp, vp, c_int, vp]),
         "mm_pred": (c_int, [vp, c_int, vp, c_int, vp, ctypes.c_ssize_t, vp, vp, ctypes.c_ssize_t]),
+        "mm_pred_device": (c_int, [vp, c_int, vp, c_int, vp, ctypes.c_ssize_t, vp, vp, ctypes.c_ssize_t]),
+        "mm_pred_status": (c_int, [vp, POINTER(c_int)]),
         "mm_pred_prepare": (c_int, [vp, c_int, vp, c_int]),
         "mm_pred_run": (c_int, [vp, vp, ctypes.c_ssize_t, vp, vp, ctypes.c_ssize_t]),
         "mm_filter": (c_int, [vp, c_int, c_int, vp, ctypes.c_ssize_t, vp, ctypes.c_ssize_t, c_int, c_int,
                               c_int, c_int, c_int]),
         "mm_last_timing": (c_int, [vp, POINTER(c_float)]),
+        "mm_set_stage_timing": (c_int, [vp, c_int]),
+        "mm_last_stage_timing": (c_int, [vp, POINTER(c_float)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -140,6 +146,14 @@ def _ptr(a) -> int:
 
 def _is_device(a) -> bool:
     return not isinstance(a, np.ndarray) and getattr(a, "is_cuda", False)
+
+
+def pus_to_device(pus: np.ndarray, device: int = 0):
+    """Copy a PU_DTYPE array into device memory (int32 CUDA tensor of 12 words per PU)."""
+    import torch
+    pus = np.ascontiguousarray(pus, dtype=PU_DTYPE)
+    words = pus.view(np.int32).reshape(len(pus), PU_DTYPE.itemsize // 4)
+    return torch.from_numpy(words.copy()).to(f"cuda:{device}")
 
 
 def subblock_count(w: int, h: int, comp: int) -> int:
@@ -240,6 +254,23 @@ class MMContext:
                                      c_void_p(_ptr(dst_cr)) if dst_cr is not None else None,
                                      dst_cb.stride(0) if dst_cb is not None else 0))
 
+    def predict_device(self, cur_poc: int, d_pus, dst_y, dst_cb=None, dst_cr=None):
+        """Whole picture path on the device from a device-resident PU list: `d_pus` is a CUDA
+        tensor holding PU_DTYPE records (e.g. pus_to_device(pus)).  Asynchronous on the context
+        stream; validation errors surface at status() / synchronize()."""
+        n = d_pus.numel() * d_pus.element_size() // PU_DTYPE.itemsize
+        self._check(self.lib.mm_pred_device(self.h, cur_poc, c_void_p(_ptr(d_pus)), n,
+                                            c_void_p(_ptr(dst_y)), dst_y.stride(0),
+                                            c_void_p(_ptr(dst_cb)) if dst_cb is not None else None,
+                                            c_void_p(_ptr(dst_cr)) if dst_cr is not None else None,
+                                            dst_cb.stride(0) if dst_cb is not None else 0))
+
+    def status(self):
+        """Deferred validation result of the last device-planned call: (code, first_bad_pu)."""
+        bad = c_int(-1)
+        rc = self.lib.mm_pred_status(self.h, byref(bad))
+        return rc, int(bad.value)
+
     def prepare(self, cur_poc: int, pus: np.ndarray):
         pus = np.ascontiguousarray(pus, dtype=PU_DTYPE)
         self._check(self.lib.mm_pred_prepare(self.h, cur_poc, c_void_p(pus.ctypes.data), len(pus)))
@@ -254,6 +285,15 @@ class MMContext:
         ms = c_float()
         self._check(self.lib.mm_last_timing(self.h, byref(ms)))
         return float(ms.value)
+
+    def set_stage_timing(self, on: bool):
+        self._check(self.lib.mm_set_stage_timing(self.h, int(on)))
+
+    def last_stage_timing_ms(self):
+        """(planning, k_setup, k_reproj, k_mc) device milliseconds of the last launch sequence."""
+        ms = (c_float * 4)()
+        self._check(self.lib.mm_last_stage_timing(self.h, ms))
+        return tuple(float(v) for v in ms)
 
     # -- InterpolationFilter -----------------------------------------------------------------
     def _filter(self, comp, vertical, src, x0, y0, w, h, frac, is_first, is_last):
