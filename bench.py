@@ -43,8 +43,11 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-steps", type=int, default=10, help="extra steps timed per launch with HIP events")
+    ap.add_argument("--lib", default=None, help="alternative build of libmm360.so (A/B experiments)")
     args = ap.parse_args()
 
+    if args.lib:
+        mm360.LIB_PATH = os.path.abspath(args.lib)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

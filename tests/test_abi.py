@@ -58,3 +58,18 @@ def test_product_has_no_oracle_dependency():
             if f.endswith((".py", ".h", ".hip", ".cpp", "Makefile")):
                 txt = open(os.path.join(dp, f)).read()
                 assert "oracle" not in txt.lower() or f == "__init__.py" and "oracle" not in txt, f
+
+
+def test_cpp_shim_example_builds_and_fails_loudly_without_gpu():
+    """The C++ host shim (host/mm360_vtm.hpp) compiles against the C-ABI; without a GPU the
+    example exits through the shim's exception with MM_ERR_NODEV (no CPU fallback)."""
+    import subprocess
+    pkg = os.path.join(ROOT, "vvc-extension-mm_amd")
+    subprocess.check_call(["make", "-s", "-C", pkg, "example"])
+    exe = os.path.join(pkg, "lib", "example_decode")
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: covered by tests/test_gpu.py::test_cpp_shim_example_on_gpu")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2, r.stdout + r.stderr
+    assert "mm360 error 6" in r.stdout

@@ -294,3 +294,14 @@ def test_device_validation_reports_lowest_failing_pu():
         # empty list is a no-op
         ctx.predict_device(W.CUR_POC, mm360.pus_to_device(pus[:0]), *dst)
         assert ctx.status() == (mm360.MM_OK, -1)
+
+
+def test_cpp_shim_example_on_gpu():
+    """C++ host shim end to end on the GPU: MVReprojection-shaped call, host and device PU lists
+    predict identical pictures."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "vvc-extension-mm_amd", "lib",
+                       "example_decode")
+    assert os.path.exists(exe), "build with __graft_entry__.build() / make -C vvc-extension-mm_amd example"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout + r.stderr

@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU-box driver: runs the named steps in order, each under its own time limit, and stops at the
 # first failure (no further GPU work after a fault / abort / timeout).
-#   tools/gpu_run.sh tests smoke bench prof pmc
+#   tools/gpu_run.sh tests smoke bench prof pmc=<tag>=<counters,...>
 set -u
 mkdir -p gpurun_out
 cd "$(dirname "$0")/.."
@@ -27,6 +27,9 @@ for step in "$@"; do
     counters) run counters 300 rocprofv3 -L ;;
     pmc_mem) run pmc_mem 600 rocprofv3 --pmc TA_BUSY_avr TA_BUSY_max TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum -d gpurun_out/pmc_mem -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 ;;
     pmc_sq) run pmc_sq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU -d gpurun_out/pmc_sq -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 ;;
+    pmc=*)  # pmc=<tag>=<counter,counter,...>: one rocprofv3 --pmc pass over a short bench run
+      tag=$(echo "$step" | cut -d= -f2); ctrs=$(echo "$step" | cut -d= -f3 | tr ',' ' ')
+      run "pmc_$tag" 600 rocprofv3 --pmc $ctrs -d "gpurun_out/pmc_$tag" -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -1,0 +1,170 @@
+// mm360_vtm.hpp -- C++ host shim over the C-ABI (include/mm360.h) with the call shape of the
+// reference's MM path, so that DecoderLib / EncoderLib call sites change as little as possible.
+//
+//   mm360::Context             one decoder/encoder instance on one GPU (mm_create / mm_destroy)
+//   mm360::MVReprojectionGPU   MVReprojection::init / isInitialized / subblockSize /
+//                              reprojectMotionVectorSubblocks      (SRC/MVReprojection.h:32-58)
+//   mm360::InterPredictionMM   xPredInterBlkMM + xWeightedAverage for a whole picture's PU list
+//                              (SRC/InterPrediction.h:151-154, InterPrediction.cpp:1584-1679)
+//
+// Status codes become exceptions, like the reference's CHECK -> Exception (SRC/TypeDef.h:1120-1135).
+// NaN reprojections (zero motion) and out-of-range sub-blocks (zero samples) are results, as in
+// the reference, not errors.  SRC = source/Lib/CommonLib of FAU-LMS/vvc-extension-mm.
+#pragma once
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/mm360.h"
+
+namespace mm360 {
+
+class Exception : public std::runtime_error {
+ public:
+  Exception(int code, const std::string& what) : std::runtime_error(what), code_(code) {}
+  int code() const { return code_; }
+
+ private:
+  int code_;
+};
+
+inline void check(mm_ctx* ctx, int rc, const char* call) {
+  if (rc != MM_OK)
+    throw Exception(rc, std::string(call) + " failed (" + std::to_string(rc) + "): " +
+                            (ctx ? mm_last_error(ctx) : "no context"));
+}
+
+// ---------------------------------------------------------------------------------------------
+class Context {
+ public:
+  // SPS-derived parameters; the defaults are the reference's hard-coded MM settings
+  // (EncApp.cpp:754-768): MMOffset4x4 code 1, GED flavour VISHWANATH_MODULATED.
+  Context(const mm_seq_params& params, int device = 0) {
+    int rc = mm_create(&params, device, &ctx_);
+    if (rc != MM_OK) throw Exception(rc, "mm_create failed (no HIP device or invalid parameters)");
+    params_ = params;
+  }
+  ~Context() {
+    if (ctx_) mm_destroy(ctx_);
+  }
+  Context(const Context&) = delete;
+  Context& operator=(const Context&) = delete;
+
+  mm_ctx* get() const { return ctx_; }
+  const mm_seq_params& params() const { return params_; }
+  void setStream(void* hipStream) { check(ctx_, mm_set_stream(ctx_, hipStream), "mm_set_stream"); }
+  void synchronize() { check(ctx_, mm_synchronize(ctx_), "mm_synchronize"); }
+
+  // EpipoleList::addEpipole (EpipoleList.cpp:8-11), Q24 fixed point; -1 = wildcard POC
+  void setEpipole(int curPOC, int refPOC, const int32_t q24[3]) {
+    check(ctx_, mm_set_epipole(ctx_, curPOC, refPOC, q24), "mm_set_epipole");
+  }
+  // A reconstructed picture becomes a reference: unpadded planes, origin at (0, 0)
+  void uploadReference(int poc, const int16_t* y, ptrdiff_t strideY, const int16_t* cb, const int16_t* cr,
+                       ptrdiff_t strideC, bool onDevice) {
+    check(ctx_, mm_upload_ref(ctx_, poc, y, strideY, cb, cr, strideC, onDevice ? 1 : 0), "mm_upload_ref");
+  }
+  void releaseReference(int poc) { check(ctx_, mm_release_ref(ctx_, poc), "mm_release_ref"); }
+
+ private:
+  mm_ctx* ctx_ = nullptr;
+  mm_seq_params params_{};
+};
+
+// ---------------------------------------------------------------------------------------------
+// ArrayXXFixedPtrPair analogue: X and Y fixed-point arrays, Eigen column-major (rows = h/sbh)
+struct FixedPair {
+  int rows = 0, cols = 0;
+  std::vector<int32_t> x, y;
+  int32_t X(int r, int c) const { return x[(size_t)c * rows + r]; }
+  int32_t Y(int r, int c) const { return y[(size_t)c * rows + r]; }
+};
+
+class MVReprojectionGPU {
+ public:
+  // MVReprojection::init(projection, resolution, sps, epipoleList): the context already holds
+  // the sequence parameters and builds the MPA frame caches on the device.
+  void init(Context* ctx) { ctx_ = ctx; }
+  bool isInitialized() const { return ctx_ != nullptr; }
+
+  // MVReprojection::subblockSize (MVReprojection.cpp:73-78): 4x4 luma, 2x2 4:2:0 chroma
+  static void subblockSize(int compID, int chromaFormat, int* w, int* h) {
+    const bool sub = compID != 0 && chromaFormat == 1;
+    *w = sub ? 2 : 4;
+    *h = sub ? 2 : 4;
+  }
+
+  // reprojectMotionVectorSubblocks (MVReprojection.cpp:80-166); position/size in component units
+  FixedPair reprojectMotionVectorSubblocks(int posX, int posY, int width, int height, int mvHor, int mvVer,
+                                           int motionModelID, int compID, int curPOC, int refPOC) const {
+    mm_block_desc b{posX, posY, width, height, mvHor, mvVer, motionModelID, compID, curPOC, refPOC};
+    int sw, sh;
+    subblockSize(compID, ctx_->params().chroma_format, &sw, &sh);
+    FixedPair out;
+    out.rows = height / sh;
+    out.cols = width / sw;
+    std::vector<int32_t> xy(2 * (size_t)out.rows * out.cols);
+    check(ctx_->get(), mm_reproject(ctx_->get(), &b, 1, xy.data()), "mm_reproject");
+    out.x.resize(xy.size() / 2);
+    out.y.resize(xy.size() / 2);
+    for (size_t i = 0; i < out.x.size(); i++) {
+      out.x[i] = xy[2 * i];
+      out.y[i] = xy[2 * i + 1];
+    }
+    return out;
+  }
+
+ private:
+  Context* ctx_ = nullptr;
+};
+
+// ---------------------------------------------------------------------------------------------
+// Batched MM motion compensation of one picture.  A decoder collects the MM PUs of a picture (or
+// of a CTU row) while parsing -- after its own xSubPuMC / DMVR / BDOF-size splitting
+// (InterPrediction.cpp:1737-1789) -- then predicts them in one call; the predictions land in
+// device planes that the reconstruction reads.
+class InterPredictionMM {
+ public:
+  explicit InterPredictionMM(Context* ctx) : ctx_(ctx) {}
+
+  void clear() { pus_.clear(); }
+  // One PU: luma area, per list (mv in 1/16 luma, reference POC or -1, motion model)
+  void addPU(int x, int y, int w, int h, const int mv[2][2], const int refPOC[2], const int model[2]) {
+    mm_pu_desc d{};
+    d.x = x;
+    d.y = y;
+    d.w = w;
+    d.h = h;
+    for (int l = 0; l < 2; l++) {
+      d.mv[l][0] = mv[l][0];
+      d.mv[l][1] = mv[l][1];
+      d.ref_poc[l] = refPOC[l];
+      d.model[l] = model[l];
+    }
+    pus_.push_back(d);
+  }
+  size_t size() const { return pus_.size(); }
+  const std::vector<mm_pu_desc>& pus() const { return pus_; }
+
+  // Synchronous: host PU list -> predicted device planes (bi: addAvg, uni: clipped).
+  void predictPicture(int curPOC, int16_t* dstY, ptrdiff_t strideY, int16_t* dstCb, int16_t* dstCr,
+                      ptrdiff_t strideC) {
+    check(ctx_->get(),
+          mm_pred(ctx_->get(), curPOC, pus_.data(), (int)pus_.size(), dstY, strideY, dstCb, dstCr, strideC),
+          "mm_pred");
+  }
+  // Asynchronous on the context stream: PU list already in device memory (e.g. written by a GPU
+  // parser); errors surface at Context::synchronize().
+  void predictPictureDevice(int curPOC, const mm_pu_desc* devPUs, int n, int16_t* dstY, ptrdiff_t strideY,
+                            int16_t* dstCb, int16_t* dstCr, ptrdiff_t strideC) {
+    check(ctx_->get(), mm_pred_device(ctx_->get(), curPOC, devPUs, n, dstY, strideY, dstCb, dstCr, strideC),
+          "mm_pred_device");
+  }
+
+ private:
+  Context* ctx_;
+  std::vector<mm_pu_desc> pus_;
+};
+
+}  // namespace mm360
