@@ -33,7 +33,7 @@ static void make_twin(const mm_seq_params* p, Twin* t) {
   t->sc.ged_flavor = p->ged_flavor;
   t->geo = Geometry{p->width,        p->height,           p->width >> 1,        p->height >> 1,
                     p->max_cu_width, p->max_cu_height,    p->max_cu_width >> 1, p->max_cu_height >> 1,
-                    p->bit_depth,    p->chroma_format == 1};
+                    p->bit_depth,    p->chroma_format == 1, 0};
   const int cols = p->width / 4, rows = p->height / 4, n = cols * rows;
   for (int pl = 0; pl < 3; pl++) {
     if (!(p->active_models & (1u << (MPA_FRONT_BACK + pl)))) continue;
@@ -74,7 +74,8 @@ static void run_reproj(const Twin& t, const Plan& plan, std::vector<int32_t>* ou
   MpaCache c = cache_of(t);
 #pragma omp parallel for schedule(static, 256)
   for (int g = 0; g < plan.n_elems; g++)
-    reproj_thread(g, t.sc, plan.jobs.data(), nj, plan.job_off.data(), plan.job_chunk.data(), setups.data(), c,
+    reproj_thread(g, find_item(plan.job_off.data(), plan.job_chunk.data(), g, nj), t.sc, plan.jobs.data(),
+                  plan.job_off.data(), setups.data(), c,
                   out->data());
 }
 
@@ -149,11 +150,12 @@ extern "C" int twin_pred(const mm_seq_params* p, int n_epi, const int32_t* epi, 
   MpaCache c = cache_of(t);
 #pragma omp parallel for schedule(static, 256)
   for (int g = 0; g < m.n_elems; g++)
-    reproj_thread(g, t.sc, jobs.data(), m.n_jobs, job_off.data(), job_chunk.data(), setups.data(), c, r.data());
+    reproj_thread(g, find_item(job_off.data(), job_chunk.data(), g, m.n_jobs), t.sc, jobs.data(), job_off.data(),
+                  setups.data(), c, r.data());
   const Taps taps{LUMA_T, CHROMA_T};
 #pragma omp parallel for schedule(static, 256)
   for (int g = 0; g < m.n_sb; g++)
-    mc_thread(g, t.geo, taps, dpus.data(), m.n_pus, pu_off.data(), pu_chunk.data(), jobs.data(), r.data(), tab.ref,
-              dy, sdy, dcb, dcr, sdc);
+    mc_thread(g, find_item(pu_off.data(), pu_chunk.data(), g, m.n_pus), t.geo, taps, dpus.data(), jobs.data(), r.data(),
+              tab.ref, dy, sdy, dcb, dcr, sdc);
   return 0;
 }

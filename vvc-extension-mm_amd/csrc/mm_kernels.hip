@@ -56,9 +56,11 @@ __global__ void __launch_bounds__(256) k_reproj(SeqConst sc, const JobDev* __res
                                                 const int* __restrict__ job_offsets, const int* __restrict__ chunk_start,
                                                 int n_elems, const BlockSetup* __restrict__ setups, MpaCache cache,
                                                 int32_t* __restrict__ out) {
-  int g = blockIdx.x * blockDim.x + threadIdx.x;
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g - (int)__lane_id() >= n_elems) return;  // whole wave past the end
+  const int ji = wave_find_item(job_offsets, chunk_start, g, n_jobs);
   if (g >= n_elems) return;
-  reproj_thread(g, sc, jobs, n_jobs, job_offsets, chunk_start, setups, cache, out);
+  reproj_thread(g, ji, sc, jobs, job_offsets, setups, cache, out);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -191,8 +193,11 @@ __global__ void __launch_bounds__(256) k_reproj_dev(SeqConst sc, const PlanMeta*
                                                     const BlockSetup* __restrict__ setups, MpaCache cache,
                                                     int32_t* __restrict__ out) {
   const int g = xcd_block() * blockDim.x + threadIdx.x;
-  if (g >= meta->n_elems) return;
-  reproj_thread(g, sc, jobs, meta->n_jobs, job_offsets, chunk_start, setups, cache, out);
+  const int n_elems = meta->n_elems;
+  if (g - (int)__lane_id() >= n_elems) return;  // whole wave past the end
+  const int ji = wave_find_item(job_offsets, chunk_start, g, meta->n_jobs);
+  if (g >= n_elems) return;
+  reproj_thread(g, ji, sc, jobs, job_offsets, setups, cache, out);
 }
 
 __global__ void __launch_bounds__(256) k_mc_dev(Geometry geo, const PlanMeta* __restrict__ meta,
@@ -202,10 +207,12 @@ __global__ void __launch_bounds__(256) k_mc_dev(Geometry geo, const PlanMeta* __
                                                 int16_t* __restrict__ dst_y, int dsy, int16_t* __restrict__ dst_cb,
                                                 int16_t* __restrict__ dst_cr, int dsc) {
   const int g = xcd_block() * blockDim.x + threadIdx.x;
-  if (g >= meta->n_sb) return;
+  const int n_sb = meta->n_sb;
+  if (g - (int)__lane_id() >= n_sb) return;  // whole wave past the end
+  const int pi = wave_find_item(pu_offsets, chunk_start, g, meta->n_pus);
+  if (g >= n_sb) return;
   const Taps taps{c_luma_taps, c_chroma_taps};
-  mc_thread(g, geo, taps, pus, meta->n_pus, pu_offsets, chunk_start, jobs, reproj, t.ref, dst_y, dsy, dst_cb, dst_cr,
-            dsc);
+  mc_thread(g, pi, geo, taps, pus, jobs, reproj, t.ref, dst_y, dsy, dst_cb, dst_cr, dsc);
 }
 
 // InterpolationFilter::filter<N, isVertical, isFirst, isLast> / filterCopy on a raw block
@@ -401,6 +408,7 @@ int mm_create(const mm_seq_params* p, int device, mm_ctx** out_ctx) {
   c->geo.maxCUwc = p->max_cu_width >> 1;
   c->geo.maxCUhc = p->max_cu_height >> 1;
   c->geo.bd = p->bit_depth;
+  c->geo.vec_store = 0;
   if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
       hipEventCreate(&c->ev_stage[0]) != hipSuccess || hipEventCreate(&c->ev_stage[1]) != hipSuccess ||
       hipEventCreate(&c->ev_stage[2]) != hipSuccess) {
@@ -572,6 +580,9 @@ static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, in
   int rc = build_pic_tables(seq_info(c->prm), c->epipoles, cur_poc, refs, &t, &err);
   if (rc) return fail(c, rc, err);
   RCCHK(ensure_plan_buffers(c, n));
+  Geometry geo = c->geo;
+  geo.vec_store = ((uintptr_t)dy % 8 == 0) && (sdy % 4 == 0) &&
+                  (!geo.chroma || ((uintptr_t)dcb % 4 == 0 && (uintptr_t)dcr % 4 == 0 && sdc % 2 == 0));
   const PlanCaps& k = c->caps;
   const int gp = (n + 255) / 256;
   const int gs = (k.jobs + 255) / 256;
@@ -589,7 +600,7 @@ static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, in
   hipLaunchKernelGGL(k_reproj_dev, dim3(gr), dim3(256), 0, c->stream, c->sc, c->d_meta.p, c->d_jobs.p,
                      c->d_job_off.p, c->d_job_chunk.p, c->d_setup.p, make_cache(c), c->d_reproj.p);
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[2], c->stream));
-  hipLaunchKernelGGL(k_mc_dev, dim3(gm), dim3(256), 0, c->stream, c->geo, c->d_meta.p, c->d_pus.p, c->d_pu_off.p,
+  hipLaunchKernelGGL(k_mc_dev, dim3(gm), dim3(256), 0, c->stream, geo, c->d_meta.p, c->d_pus.p, c->d_pu_off.p,
                      c->d_pu_chunk.p, c->d_jobs.p, c->d_reproj.p, t, dy, (int)sdy, dcb, dcr, (int)sdc);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipEventRecord(c->ev1, c->stream));

@@ -49,7 +49,8 @@ struct Geometry {
   int W, H, Wc, Hc;
   int maxCUw, maxCUh, maxCUwc, maxCUhc;
   int bd;
-  int chroma;  // 1 = 4:2:0
+  int chroma;     // 1 = 4:2:0
+  int vec_store;  // destination planes allow 8-byte luma / 4-byte chroma row stores
 };
 
 struct Taps {
@@ -63,6 +64,31 @@ MM_HD int find_item(const int* offsets, const int* chunk_start, int g, int n_ite
   while (j + 1 < n_items && offsets[j + 1] <= g) j++;
   return j;
 }
+
+#if defined(__HIP__)
+// The same lookup for a whole wavefront whose lanes hold g = g0 + lane (g0 % 64 == 0): one
+// uniform chunk_start load, one coalesced load of the next 64 item offsets, and a 6-step binary
+// search over them with cross-lane reads -- instead of a chain of dependent loads per lane.
+// Items are non-empty, so the offsets relative to g0 are strictly increasing.
+__device__ __forceinline__ int wave_find_item(const int* offsets, const int* chunk_start, int g, int n_items) {
+  const int lane = __lane_id();
+  const int g0 = g - lane;
+  const int j0 = __builtin_amdgcn_readfirstlane(chunk_start[g0 >> 6]);
+  const int i = j0 + lane;
+  int s = 64;
+  if (i < n_items) {
+    s = offsets[i] - g0;
+    s = s < 0 ? 0 : s;
+  }
+  int lo = 0;
+#pragma unroll
+  for (int step = 32; step > 0; step >>= 1) {
+    const int cand = __shfl(s, lo + step);  // lo + step <= 63
+    if (cand <= lane) lo += step;
+  }
+  return j0 + lo;
+}
+#endif
 
 // MotionPlaneAdaptiveMotionModel::fillCache on MVReprojection::fillCache's frame grid; storage
 // row-major [j][i], Eigen column-major index i*rows + j decides packet vs tail.
@@ -87,9 +113,9 @@ MM_HD void setup_thread(int t, const SeqConst& sc, const JobDev* jobs, const M3*
               j.ged_idx >= 0 ? &ged[j.ged_idx] : nullptr);
 }
 
-MM_HD void reproj_thread(int g, const SeqConst& sc, const JobDev* jobs, int n_jobs, const int* job_offsets,
-                         const int* chunk_start, const BlockSetup* setups, const MpaCache& cache, int32_t* out_xy) {
-  const int ji = find_item(job_offsets, chunk_start, g, n_jobs);
+// ji = the job holding flat element g (find_item / wave_find_item)
+MM_HD void reproj_thread(int g, int ji, const SeqConst& sc, const JobDev* jobs, const int* job_offsets,
+                         const BlockSetup* setups, const MpaCache& cache, int32_t* out_xy) {
   const JobDev& j = jobs[ji];
   const int local = g - job_offsets[ji];  // enumeration order; results go to j.offset + local
   const int col = local / j.rows, row = local - col * j.rows;
@@ -113,13 +139,35 @@ MM_HD void reproj_thread(int g, const SeqConst& sc, const JobDev* jobs, int n_jo
   out_xy[2 * (j.offset + local) + 1] = fy;
 }
 
+// N output samples of one row: one 8-byte (N = 4) or 4-byte (N = 2) store when the destination
+// allows it (Geometry::vec_store), else per-sample stores
+template <int N>
+MM_HD void store_row(int16_t* d, const int16_t* v, int vec) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (vec) {
+    if constexpr (N == 4) {
+      typedef uint32_t u32x2_a8 __attribute__((ext_vector_type(2), aligned(8)));
+      u32x2_a8 w;
+      w.x = ((uint32_t)(uint16_t)v[0]) | ((uint32_t)(uint16_t)v[1] << 16);
+      w.y = ((uint32_t)(uint16_t)v[2]) | ((uint32_t)(uint16_t)v[3] << 16);
+      *reinterpret_cast<u32x2_a8*>(d) = w;
+    } else {
+      *reinterpret_cast<uint32_t*>(d) = ((uint32_t)(uint16_t)v[0]) | ((uint32_t)(uint16_t)v[1] << 16);
+    }
+    return;
+  }
+#endif
+  (void)vec;
+  for (int c = 0; c < N; c++) d[c] = v[c];
+}
+
 // One luma 4x4 sub-block (and its two 4:2:0 chroma 2x2 sub-blocks) of one PU: both lists,
 // xPredInterBlkMM's per-sub-block dispatch (InterPrediction.cpp:776-828), then addAvg (bi) or the
 // rndRes uni prediction (xWeightedAverage, InterPrediction.cpp:1584-1679).
-MM_HD void mc_thread(int g, const Geometry& geo, const Taps& taps, const PuDev* pus, int n_pus,
-                     const int* pu_offsets, const int* chunk_start, const JobDev* jobs, const int32_t* reproj,
-                     const RefDev* refs, int16_t* dst_y, int dsy, int16_t* dst_cb, int16_t* dst_cr, int dsc) {
-  const int pi = find_item(pu_offsets, chunk_start, g, n_pus);
+// pi = the PU holding luma sub-block g (find_item / wave_find_item)
+MM_HD void mc_thread(int g, int pi, const Geometry& geo, const Taps& taps, const PuDev* pus, const JobDev* jobs,
+                     const int32_t* reproj, const RefDev* refs, int16_t* dst_y, int dsy, int16_t* dst_cb,
+                     int16_t* dst_cr, int dsc) {
   const PuDev pu = pus[pi];
   // lanes walk the PU row-major (horizontally adjacent sub-blocks in adjacent lanes share the
   // reference cache lines of each window row); reprojection results are Eigen column-major
@@ -151,12 +199,15 @@ MM_HD void mc_thread(int g, const Geometry& geo, const Taps& taps, const PuDev* 
   }
   {
     const int ox = pu.x + 4 * col, oy = pu.y + 4 * row;
+#pragma unroll
     for (int r = 0; r < 4; r++) {
-      int16_t* d = dst_y + (long)(oy + r) * dsy + ox;
+      int16_t o[4];
+#pragma unroll
       for (int c = 0; c < 4; c++) {
         const int i = r * 4 + c;
-        d[c] = bi ? add_avg(pl[0][i], pl[1][i], geo.bd) : (uni_list == 0 ? pl[0][i] : pl[1][i]);
+        o[c] = bi ? add_avg(pl[0][i], pl[1][i], geo.bd) : (uni_list == 0 ? pl[0][i] : pl[1][i]);
       }
+      store_row<4>(dst_y + (long)(oy + r) * dsy + ox, o, geo.vec_store);
     }
   }
   if (!geo.chroma) return;
@@ -185,14 +236,17 @@ MM_HD void mc_thread(int g, const Geometry& geo, const Taps& taps, const PuDev* 
   }
   {
     const int ox = (pu.x >> 1) + 2 * col, oy = (pu.y >> 1) + 2 * row;
+#pragma unroll
     for (int r = 0; r < 2; r++) {
-      int16_t* db = dst_cb + (long)(oy + r) * dsc + ox;
-      int16_t* dr = dst_cr + (long)(oy + r) * dsc + ox;
+      int16_t ob[2], orr[2];
+#pragma unroll
       for (int c = 0; c < 2; c++) {
         const int i = r * 2 + c;
-        db[c] = bi ? add_avg(pcb[0][i], pcb[1][i], geo.bd) : (uni_list == 0 ? pcb[0][i] : pcb[1][i]);
-        dr[c] = bi ? add_avg(pcr[0][i], pcr[1][i], geo.bd) : (uni_list == 0 ? pcr[0][i] : pcr[1][i]);
+        ob[c] = bi ? add_avg(pcb[0][i], pcb[1][i], geo.bd) : (uni_list == 0 ? pcb[0][i] : pcb[1][i]);
+        orr[c] = bi ? add_avg(pcr[0][i], pcr[1][i], geo.bd) : (uni_list == 0 ? pcr[0][i] : pcr[1][i]);
       }
+      store_row<2>(dst_cb + (long)(oy + r) * dsc + ox, ob, geo.vec_store);
+      store_row<2>(dst_cr + (long)(oy + r) * dsc + ox, orr, geo.vec_store);
     }
   }
 }
