@@ -17,6 +17,9 @@
  *                       xPredInterUni (InterPrediction.cpp:455-533) and xWeightedAverage
  *                       (addAvg / copyClip)               SRC/InterPrediction.cpp:1584-1679
  *   mm_filter        <- InterpolationFilter::filterHor/filterVer  SRC/InterpolationFilter.h:123-128
+ *   mm_sad_window    <- InterSearch::xMVReprojectionInterpolation + RdCost::xGetSAD per candidate
+ *                       (EncoderLib/InterSearch.cpp:6277-6385, 363-443; SRC/RdCost.cpp:482-517)
+ *   mm_upload_org    <- the original picture (pcPatternKey) the encoder SAD compares against
  *   mm_destroy       <- (MVReprojection / InterPrediction destructors)
  *
  * Conventions: plain C, int status return (MM_OK = 0), one opaque context per
@@ -88,6 +91,17 @@ typedef struct mm_pu_desc {
   int32_t model[2];            /* mm_model_id per list (non-CLASSIC for MM MC) */
 } mm_pu_desc;
 
+/* One block of an encoder motion search (InterSearch::xMVReprojectionInterpolation call site,
+ * EncoderLib/InterSearch.cpp:6189-6273): a window of candidate MVs around `mv` is evaluated. */
+typedef struct mm_me_block {
+  int32_t x, y, w, h;          /* luma block (PU) */
+  int32_t mv_hor, mv_ver;      /* window centre, 1/16 luma (MV_PRECISION_INTERNAL) */
+  int32_t model;               /* mm_model_id, not CLASSIC */
+  int32_t ref_poc;
+  int32_t sub_shift;           /* SAD row subsampling: 0 = every row, 1 = every other row
+                                  (RdCost::setDistParam subShiftMode 2, RdCost.cpp:296-303) */
+} mm_me_block;
+
 typedef struct mm_ctx mm_ctx;
 
 /* Lifecycle */
@@ -148,7 +162,23 @@ int mm_filter(mm_ctx* ctx, int comp, int vertical, const int16_t* src, ptrdiff_t
               int16_t* dst, ptrdiff_t dst_stride, int w, int h, int frac, int is_first,
               int is_last);
 
-/* Device time of the last mm_pred_device / mm_pred_run launch sequence (HIP events on the
+/* Original (source) luma picture of `poc` for the encoder SAD (the pcPatternKey / org buffer of
+ * RdCost::xGetSAD); unpadded, picture origin at y[0]. */
+int mm_upload_org(mm_ctx* ctx, int poc, const int16_t* y, ptrdiff_t stride_y, int src_is_device);
+
+/* Encoder ME candidate evaluation (InterSearch::xMVReprojectionInterpolation + RdCost::xGetSAD,
+ * EncoderLib/InterSearch.cpp:6277-6385, CommonLib/RdCost.cpp:482-517), batched:
+ * for every block b and candidate (i, j) in [-range, range]^2 the block's luma is reprojected with
+ * mv = (mv_hor + i*step, mv_ver + j*step) in its model, predicted as the reference does for the
+ * encoder (rounded uni prediction, out-of-range margin 0) and compared with the original picture
+ * of cur_poc.  sads (DEVICE memory, n * (2*range+1)^2 uint32) receives the SAD of candidate
+ * c = (j + range) * (2*range + 1) + (i + range) at sads[b * (2*range+1)^2 + c].  step = 16 / 8 / 4
+ * gives integer / half / quarter-pel windows.  Synchronous; the full SAD is returned where the
+ * reference may stop early past its running best (same search decisions). */
+int mm_sad_window(mm_ctx* ctx, int cur_poc, const mm_me_block* blocks, int n, int range, int step,
+                  uint32_t* sads);
+
+/* Device time of the last mm_pred_device / mm_pred_run / mm_sad_window launch sequence (HIP events on the
  * context stream around all of its launches), milliseconds. */
 int mm_last_timing(mm_ctx* ctx, float* ms_total);
 

@@ -734,10 +734,12 @@ static void pad_plane(const int16_t* src, ptrdiff_t sstride, int w, int h, int m
   *ostride = stride;
 }
 
-/* InterPrediction::xPredInterBlkMM (InterPrediction.cpp:683-856) for one component of one list.
+/* InterPrediction::xPredInterBlkMM (InterPrediction.cpp:683-856) for one component of one list,
+ * and (enc = 1) its encoder twin InterSearch::xMVReprojectionInterpolation
+ * (EncoderLib/InterSearch.cpp:6277-6385: luma, out-of-range margin maxCUWidth = 0 for both axes).
  * dst: w*h int16 (component units) */
-static int pred_blk_mm(Orc* o, int comp, const OPic* ref, int x, int y, int w, int h, int mvh, int mvv, int model,
-                       int bi, int cur_poc, int16_t* dst) {
+static int pred_blk_mm_x(Orc* o, int comp, const OPic* ref, int x, int y, int w, int h, int mvh, int mvv, int model,
+                         int bi, int cur_poc, int16_t* dst, int enc) {
   const int chroma = comp != 0;
   const int sbw = chroma ? 2 : 4, sbh = chroma ? 2 : 4;
   const int rows = h / sbh, cols = w / sbw;
@@ -748,7 +750,7 @@ static int pred_blk_mm(Orc* o, int comp, const OPic* ref, int x, int y, int w, i
   const int rndRes = !bi;
   const int pi = chroma ? 1 : 0;
   const int refW = o->W >> chroma, refH = o->H >> chroma;
-  const int maxCUw = o->maxcu_w >> chroma, maxCUh = o->maxcu_h >> chroma;
+  const int maxCUw = enc ? 0 : o->maxcu_w >> chroma, maxCUh = enc ? 0 : o->maxcu_h >> chroma;
   const int16_t* org = ref->buf[pi] + (size_t)ref->margin[pi] * ref->stride[pi] + ref->margin[pi];
   const ptrdiff_t rs = ref->stride[pi];
   int16_t tmp[(4 + 7) * 4];
@@ -776,6 +778,11 @@ static int pred_blk_mm(Orc* o, int comp, const OPic* ref, int x, int y, int w, i
     }
   free(fx);
   return 0;
+}
+
+static int pred_blk_mm(Orc* o, int comp, const OPic* ref, int x, int y, int w, int h, int mvh, int mvv, int model,
+                       int bi, int cur_poc, int16_t* dst) {
+  return pred_blk_mm_x(o, comp, ref, x, y, w, h, mvh, mvv, model, bi, cur_poc, dst, 0);
 }
 
 /* ==========================================================================================
@@ -931,4 +938,49 @@ int orc_filter(int comp, int vertical, int bd, const int16_t* src, ptrdiff_t ss,
     filter_hor(comp, bd, src, ss, dst, ds, w, h, frac, last);
   }
   return 0;
+}
+
+/* Encoder candidate windows (mm_sad_window twin): for each block and candidate (i, j) in
+ * [-range, range]^2, xMVReprojectionInterpolation with rndRes = true (InterSearch.h:555-566) and
+ * RdCost::xGetSAD (RdCost.cpp:482-517: rows stepped by 1 << subShift, sum <<= subShift,
+ * FULL_NBIT so no distortion shift; the early exit only truncates values above the running best
+ * and is not modelled). */
+int orc_sad_window(void* h, int cur_poc, const mm_me_block* blocks, int n, int range, int step, int n_refs,
+                   const int32_t* pocs, const int16_t* const* ys, ptrdiff_t stride_y, const int16_t* org,
+                   ptrdiff_t org_stride, uint32_t* sads) {
+  Orc* o = (Orc*)h;
+  OPic* pics = (OPic*)calloc((size_t)n_refs, sizeof(OPic));
+  const int margin = 2 * (o->maxcu_w + 16);
+  for (int r = 0; r < n_refs; r++) {
+    pics[r].poc = pocs[r];
+    pad_plane(ys[r], stride_y, o->W, o->H, margin, &pics[r].buf[0], &pics[r].stride[0]);
+    pics[r].margin[0] = margin;
+  }
+  const int side = 2 * range + 1, C = side * side;
+  int16_t* pred = (int16_t*)malloc(sizeof(int16_t) * 128 * 128);
+  int rc = 0;
+  for (int b = 0; b < n && !rc; b++) {
+    const mm_me_block* k = &blocks[b];
+    const OPic* ref = NULL;
+    for (int r = 0; r < n_refs; r++)
+      if (pics[r].poc == k->ref_poc) ref = &pics[r];
+    if (!ref) { rc = MM_ERR_NOREF; break; }
+    for (int c = 0; c < C && !rc; c++) {
+      const int i = c % side - range, j = c / side - range;
+      rc = pred_blk_mm_x(o, 0, ref, k->x, k->y, k->w, k->h, k->mv_hor + i * step, k->mv_ver + j * step, k->model, 0,
+                         cur_poc, pred, 1);
+      uint64_t sum = 0;
+      const int sub = 1 << k->sub_shift;
+      for (int y = 0; y < k->h; y += sub)
+        for (int x = 0; x < k->w; x++) {
+          int d = org[(ptrdiff_t)(k->y + y) * org_stride + k->x + x] - pred[y * k->w + x];
+          sum += (uint64_t)(d < 0 ? -d : d);
+        }
+      sads[(size_t)b * C + c] = (uint32_t)(sum << k->sub_shift);
+    }
+  }
+  free(pred);
+  for (int r = 0; r < n_refs; r++) free(pics[r].buf[0]);
+  free(pics);
+  return rc;
 }

@@ -34,6 +34,8 @@ def load():
                              ctypes.c_ssize_t]
     lib.orc_filter.argtypes = [c_int, c_int, c_int, c_void_p, ctypes.c_ssize_t, c_void_p, ctypes.c_ssize_t, c_int,
                                c_int, c_int, c_int, c_int]
+    lib.orc_sad_window.argtypes = [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                                   ctypes.c_ssize_t, c_void_p, ctypes.c_ssize_t, c_void_p]
     return lib
 
 
@@ -88,6 +90,22 @@ class Oracle:
         if rc:
             raise RuntimeError(f"oracle predict failed: {rc}")
         return dy, dcb, dcr
+
+    def sad_window(self, cur_poc, blocks, range_, step, refs, org):
+        """Encoder candidate windows: uint32 SADs [n_blocks, (2*range+1)**2].  refs: poc -> luma."""
+        blocks = np.ascontiguousarray(blocks)
+        pocs = sorted(refs)
+        ys = [np.ascontiguousarray(refs[p]) for p in pocs]
+        org = np.ascontiguousarray(org, dtype=np.int16)
+        C = (2 * range_ + 1) ** 2
+        out = np.zeros((len(blocks), C), dtype=np.uint32)
+        pa = np.array(pocs, dtype=np.int32)
+        rc = self.lib.orc_sad_window(self.h, cur_poc, c_void_p(blocks.ctypes.data), len(blocks), range_, step,
+                                     len(pocs), c_void_p(pa.ctypes.data), _ptr_array(ys), ys[0].shape[1],
+                                     c_void_p(org.ctypes.data), org.shape[1], c_void_p(out.ctypes.data))
+        if rc:
+            raise RuntimeError(f"oracle sad_window failed: {rc}")
+        return out
 
     def filter(self, comp, vertical, bd, src, x0, y0, w, h, frac, first, last):
         src = np.ascontiguousarray(src, dtype=np.int16)

@@ -152,10 +152,124 @@ extern "C" int twin_pred(const mm_seq_params* p, int n_epi, const int32_t* epi, 
   for (int g = 0; g < m.n_elems; g++)
     reproj_thread(g, find_item(job_off.data(), job_chunk.data(), g, m.n_jobs), t.sc, jobs.data(), job_off.data(),
                   setups.data(), c, r.data());
-  const Taps taps{LUMA_T, CHROMA_T};
+  const Taps taps{LUMA_T, CHROMA_T, nullptr};
 #pragma omp parallel for schedule(static, 256)
   for (int g = 0; g < m.n_sb; g++)
     mc_thread(g, find_item(pu_off.data(), pu_chunk.data(), g, m.n_pus), t.geo, taps, dpus.data(), jobs.data(), r.data(),
               tab.ref, dy, sdy, dcb, dcr, sdc);
+  return 0;
+}
+
+// Host emulation of the device interior filter's tap-pair regrouping (mm_filter.h PackedTaps):
+// every phase, both window parities, random windows, both bi/uni -- against the scalar 2-D form.
+// Returns the number of mismatching samples.
+static int emu_dot2(uint32_t a, uint32_t b, int c) {
+  return c + (int)(int16_t)(a & 0xffff) * (int)(int16_t)(b & 0xffff) + (int)(int16_t)(a >> 16) * (int)(int16_t)(b >> 16);
+}
+template <int NT, int SBW, int SBH>
+static void emu_interior(const int16_t* ref, int stride, int xPos, int yPos, const uint32_t* ht, const uint32_t* vt,
+                         bool bi, int bd, int16_t* out) {
+  constexpr int R = SBH + NT - 1, H0 = NT / 2 - 1, L = SBW + NT - 1, ND = (L + 2) / 2, NP = NT / 2, NQ = NP + 1;
+  constexpr int RP = (R + 1) / 2;
+  const FiltParam fh = filt_param(true, false, bd), fv = filt_param(false, !bi, bd);
+  const int x0 = xPos - H0;
+  uint32_t tmp[R + 1][SBW] = {};
+  for (int r = 0; r < R; r++) {
+    const int16_t* row = ref + (long)(yPos + r - H0) * stride + (x0 & ~1);
+    uint32_t d[ND];
+    for (int m = 0; m < ND; m++) d[m] = (uint16_t)row[2 * m] | ((uint32_t)(uint16_t)row[2 * m + 1] << 16);
+    for (int c = 0; c < SBW; c++) {
+      const uint32_t* tp = ht + ((c & 1) ? NQ : 0);
+      int sum = fh.offset;
+      for (int k = 0; k < NQ; k++) sum = emu_dot2(d[(c >> 1) + k], tp[k], sum);
+      tmp[r][c] = (uint32_t)(sum >> fh.shift);
+    }
+  }
+  for (int c = 0; c < SBW; c++) {
+    uint32_t pr[RP];
+    for (int m = 0; m < RP; m++) pr[m] = (tmp[2 * m][c] & 0xffff) | (tmp[2 * m + 1][c] << 16);
+    for (int r = 0; r < SBH; r++) {
+      int sum = fv.offset;
+      if (r & 1)
+        for (int k = 0; k < NQ; k++) sum = emu_dot2(pr[(r >> 1) + k], vt[NP + k], sum);
+      else
+        for (int k = 0; k < NP; k++) sum = emu_dot2(pr[(r >> 1) + k], vt[k], sum);
+      int v = (int16_t)(sum >> fv.shift);
+      if (fv.clip) v = clip_pel(v, (1 << bd) - 1);
+      out[r * SBW + c] = (int16_t)v;
+    }
+  }
+}
+
+extern "C" long twin_packed_taps_selftest(int trials) {
+  static constexpr PackedTaps PT = make_packed_taps();
+  const int W = 64, H = 64;
+  std::vector<int16_t> img(W * H);
+  uint32_t seed = 12345;
+  auto rnd = [&]() { seed = seed * 1664525u + 1013904223u; return seed >> 8; };
+  long bad = 0;
+  for (int t = 0; t < trials; t++) {
+    const int bd = 8 + (int)(rnd() % 5);
+    for (auto& v : img) v = (int16_t)(rnd() % (1u << bd));
+    const bool bi = rnd() & 1;
+    for (int comp = 0; comp < 2; comp++) {
+      const int xPos = 8 + (int)(rnd() % 40), yPos = 8 + (int)(rnd() % 40);
+      if (comp == 0) {
+        const int xf = (int)(rnd() % 16), yf = (int)(rnd() % 16);
+        int16_t a[16], b[16];
+        predict_subblock<8, 4, 4>(img.data(), W, W, H, xPos, yPos, LUMA_T[xf], LUMA_T[yf], bi, bd, a);
+        emu_interior<8, 4, 4>(img.data(), W, xPos, yPos, PT.lh[xf][(xPos - 3) & 1], PT.lv[yf], bi, bd, b);
+        for (int i = 0; i < 16; i++) bad += a[i] != b[i];
+      } else {
+        const int xf = (int)(rnd() % 32), yf = (int)(rnd() % 32);
+        int16_t a[4], b[4];
+        predict_subblock<4, 2, 2>(img.data(), W, W, H, xPos, yPos, CHROMA_T[xf], CHROMA_T[yf], bi, bd, a);
+        emu_interior<4, 2, 2>(img.data(), W, xPos, yPos, PT.ch[xf][(xPos - 1) & 1], PT.cv[yf], bi, bd, b);
+        for (int i = 0; i < 4; i++) bad += a[i] != b[i];
+      }
+    }
+  }
+  return bad;
+}
+
+// Encoder candidate windows (mm_sad_window) through the product's planner and per-thread bodies.
+extern "C" int twin_sad_window(const mm_seq_params* p, int n_epi, const int32_t* epi, int cur_poc,
+                               const mm_me_block* blocks, int n, int range, int step, int n_refs, const int32_t* pocs,
+                               const int16_t* const* ys, int stride_y, const int16_t* org, int org_stride,
+                               uint32_t* sads) {
+  using namespace mmdev;
+  using namespace mmme;
+  Twin t;
+  make_twin(p, &t);
+  EpipoleMap em = epi_of(n_epi, epi);
+  std::vector<std::pair<int, RefDev>> refs;
+  for (int i = 0; i < n_refs; i++) refs.emplace_back(pocs[i], RefDev{ys[i], nullptr, nullptr, stride_y, 0});
+  std::sort(refs.begin(), refs.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+  PicTables tab;
+  std::string err;
+  int rc = build_pic_tables(seq_info(*p), em, cur_poc, refs, &tab, &err);
+  if (rc) return rc;
+  MeWindow w{range, step, 2 * range + 1, (2 * range + 1) * (2 * range + 1)};
+  std::vector<MeBatch> batches;
+  rc = plan_me_window(seq_info(*p), tab, blocks, n, w, &batches, &err);
+  if (rc) return rc;
+  for (long i = 0; i < (long)n * w.C; i++) sads[i] = 0;
+  const Taps taps{LUMA_T, CHROMA_T, nullptr};
+  MpaCache c = cache_of(t);
+  for (const MeBatch& bt : batches) {
+    std::vector<BlockSetup> setups(bt.n_jobs);
+#pragma omp parallel for schedule(static)
+    for (int j = 0; j < bt.n_jobs; j++) me_setup_thread(j, t.sc, w, bt.blocks.data(), tab.ged, setups.data());
+    const int nb = (int)bt.blocks.size();
+#pragma omp parallel for schedule(static, 256)
+    for (long g = 0; g < bt.n_elems; g++) {
+      int idx;
+      const int bi = find_item(bt.blk_off.data(), bt.chunk.data(), (int)g, nb);
+      uint32_t v = me_sad_thread((int)g, bi, t.sc, t.geo, taps, w, bt.blocks.data(), setups.data(), c, tab.ref, org,
+                                 org_stride, &idx);
+#pragma omp atomic
+      sads[idx] += v;
+    }
+  }
   return 0;
 }

@@ -17,6 +17,8 @@ def load():
     lib.twin_reproject.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]
     lib.twin_pred.argtypes = [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p,
                               c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int]
+    lib.twin_sad_window.argtypes = [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
+                                    c_void_p, c_int, c_void_p, c_int, c_void_p]
     return lib
 
 
@@ -57,3 +59,24 @@ def predict(params, cur_poc, pus, refs, W, H, epipoles=()):
     if rc:
         raise RuntimeError(f"twin predict failed: {rc}")
     return dy, dcb, dcr
+
+
+def sad_window(params, cur_poc, blocks, range_, step, refs, org, epipoles=()):
+    """refs: poc -> luma plane.  uint32 SADs [n_blocks, (2*range+1)**2]."""
+    lib = load()
+    blocks = np.ascontiguousarray(blocks)
+    pocs = sorted(refs)
+    ys = [np.ascontiguousarray(refs[p]) for p in pocs]
+    ptrs = (c_void_p * len(pocs))(*[a.ctypes.data for a in ys])
+    org = np.ascontiguousarray(org, dtype=np.int16)
+    C = (2 * range_ + 1) ** 2
+    out = np.zeros((len(blocks), C), dtype=np.uint32)
+    pa = np.array(pocs, dtype=np.int32)
+    n_epi, ea = _epi(epipoles)
+    rc = lib.twin_sad_window(ctypes.addressof(params), n_epi, c_void_p(ea.ctypes.data), cur_poc,
+                             c_void_p(blocks.ctypes.data), len(blocks), range_, step, len(pocs),
+                             c_void_p(pa.ctypes.data), ptrs, ys[0].shape[1], c_void_p(org.ctypes.data), org.shape[1],
+                             c_void_p(out.ctypes.data))
+    if rc:
+        raise RuntimeError(f"twin sad_window failed: {rc}")
+    return out

@@ -71,3 +71,16 @@ def test_two_d_form_equals_dispatch(nt, table, bd):
         two = (xf != 0) & (yf != 0)
         ref[two] = u[two]
         assert np.array_equal(u, ref), f"bi={bi}: {(u != ref).sum()} mismatches"
+
+
+def test_packed_tap_pair_regrouping_matches_scalar_filter():
+    """The device interior filter regroups the 8-/4-tap sums into v_dot2 tap pairs chosen by
+    output and window parity (mm_filter.h PackedTaps).  A host emulation of exactly that
+    arithmetic equals the scalar 2-D filter for random windows, every phase, bit depths 8-12,
+    bi and uni."""
+    import ctypes
+    import twin
+    lib = twin.load()
+    lib.twin_packed_taps_selftest.restype = ctypes.c_long
+    lib.twin_packed_taps_selftest.argtypes = [ctypes.c_int]
+    assert lib.twin_packed_taps_selftest(20000) == 0

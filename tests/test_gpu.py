@@ -305,3 +305,45 @@ def test_cpp_shim_example_on_gpu():
     assert os.path.exists(exe), "build with __graft_entry__.build() / make -C vvc-extension-mm_amd example"
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout + r.stderr
+
+
+ME_ALL = W.MPA3 + (mm360.TANGENTIAL, mm360.THREE_D_TRANSLATIONAL, mm360.ROTATIONAL, mm360.GEODESIC_CAMPOSE)
+
+
+def _me_ctx(params, w, h):
+    ctx = _ctx(params)
+    for poc in W.REF_POCS:
+        y, cb, cr = W.ref_planes(w, h, poc)
+        ctx.upload_ref(poc, y, cb, cr)
+    ctx.upload_org(W.CUR_POC, W.org_plane(w, h))
+    return ctx
+
+
+@pytest.mark.parametrize("step,sub_shift", [(16, 0), (4, 1)])
+def test_sad_window_vs_oracle(step, sub_shift):
+    """mm_sad_window (encoder candidate SADs) == the oracle, bit-exact, all models, edge blocks."""
+    from test_me import _case
+    w, h = 256, 128
+    params = mm360.seq_params(w, h, ME_ALL)
+    blocks, refs, org = _case(w, h, ME_ALL, 60, seed=3 + step, sub_shift=sub_shift)
+    want = Oracle(params, EPI).sad_window(W.CUR_POC, blocks, 3, step, refs, org)
+    with _me_ctx(params, w, h) as ctx:
+        got = ctx.sad_window(W.CUR_POC, blocks, 3, step).cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, want), np.argwhere(got != want)[:5]
+
+
+def test_sad_window_c5_full_window_vs_twin():
+    """C5 geometry (2048x1024, all models, 33x33 integer window) on a seeded subset of the PU
+    grid: the GPU equals the CPU twin of the same bodies, which the CPU suite ties to the oracle."""
+    import twin
+    w, h = 2048, 1024
+    params = mm360.seq_params(w, h, ME_ALL)
+    blocks = W.me_blocks(w, h, ME_ALL, grid=16, seed=11, max_blocks=96)
+    refs = {poc: W.ref_planes(w, h, poc)[0] for poc in W.REF_POCS}
+    org = W.org_plane(w, h)
+    want = twin.sad_window(params, W.CUR_POC, blocks, 16, 16, refs, org, EPI)
+    with _me_ctx(params, w, h) as ctx:
+        got = ctx.sad_window(W.CUR_POC, blocks, 16, 16).cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, want), np.argwhere(got != want)[:5]
+    # the search picks the same best candidate per block
+    assert np.array_equal(got.argmin(axis=1), want.argmin(axis=1))

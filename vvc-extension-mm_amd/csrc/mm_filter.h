@@ -31,6 +31,59 @@ namespace mmflt {
    {-2, 15, 55, -4}, {-2, 14, 56, -4}, {-2, 12, 57, -3}, {-2, 10, 58, -2}, {-1, 7, 60, -2},         \
    {0, 4, 62, -2},   {0, 2, 63, -1}}
 
+// Tap pairs for v_dot2 (int16 lo | int16 hi << 16), built at compile time from the tables above.
+// Horizontal pass, per phase and window-start parity p (the row is read from the even sample at
+// or below the window start, so p = 1 shifts every tap by one sample):
+//   A = (f0,f1) (f2,f3) ... (0,0)     B = (0,f0) (f1,f2) ... (f_{N-1},0)     C = (0,0) (f0,f1) ...
+//   p = 0: even outputs A, odd outputs B;   p = 1: even outputs B, odd outputs C
+// all applied to the aligned sample pairs starting at pair (c >> 1).  Vertical pass: even
+// output rows A without its zero pair, odd rows B, on the H-output row pairs (2m, 2m+1).
+struct PackedTaps {
+  uint32_t lh[16][2][10];  // luma H  [phase][parity][even 5 | odd 5]
+  uint32_t lv[16][9];      // luma V  [phase][even 4 | odd 5]
+  uint32_t ch[32][2][6];   // chroma H [phase][parity][even 3 | odd 3]
+  uint32_t cv[32][5];      // chroma V [phase][even 2 | odd 3]
+};
+constexpr uint32_t tap_pair_(int lo, int hi) { return ((uint32_t)lo & 0xffffu) | ((uint32_t)hi << 16); }
+template <int NT>
+constexpr void pair_sets_(const int8_t* f, uint32_t* A, uint32_t* B, uint32_t* C) {
+  for (int k = 0; k <= NT / 2; k++) {
+    A[k] = k < NT / 2 ? tap_pair_(f[2 * k], f[2 * k + 1]) : 0u;
+    B[k] = tap_pair_(k > 0 ? f[2 * k - 1] : 0, k < NT / 2 ? f[2 * k] : 0);
+    C[k] = k > 0 ? tap_pair_(f[2 * k - 2], f[2 * k - 1]) : 0u;
+  }
+}
+constexpr PackedTaps make_packed_taps() {
+  PackedTaps t{};
+  const int8_t L[16][8] = MM_LUMA_TAPS_INIT;
+  const int8_t Ch[32][4] = MM_CHROMA_TAPS_INIT;
+  for (int ph = 0; ph < 16; ph++) {
+    uint32_t A[5] = {}, B[5] = {}, C[5] = {};
+    pair_sets_<8>(L[ph], A, B, C);
+    for (int k = 0; k < 5; k++) {
+      t.lh[ph][0][k] = A[k];
+      t.lh[ph][0][5 + k] = B[k];
+      t.lh[ph][1][k] = B[k];
+      t.lh[ph][1][5 + k] = C[k];
+    }
+    for (int k = 0; k < 4; k++) t.lv[ph][k] = A[k];
+    for (int k = 0; k < 5; k++) t.lv[ph][4 + k] = B[k];
+  }
+  for (int ph = 0; ph < 32; ph++) {
+    uint32_t A[3] = {}, B[3] = {}, C[3] = {};
+    pair_sets_<4>(Ch[ph], A, B, C);
+    for (int k = 0; k < 3; k++) {
+      t.ch[ph][0][k] = A[k];
+      t.ch[ph][0][3 + k] = B[k];
+      t.ch[ph][1][k] = B[k];
+      t.ch[ph][1][3 + k] = C[k];
+    }
+    for (int k = 0; k < 2; k++) t.cv[ph][k] = A[k];
+    for (int k = 0; k < 3; k++) t.cv[ph][2 + k] = B[k];
+  }
+  return t;
+}
+
 constexpr int IF_INTERNAL_PREC = 14;
 constexpr int IF_FILTER_PREC = 6;
 constexpr int IF_INTERNAL_OFFS = 1 << (IF_INTERNAL_PREC - 1);
@@ -172,43 +225,47 @@ __device__ __forceinline__ uint32_t pack2_(int lo, int hi) {
 __device__ __forceinline__ uint32_t pack_lo16_(uint32_t lo, uint32_t hi) {
   return __builtin_amdgcn_perm(hi, lo, 0x05040100u);  // (lo & 0xffff) | (hi << 16), one v_perm_b32
 }
+// Head of a dot2 accumulation chain with a uniform seed: the VOP3P form takes the seed from an
+// SGPR, where the builtin would materialise it with a v_mov for v_dot2c.
+__device__ __forceinline__ int dot2_seed_(uint32_t a, uint32_t b, int seed) {
+  int r;
+  asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(seed));
+  return r;
+}
 // predict_subblock for an interior window (device): the same integer sums, regrouped as packed
-// int16 pairs so that each pair of taps is one v_dot2c_i32_i16:
-//  * a window row is loaded as dwords from the even sample below it; e[m] = samples (2m, 2m+1)
-//    (one v_alignbit when the window starts on an odd sample);
-//  * even outputs use the sample pairs e[] with the tap pairs (f0,f1), (f2,f3), ...; odd outputs
-//    use the same sample pairs with the shifted tap pairs (0,f0), (f1,f2), ..., (f_{N-1},0);
-//  * the rounding offsets seed the dot2 accumulators; the H outputs (Pel, 16 bits) are packed
-//    row pairs (one v_perm each) for the vertical pass, which uses the same even/odd tap trick.
+// int16 pairs so that each pair of taps is one v_dot2:
+//  * a window row is loaded as dwords from the even sample at or below its start; dword m holds
+//    the aligned sample pair m;
+//  * output c of a row is the dot product of pairs (c >> 1) .. (c >> 1) + NT/2 with one of the
+//    precomputed tap-pair sets of PackedTaps (chosen by output parity and window parity);
+//  * the rounding offsets seed the dot2 chains; the H outputs (Pel, 16 bits) are packed as row
+//    pairs (one v_perm each) for the vertical pass, which uses the even/odd tap sets the same way.
+// ht: 2 * NQ H tap pairs (even outputs, odd outputs) for this window's phase and parity;
+// vt: NP + NQ V tap pairs (even rows, odd rows).
 template <int NT, int SBW, int SBH>
 __device__ __forceinline__ void predict_subblock_interior(const int16_t* __restrict__ ref, int stride, int xPos, int yPos,
-                                                          const int8_t* cx, const int8_t* cy, bool bi, int bd,
+                                                          const uint32_t* __restrict__ ht,
+                                                          const uint32_t* __restrict__ vt, bool bi, int bd,
                                                           int16_t* out) {
-  constexpr int L = SBW + NT - 1, R = SBH + NT - 1, H0 = NT / 2 - 1;
+  constexpr int R = SBH + NT - 1, H0 = NT / 2 - 1;
+  constexpr int L = SBW + NT - 1;
   constexpr int ND = (L + 2) / 2;  // dwords loaded per row (L + 1 samples from the even base)
-  constexpr int NP = NT / 2;       // tap pairs of an even output
-  constexpr int NQ = NP + 1;       // shifted tap pairs of an odd output
+  constexpr int NP = NT / 2;       // tap pairs of an even V output
+  constexpr int NQ = NP + 1;       // tap pairs of an H output / odd V output
   constexpr int RP = (R + 1) / 2;  // packed H-output row pairs
   const int maxv = (1 << bd) - 1;
   const FiltParam fh = filt_param(true, false, bd);
   const FiltParam fv = filt_param(false, !bi, bd);
-  uint32_t he[NP], ho[NQ], ve[NP], vo[NQ];
+  uint32_t he[NQ], ho[NQ], ve[NP], vo[NQ];
 #pragma unroll
-  for (int k = 0; k < NP; k++) {
-    he[k] = pack2_(cx[2 * k], cx[2 * k + 1]);
-    ve[k] = pack2_(cy[2 * k], cy[2 * k + 1]);
+  for (int k = 0; k < NQ; k++) {
+    he[k] = ht[k];
+    ho[k] = ht[NQ + k];
+    vo[k] = vt[NP + k];
   }
-  ho[0] = pack2_(0, cx[0]);
-  vo[0] = pack2_(0, cy[0]);
 #pragma unroll
-  for (int k = 1; k < NP; k++) {
-    ho[k] = pack2_(cx[2 * k - 1], cx[2 * k]);
-    vo[k] = pack2_(cy[2 * k - 1], cy[2 * k]);
-  }
-  ho[NP] = pack2_(cx[NT - 1], 0);
-  vo[NP] = pack2_(cy[NT - 1], 0);
+  for (int k = 0; k < NP; k++) ve[k] = vt[k];
   const int x0 = xPos - H0;
-  const uint32_t sh = (x0 & 1) ? 16u : 0u;
   uint32_t tmp[R + 1][SBW];  // H outputs; only the low 16 bits are used
 #pragma unroll
   for (int c = 0; c < SBW; c++) tmp[R][c] = 0u;
@@ -217,19 +274,12 @@ __device__ __forceinline__ void predict_subblock_interior(const int16_t* __restr
     const uint32_t* p = reinterpret_cast<const uint32_t*>(ref + (long)(yPos + r - H0) * stride + (x0 & ~1));
     uint32_t d[ND];
     load_dwords<ND>(p, d);
-    uint32_t e[ND];
-#pragma unroll
-    for (int m = 0; m < ND; m++) e[m] = __builtin_amdgcn_alignbit(m + 1 < ND ? d[m + 1] : 0u, d[m], sh);
 #pragma unroll
     for (int c = 0; c < SBW; c++) {
-      int sum = fh.offset;
-      if (c & 1) {
+      const uint32_t* tp = (c & 1) ? ho : he;
+      int sum = dot2_seed_(d[c >> 1], tp[0], fh.offset);
 #pragma unroll
-        for (int k = 0; k < NQ; k++) sum = dot2_(e[(c >> 1) + k], ho[k], sum);
-      } else {
-#pragma unroll
-        for (int k = 0; k < NP; k++) sum = dot2_(e[(c >> 1) + k], he[k], sum);
-      }
+      for (int k = 1; k < NQ; k++) sum = dot2_(d[(c >> 1) + k], tp[k], sum);
       tmp[r][c] = (uint32_t)(sum >> fh.shift);
     }
   }
@@ -240,13 +290,15 @@ __device__ __forceinline__ void predict_subblock_interior(const int16_t* __restr
     for (int m = 0; m < RP; m++) pr[m] = pack_lo16_(tmp[2 * m][c], tmp[2 * m + 1][c]);
 #pragma unroll
     for (int r = 0; r < SBH; r++) {
-      int sum = fv.offset;
+      int sum;
       if (r & 1) {
+        sum = dot2_seed_(pr[r >> 1], vo[0], fv.offset);
 #pragma unroll
-        for (int k = 0; k < NQ; k++) sum = dot2_(pr[(r >> 1) + k], vo[k], sum);
+        for (int k = 1; k < NQ; k++) sum = dot2_(pr[(r >> 1) + k], vo[k], sum);
       } else {
+        sum = dot2_seed_(pr[r >> 1], ve[0], fv.offset);
 #pragma unroll
-        for (int k = 0; k < NP; k++) sum = dot2_(pr[(r >> 1) + k], ve[k], sum);
+        for (int k = 1; k < NP; k++) sum = dot2_(pr[(r >> 1) + k], ve[k], sum);
       }
       int v = (int16_t)(sum >> fv.shift);
       if (fv.clip) v = clip_pel(v, maxv);

@@ -38,6 +38,7 @@ namespace {
 
 __constant__ int8_t c_luma_taps[16][8] = MM_LUMA_TAPS_INIT;
 __constant__ int8_t c_chroma_taps[32][4] = MM_CHROMA_TAPS_INIT;
+__constant__ PackedTaps c_packed_taps = make_packed_taps();
 
 __global__ void k_mpa_cache(SeqConst sc, int plane, int cols, int rows, float* px, float* py, uint8_t* vip) {
   int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -211,8 +212,49 @@ __global__ void __launch_bounds__(256) k_mc_dev(Geometry geo, const PlanMeta* __
   if (g - (int)__lane_id() >= n_sb) return;  // whole wave past the end
   const int pi = wave_find_item(pu_offsets, chunk_start, g, meta->n_pus);
   if (g >= n_sb) return;
-  const Taps taps{c_luma_taps, c_chroma_taps};
+  const Taps taps{c_luma_taps, c_chroma_taps, &c_packed_taps};
   mc_thread(g, pi, geo, taps, pus, jobs, reproj, t.ref, dst_y, dsy, dst_cb, dst_cr, dsc);
+}
+
+// --------------------------------------------------------------------------------------------
+// Encoder candidate windows (mm_sad_window, mm_me.h)
+// --------------------------------------------------------------------------------------------
+using namespace mmme;
+
+__global__ void __launch_bounds__(256) k_me_setup(SeqConst sc, MeWindow w, const MeBlockDev* __restrict__ blocks,
+                                                  int n_jobs, const PicTables t, BlockSetup* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_jobs) return;
+  me_setup_thread(i, sc, w, blocks, t.ged, out);
+}
+
+// thread per (block, candidate, sub-block); the sub-block SADs of one candidate are summed
+// across the lanes that hold it (segmented shuffle scan) and added to sads[] by its last lane.
+__global__ void __launch_bounds__(256) k_me_sad(SeqConst sc, Geometry geo, MeWindow w,
+                                                const MeBlockDev* __restrict__ blocks, int n_blocks,
+                                                const int* __restrict__ blk_off, const int* __restrict__ chunk,
+                                                int n_elems, const BlockSetup* __restrict__ setups, MpaCache cache,
+                                                const PicTables t, const int16_t* __restrict__ org, int org_stride,
+                                                uint32_t* __restrict__ sads) {
+  const int g = xcd_block() * blockDim.x + threadIdx.x;
+  const int lane = __lane_id();
+  if (g - lane >= n_elems) return;  // whole wave past the end
+  const int bi = wave_find_item(blk_off, chunk, g, n_blocks);
+  const bool active = g < n_elems;
+  int idx = -1 - lane;  // inactive lanes: distinct keys that never merge
+  uint32_t v = 0;
+  if (active) {
+    const Taps taps{c_luma_taps, c_chroma_taps, &c_packed_taps};
+    v = me_sad_thread(g, bi, sc, geo, taps, w, blocks, setups, cache, t.ref, org, org_stride, &idx);
+  }
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t vu = __shfl_up(v, d);
+    const int iu = __shfl_up(idx, d);
+    if (lane >= d && iu == idx) v += vu;
+  }
+  const int inext = __shfl_down(idx, 1);
+  if (active && (lane == 63 || inext != idx)) atomicAdd(&sads[idx], v);
 }
 
 // InterpolationFilter::filter<N, isVertical, isFirst, isLast> / filterCopy on a raw block
@@ -310,6 +352,9 @@ struct mm_ctx {
   bool prepared = false;
   bool status_pending = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::map<int, RefHost> orgs;  // original luma pictures for mm_sad_window
+  DevBuf<MeBlockDev> d_me_blocks;
+  DevBuf<int> d_me_off, d_me_chunk;
   bool stage_timing = false;
   hipEvent_t ev_stage[3] = {nullptr, nullptr, nullptr};  // after planning, setup, reprojection
 };
@@ -461,6 +506,10 @@ int mm_destroy(mm_ctx* c) {
   c->d_cnt.release();
   c->d_meta.release();
   c->d_ged.release();
+  for (auto& kv : c->orgs) (void)hipFree(kv.second.y);
+  c->d_me_blocks.release();
+  c->d_me_off.release();
+  c->d_me_chunk.release();
   for (auto& e : c->ev_stage)
     if (e) (void)hipEventDestroy(e);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -669,6 +718,63 @@ int mm_last_timing(mm_ctx* c, float* ms) {
   if (!c || !ms) return MM_ERR_ARG;
   HIPCHK(c, hipEventSynchronize(c->ev1));
   HIPCHK(c, hipEventElapsedTime(ms, c->ev0, c->ev1));
+  return MM_OK;
+}
+
+int mm_upload_org(mm_ctx* c, int poc, const int16_t* y, ptrdiff_t sy, int src_dev) {
+  if (!c || !y) return MM_ERR_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  RefHost& r = c->orgs[poc];
+  if (!r.y) {
+    r.stride_y = (c->geo.W + 63) & ~63;
+    HIPCHK(c, hipMalloc(&r.y, (size_t)r.stride_y * c->geo.H * sizeof(int16_t)));
+  }
+  HIPCHK(c, hipMemcpy2DAsync(r.y, r.stride_y * 2, y, sy * 2, c->geo.W * 2, c->geo.H,
+                             src_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return MM_OK;
+}
+
+int mm_sad_window(mm_ctx* c, int cur_poc, const mm_me_block* blocks, int n, int range, int step, uint32_t* sads) {
+  if (!c || n < 0 || (n > 0 && (!blocks || !sads)) || range < 0 || range > 64 || step <= 0) return MM_ERR_ARG;
+  if (n == 0) return MM_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  auto oit = c->orgs.find(cur_poc);
+  if (oit == c->orgs.end()) return fail(c, MM_ERR_ARG, "no original picture uploaded for the current POC");
+  std::vector<std::pair<int, RefDev>> refs;
+  for (auto& kv : c->refs)
+    refs.emplace_back(kv.first, RefDev{kv.second.y, kv.second.cb, kv.second.cr, kv.second.stride_y, kv.second.stride_c});
+  PicTables t;
+  std::string err;
+  int rc = build_pic_tables(seq_info(c->prm), c->epipoles, cur_poc, refs, &t, &err);
+  if (rc) return fail(c, rc, err);
+  MeWindow w;
+  w.range = range;
+  w.step = step;
+  w.side = 2 * range + 1;
+  w.C = w.side * w.side;
+  std::vector<MeBatch> batches;
+  rc = plan_me_window(seq_info(c->prm), t, blocks, n, w, &batches, &err);
+  if (rc) return fail(c, rc, err);
+  HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+  HIPCHK(c, hipMemsetAsync(sads, 0, (size_t)n * w.C * sizeof(uint32_t), c->stream));
+  for (const MeBatch& bt : batches) {
+    RCCHK(upload(c, c->d_me_blocks, bt.blocks));
+    RCCHK(upload(c, c->d_me_off, bt.blk_off));
+    RCCHK(upload(c, c->d_me_chunk, bt.chunk));
+    HIPCHK(c, c->d_setup.ensure(bt.n_jobs));
+    hipLaunchKernelGGL(k_me_setup, dim3((bt.n_jobs + 255) / 256), dim3(256), 0, c->stream, c->sc, w, c->d_me_blocks.p,
+                       bt.n_jobs, t, c->d_setup.p);
+    const int ne = (int)bt.n_elems;
+    hipLaunchKernelGGL(k_me_sad, dim3(round_grid((ne + 255) / 256)), dim3(256), 0, c->stream, c->sc, c->geo, w,
+                       c->d_me_blocks.p, (int)bt.blocks.size(), c->d_me_off.p, c->d_me_chunk.p, ne, c->d_setup.p,
+                       make_cache(c), t, oit->second.y, oit->second.stride_y, sads);
+    HIPCHK(c, hipGetLastError());
+    // the host vectors of this batch are re-used by the next upload: wait for the copies
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   return MM_OK;
 }
 

@@ -56,6 +56,7 @@ struct Geometry {
 struct Taps {
   const int8_t (*luma)[8];
   const int8_t (*chroma)[4];
+  const PackedTaps* packed;  // tap pairs of the device interior filter
 };
 
 // item containing flat index g: chunk_start[g/64] is the item holding g rounded down to 64
@@ -190,8 +191,13 @@ MM_HD void mc_thread(int g, int pi, const Geometry& geo, const Taps& taps, const
     if (sb_out_of_range(xPos, yPos, geo.W, geo.H, geo.maxCUw, geo.maxCUh, 4, 4)) {
       for (int i = 0; i < 16; i++) pl[l][i] = 0;
     } else if (window_interior<8, 4, 4>(xPos, yPos, geo.W, geo.H)) {
-      predict_subblock_interior<8, 4, 4>(r.y, r.stride_y, xPos, yPos, taps.luma[xFrac],
-                                         taps.luma[yFrac], bi, geo.bd, pl[l]);
+#if defined(__HIP_DEVICE_COMPILE__)
+      predict_subblock_interior<8, 4, 4>(r.y, r.stride_y, xPos, yPos, taps.packed->lh[xFrac][(xPos - 3) & 1],
+                                         taps.packed->lv[yFrac], bi, geo.bd, pl[l]);
+#else
+      predict_subblock_interior<8, 4, 4>(r.y, r.stride_y, xPos, yPos, taps.luma[xFrac], taps.luma[yFrac], bi, geo.bd,
+                                         pl[l]);
+#endif
     } else {
       predict_subblock<8, 4, 4>(r.y, r.stride_y, geo.W, geo.H, xPos, yPos, taps.luma[xFrac],
                                 taps.luma[yFrac], bi, geo.bd, pl[l]);
@@ -223,10 +229,17 @@ MM_HD void mc_thread(int g, int pi, const Geometry& geo, const Taps& taps, const
     if (sb_out_of_range(xPos, yPos, geo.Wc, geo.Hc, geo.maxCUwc, geo.maxCUhc, 2, 2)) {
       for (int i = 0; i < 4; i++) pcb[l][i] = pcr[l][i] = 0;
     } else if (window_interior<4, 2, 2>(xPos, yPos, geo.Wc, geo.Hc)) {
-      predict_subblock_interior<4, 2, 2>(r.cb, r.stride_c, xPos, yPos, taps.chroma[xFrac],
-                                         taps.chroma[yFrac], bi, geo.bd, pcb[l]);
-      predict_subblock_interior<4, 2, 2>(r.cr, r.stride_c, xPos, yPos, taps.chroma[xFrac],
-                                         taps.chroma[yFrac], bi, geo.bd, pcr[l]);
+#if defined(__HIP_DEVICE_COMPILE__)
+      const uint32_t* ht = taps.packed->ch[xFrac][(xPos - 1) & 1];
+      const uint32_t* vt = taps.packed->cv[yFrac];
+      predict_subblock_interior<4, 2, 2>(r.cb, r.stride_c, xPos, yPos, ht, vt, bi, geo.bd, pcb[l]);
+      predict_subblock_interior<4, 2, 2>(r.cr, r.stride_c, xPos, yPos, ht, vt, bi, geo.bd, pcr[l]);
+#else
+      predict_subblock_interior<4, 2, 2>(r.cb, r.stride_c, xPos, yPos, taps.chroma[xFrac], taps.chroma[yFrac], bi,
+                                         geo.bd, pcb[l]);
+      predict_subblock_interior<4, 2, 2>(r.cr, r.stride_c, xPos, yPos, taps.chroma[xFrac], taps.chroma[yFrac], bi,
+                                         geo.bd, pcr[l]);
+#endif
     } else {
       predict_subblock<4, 2, 2>(r.cb, r.stride_c, geo.Wc, geo.Hc, xPos, yPos, taps.chroma[xFrac],
                                 taps.chroma[yFrac], bi, geo.bd, pcb[l]);

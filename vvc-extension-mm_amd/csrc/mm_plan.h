@@ -18,6 +18,7 @@
 
 #include "../../include/mm360.h"
 #include "mm_devplan.h"
+#include "mm_me.h"
 #include "mm_pipeline.h"
 
 namespace mmplan {
@@ -222,6 +223,81 @@ inline int build_pic_tables(const SeqInfo& s, const EpipoleMap& epi, int cur_poc
       t->ged_cam[k] = 3 + k;
     }
   }
+  return MM_OK;
+}
+
+// ---- encoder candidate windows (mm_sad_window) ---------------------------------------------
+// Batches of blocks with at most ME_BATCH_JOBS (block, candidate) jobs each; every block is
+// validated as the reference's CHECKs / preconditions would (geometry, model, reference,
+// epipole) before anything runs.
+constexpr long ME_BATCH_JOBS = 1L << 20;
+
+struct MeBatch {
+  std::vector<mmme::MeBlockDev> blocks;
+  std::vector<int> blk_off, chunk;  // element offsets per block, 64-element chunk starts
+  int n_jobs = 0;
+  long n_elems = 0;
+};
+
+inline int plan_me_window(const SeqInfo& s, const mmdev::PicTables& t, const mm_me_block* blocks, int n,
+                          const mmme::MeWindow& w, std::vector<MeBatch>* batches, std::string* err) {
+  batches->clear();
+  MeBatch cur;
+  for (int i = 0; i < n; i++) {
+    const mm_me_block& b = blocks[i];
+    if (b.w < 4 || b.h < 4 || b.w > 128 || b.h > 128 || (b.w & 3) || (b.h & 3) || (b.x & 3) || (b.y & 3) ||
+        b.x < 0 || b.y < 0 || b.x > s.W - b.w || b.y > s.H - b.h || b.sub_shift < 0 || b.sub_shift > 1) {
+      *err = "ME block " + std::to_string(i) + " outside the picture, not 4x4 aligned or invalid subShift";
+      return MM_ERR_ARG;
+    }
+    if (b.model <= CLASSIC || b.model >= NUM_MODELS || !(t.active & (1u << b.model))) {
+      *err = "ME block " + std::to_string(i) + ": invalid, CLASSIC or inactive motion model";
+      return MM_ERR_MODEL;
+    }
+    int slot = -1;
+    for (int k = 0; k < t.n_slots; k++)
+      if (t.poc[k] == b.ref_poc) slot = k;
+    if (slot < 0) {
+      *err = "ME block " + std::to_string(i) + ": reference POC " + std::to_string(b.ref_poc) + " not uploaded";
+      return MM_ERR_NOREF;
+    }
+    int ged = -1;
+    if (b.model == GEODESIC_CAMPOSE) {
+      if (t.ged_cam[slot] < 0) {
+        *err = "ME block " + std::to_string(i) + ": no epipole for (curPOC, refPOC)";
+        return MM_ERR_NOEPIPOLE;
+      }
+      ged = t.ged_cam[slot];
+    } else if (b.model >= GEODESIC_X && b.model <= GEODESIC_Z) {
+      ged = b.model - GEODESIC_X;
+    }
+    const int nsb = (b.w / 4) * (b.h / 4);
+    if (!cur.blocks.empty() && (long)cur.n_jobs + w.C > ME_BATCH_JOBS) {
+      batches->push_back(std::move(cur));
+      cur = MeBatch();
+    }
+    mmme::MeBlockDev d;
+    d.x = b.x;
+    d.y = b.y;
+    d.w = b.w;
+    d.h = b.h;
+    d.mvh = b.mv_hor;
+    d.mvv = b.mv_ver;
+    d.model = b.model;
+    d.slot = slot;
+    d.ged_idx = ged;
+    d.sub_shift = b.sub_shift;
+    d.n = nsb;
+    d.rows = b.h / 4;
+    d.elem_off = (int)cur.n_elems;
+    d.sad_off = i * w.C;
+    cur.blocks.push_back(d);
+    cur.blk_off.push_back(d.elem_off);
+    cur.n_jobs += w.C;
+    cur.n_elems += (long)w.C * nsb;
+  }
+  if (!cur.blocks.empty()) batches->push_back(std::move(cur));
+  for (auto& bt : *batches) build_chunks(bt.blk_off, (int)bt.n_elems, &bt.chunk);
   return MM_OK;
 }
 

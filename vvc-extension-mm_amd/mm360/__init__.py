@@ -49,7 +49,7 @@ EXPORTED_SYMBOLS = (
     "mm_create", "mm_destroy", "mm_set_stream", "mm_synchronize", "mm_last_error", "mm_get_version",
     "mm_set_epipole", "mm_upload_ref", "mm_release_ref", "mm_reproject", "mm_pred",
     "mm_pred_device", "mm_pred_status", "mm_pred_prepare", "mm_pred_run", "mm_filter", "mm_last_timing",
-    "mm_set_stage_timing", "mm_last_stage_timing",
+    "mm_set_stage_timing", "mm_last_stage_timing", "mm_upload_org", "mm_sad_window",
 )
 
 
@@ -75,7 +75,9 @@ BLOCK_DTYPE = np.dtype([("x", "<i4"), ("y", "<i4"), ("w", "<i4"), ("h", "<i4"), 
                         ("ref_poc", "<i4")])
 PU_DTYPE = np.dtype([("x", "<i4"), ("y", "<i4"), ("w", "<i4"), ("h", "<i4"), ("mv", "<i4", (2, 2)),
                      ("ref_poc", "<i4", (2,)), ("model", "<i4", (2,))])
-assert BLOCK_DTYPE.itemsize == 40 and PU_DTYPE.itemsize == 48
+ME_BLOCK_DTYPE = np.dtype([("x", "<i4"), ("y", "<i4"), ("w", "<i4"), ("h", "<i4"), ("mv_hor", "<i4"),
+                           ("mv_ver", "<i4"), ("model", "<i4"), ("ref_poc", "<i4"), ("sub_shift", "<i4")])
+assert BLOCK_DTYPE.itemsize == 40 and PU_DTYPE.itemsize == 48 and ME_BLOCK_DTYPE.itemsize == 36
 
 
 def active_mask(models: Sequence[int]) -> int:
@@ -127,6 +129,8 @@ def load_library() -> ctypes.CDLL:
                               c_int, c_int, c_int]),
         "mm_last_timing": (c_int, [vp, POINTER(c_float)]),
         "mm_set_stage_timing": (c_int, [vp, c_int]),
+        "mm_upload_org": (c_int, [vp, c_int, vp, ctypes.c_ssize_t, c_int]),
+        "mm_sad_window": (c_int, [vp, c_int, vp, c_int, c_int, c_int, vp]),
         "mm_last_stage_timing": (c_int, [vp, POINTER(c_float)]),
     }
     for name, (res, args) in sig.items():
@@ -294,6 +298,24 @@ class MMContext:
         ms = (c_float * 4)()
         self._check(self.lib.mm_last_stage_timing(self.h, ms))
         return tuple(float(v) for v in ms)
+
+    # -- encoder motion search (InterSearch::xMVReprojectionInterpolation + RdCost::xGetSAD) -
+    def upload_org(self, poc: int, y):
+        """Original luma picture of `poc` (numpy int16 host array or torch int16 CUDA tensor)."""
+        sy = y.strides[0] // 2 if isinstance(y, np.ndarray) else y.stride(0)
+        self._check(self.lib.mm_upload_org(self.h, poc, c_void_p(_ptr(y)), sy, int(_is_device(y))))
+
+    def sad_window(self, cur_poc: int, blocks: np.ndarray, range_: int, step: int = 16, out=None):
+        """SADs of every candidate of every block's window: a torch uint32-as-int32 CUDA tensor
+        [n_blocks, (2*range+1)**2] (candidate c = (j+range)*(2*range+1) + (i+range))."""
+        import torch
+        blocks = np.ascontiguousarray(blocks, dtype=ME_BLOCK_DTYPE)
+        C = (2 * range_ + 1) ** 2
+        if out is None:
+            out = torch.zeros((len(blocks), C), dtype=torch.int32, device=f"cuda:{self.device}")
+        self._check(self.lib.mm_sad_window(self.h, cur_poc, c_void_p(blocks.ctypes.data), len(blocks), range_, step,
+                                           c_void_p(_ptr(out))))
+        return out
 
     # -- InterpolationFilter -----------------------------------------------------------------
     def _filter(self, comp, vertical, src, x0, y0, w, h, frac, is_first, is_last):

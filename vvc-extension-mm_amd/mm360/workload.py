@@ -47,7 +47,10 @@ CONFIGS = {
     "C2": Config("C2", 2048, 1024, MPA3 + (GEODESIC_CAMPOSE, ROTATIONAL), 32,
                  "2048x1024 ERP decode, MPA+GED+ROT"),
     "C3": Config("C3", 6144, 3072, ALL_MODELS, 1, "6144x3072 ERP decode, all 5 motion models"),
+    "C5": Config("C5", 2048, 1024, ALL_MODELS, 1,
+                 "2048x1024 ERP encoder ME candidate eval: 16x16 PU grid x every model x 33x33 integer window"),
 }
+ME_RANGE = 16  # C5: 33x33 integer candidate window
 
 
 def ref_planes(width: int, height: int, poc: int, bit_depth: int = 10):
@@ -190,4 +193,29 @@ def random_blocks(width: int, height: int, models: Sequence[int], n: int, seed: 
         model = int(models[rng.integers(0, len(models))])
         out[i] = (x, y, wc, hc, mvh, mvv, model, comp if comp == 0 else int(rng.integers(1, 3)),
                   cur_poc, int(ref_pocs[rng.integers(0, len(ref_pocs))]))
+    return out
+
+
+def org_plane(width: int, height: int, poc: int = CUR_POC, bit_depth: int = 10) -> np.ndarray:
+    """Seeded 'original' luma picture for the encoder SAD (the reference content of POC `poc`
+    plus noise, so that good candidates exist)."""
+    y, _, _ = ref_planes(width, height, poc, bit_depth)
+    return y
+
+
+def me_blocks(width: int, height: int, models: Sequence[int], grid: int = 16, seed: int = 5,
+              ref_poc: int = REF_POCS[0], sub_shift: int = 0, max_blocks: int = None) -> np.ndarray:
+    """a grid x grid PU grid, every block once per active model, seeded window
+    centres (integer MVs within +-32 px, 1/16 units)."""
+    from . import ME_BLOCK_DTYPE
+    rng = np.random.default_rng(0x4D4D2000 + seed)
+    rows = []
+    for y in range(0, height, grid):
+        for x in range(0, width, grid):
+            for m in models:
+                mvx, mvy = (int(v) * 16 for v in rng.integers(-32, 33, size=2))
+                rows.append((x, y, grid, grid, mvx, mvy, int(m), ref_poc, sub_shift))
+    out = np.array(rows, dtype=ME_BLOCK_DTYPE)
+    if max_blocks is not None and len(out) > max_blocks:
+        out = out[rng.choice(len(out), size=max_blocks, replace=False)]
     return out
