@@ -17,6 +17,7 @@
  *                       xPredInterUni (InterPrediction.cpp:455-533) and xWeightedAverage
  *                       (addAvg / copyClip)               SRC/InterPrediction.cpp:1584-1679
  *   mm_filter        <- InterpolationFilter::filterHor/filterVer  SRC/InterpolationFilter.h:123-128
+ *   mm_pred_dmvr     <- InterPrediction::xProcessDMVRProjected  SRC/InterPrediction.cpp:2442-2634
  *   mm_sad_window    <- InterSearch::xMVReprojectionInterpolation + RdCost::xGetSAD per candidate
  *                       (EncoderLib/InterSearch.cpp:6277-6385, 363-443; SRC/RdCost.cpp:482-517)
  *   mm_upload_org    <- the original picture (pcPatternKey) the encoder SAD compares against
@@ -153,6 +154,18 @@ int mm_pred_status(mm_ctx* ctx, int* first_bad_pu);
 int mm_pred_prepare(mm_ctx* ctx, int cur_poc, const mm_pu_desc* pus, int n);
 int mm_pred_run(mm_ctx* ctx, int16_t* dst_y, ptrdiff_t dst_stride_y, int16_t* dst_cb,
                 int16_t* dst_cr, ptrdiff_t dst_stride_c);
+
+/* MM-DMVR (InterPrediction::xProcessDMVRProjected, InterPrediction.cpp:2442-2634): bi PUs that
+ * pass PU::checkDMVRCondition (UnitTools.cpp:1698-1726; equal models, w, h >= 8, w*h >= 128 are
+ * checked here, merge mode / POC distances / weights are the caller's decision).  Every
+ * min(w,16) x min(h,16) sub-PU runs the 25-point mirrored integer search and the parabolic sub-pel
+ * refinement on 14-bit luma predictions, then is predicted as a bi PU at the refined MVs (all
+ * components, addAvg) into the destination planes (device memory).  mvd_out (host, optional):
+ * the refined L0 delta (1/16 luma, pu.mvdL0SubPu) of every sub-PU, PU after PU, sub-PUs in raster
+ * order.  Synchronous. */
+int mm_pred_dmvr(mm_ctx* ctx, int cur_poc, const mm_pu_desc* pus, int n, int16_t* dst_y,
+                 ptrdiff_t dst_stride_y, int16_t* dst_cb, int16_t* dst_cr, ptrdiff_t dst_stride_c,
+                 int32_t* mvd_out);
 
 /* Single-block interpolation (InterpolationFilter::filterHor/filterVer on the device), for
  * parity tests of the integer pel pipeline.  comp 0 = luma 8-tap (16 phases), else chroma 4-tap

@@ -864,67 +864,195 @@ int orc_reproject(void* h, const mm_block_desc* b, int n, int32_t* out) {
 }
 
 /* mm_pred twin.  refs: n_refs pictures given as pocs[i] + planes (unpadded host planes). */
-int orc_pred(void* h, int cur_poc, const mm_pu_desc* pus, int n, int n_refs, const int32_t* pocs,
-             const int16_t* const* ys, const int16_t* const* cbs, const int16_t* const* crs, ptrdiff_t stride_y,
-             ptrdiff_t stride_c, int16_t* dy, ptrdiff_t sdy, int16_t* dcb, int16_t* dcr, ptrdiff_t sdc) {
-  Orc* o = (Orc*)h;
+/* One PU: xPredInterUni per list (xPredInterBlkMM per component) + xWeightedAverage
+ * (addAvg / copyClip, InterPrediction.cpp:1584-1679) into the destination planes. */
+static int pred_pu(Orc* o, const OPic* pics, int n_refs, const mm_pu_desc* u, int cur_poc, int16_t* pred[2][3],
+                   int16_t* dy, ptrdiff_t sdy, int16_t* dcb, int16_t* dcr, ptrdiff_t sdc) {
+  int rc = 0;
+  int bi = u->ref_poc[0] >= 0 && u->ref_poc[1] >= 0;
+  int ncomp = o->chroma ? 3 : 1;
+  for (int l = 0; l < 2 && !rc; l++) {
+    if (u->ref_poc[l] < 0) continue;
+    const OPic* ref = NULL;
+    for (int r = 0; r < n_refs; r++)
+      if (pics[r].poc == u->ref_poc[l]) ref = &pics[r];
+    if (!ref) return MM_ERR_NOREF;
+    for (int c = 0; c < ncomp && !rc; c++) {
+      int cs = c ? 1 : 0;
+      OPic tmp = *ref;
+      if (c == 2) { tmp.buf[1] = ref->buf[2]; tmp.stride[1] = ref->stride[2]; tmp.margin[1] = ref->margin[2]; }
+      rc = pred_blk_mm(o, c, &tmp, u->x >> cs, u->y >> cs, u->w >> cs, u->h >> cs, u->mv[l][0], u->mv[l][1],
+                       u->model[l], bi, cur_poc, pred[l][c]);
+    }
+  }
+  for (int c = 0; c < ncomp && !rc; c++) {
+    int cs = c ? 1 : 0, w = u->w >> cs, hh = u->h >> cs;
+    int16_t* d = c == 0 ? dy : (c == 1 ? dcb : dcr);
+    ptrdiff_t ds = c == 0 ? sdy : sdc;
+    d += (ptrdiff_t)(u->y >> cs) * ds + (u->x >> cs);
+    for (int y = 0; y < hh; y++)
+      for (int x = 0; x < w; x++) {
+        int k = y * w + x;
+        if (bi) { /* AreaBuf<Pel>::addAvg */
+          int shiftNum = frac_bits(o->bd) + 1, offset = (1 << (shiftNum - 1)) + 2 * 8192;
+          d[y * ds + x] = clip_pel((pred[0][c][k] + pred[1][c][k] + offset) >> shiftNum, o->bd);
+        } else { /* copyClip */
+          int l = u->ref_poc[0] >= 0 ? 0 : 1;
+          d[y * ds + x] = clip_pel(pred[l][c][k], o->bd);
+        }
+      }
+  }
+  return rc;
+}
+
+static OPic* pad_refs(Orc* o, int n_refs, const int32_t* pocs, const int16_t* const* ys, const int16_t* const* cbs,
+                      const int16_t* const* crs, ptrdiff_t stride_y, ptrdiff_t stride_c) {
   OPic* pics = (OPic*)calloc((size_t)n_refs, sizeof(OPic));
   const int margin = 2 * (o->maxcu_w + 16);
   for (int r = 0; r < n_refs; r++) {
     pics[r].poc = pocs[r];
     pad_plane(ys[r], stride_y, o->W, o->H, margin, &pics[r].buf[0], &pics[r].stride[0]);
     pics[r].margin[0] = margin;
-    if (o->chroma) {
+    if (o->chroma && cbs) {
       pad_plane(cbs[r], stride_c, o->Wc, o->Hc, margin / 2, &pics[r].buf[1], &pics[r].stride[1]);
       pad_plane(crs[r], stride_c, o->Wc, o->Hc, margin / 2, &pics[r].buf[2], &pics[r].stride[2]);
       pics[r].margin[1] = pics[r].margin[2] = margin / 2;
     }
   }
+  return pics;
+}
+
+static void free_refs(OPic* pics, int n_refs) {
+  for (int r = 0; r < n_refs; r++)
+    for (int c = 0; c < 3; c++) free(pics[r].buf[c]);
+  free(pics);
+}
+
+int orc_pred(void* h, int cur_poc, const mm_pu_desc* pus, int n, int n_refs, const int32_t* pocs,
+             const int16_t* const* ys, const int16_t* const* cbs, const int16_t* const* crs, ptrdiff_t stride_y,
+             ptrdiff_t stride_c, int16_t* dy, ptrdiff_t sdy, int16_t* dcb, int16_t* dcr, ptrdiff_t sdc) {
+  Orc* o = (Orc*)h;
+  OPic* pics = pad_refs(o, n_refs, pocs, ys, cbs, crs, stride_y, stride_c);
   int rc = 0;
   int16_t* pred[2][3];
   for (int l = 0; l < 2; l++)
     for (int c = 0; c < 3; c++) pred[l][c] = (int16_t*)malloc(sizeof(int16_t) * 128 * 128);
-  for (int i = 0; i < n && !rc; i++) {
-    const mm_pu_desc* u = &pus[i];
-    int bi = u->ref_poc[0] >= 0 && u->ref_poc[1] >= 0;
-    int ncomp = o->chroma ? 3 : 1;
-    for (int l = 0; l < 2 && !rc; l++) {
-      if (u->ref_poc[l] < 0) continue;
-      const OPic* ref = NULL;
-      for (int r = 0; r < n_refs; r++)
-        if (pics[r].poc == u->ref_poc[l]) ref = &pics[r];
-      if (!ref) { rc = MM_ERR_NOREF; break; }
-      for (int c = 0; c < ncomp && !rc; c++) {
-        int cs = c ? 1 : 0;
-        OPic tmp = *ref;
-        if (c == 2) { tmp.buf[1] = ref->buf[2]; tmp.stride[1] = ref->stride[2]; tmp.margin[1] = ref->margin[2]; }
-        rc = pred_blk_mm(o, c, &tmp, u->x >> cs, u->y >> cs, u->w >> cs, u->h >> cs, u->mv[l][0], u->mv[l][1],
-                         u->model[l], bi, cur_poc, pred[l][c]);
-      }
-    }
-    for (int c = 0; c < ncomp && !rc; c++) {
-      int cs = c ? 1 : 0, w = u->w >> cs, hh = u->h >> cs;
-      int16_t* d = c == 0 ? dy : (c == 1 ? dcb : dcr);
-      ptrdiff_t ds = c == 0 ? sdy : sdc;
-      d += (ptrdiff_t)(u->y >> cs) * ds + (u->x >> cs);
-      for (int y = 0; y < hh; y++)
-        for (int x = 0; x < w; x++) {
-          int k = y * w + x;
-          if (bi) { /* AreaBuf<Pel>::addAvg */
-            int shiftNum = frac_bits(o->bd) + 1, offset = (1 << (shiftNum - 1)) + 2 * 8192;
-            d[y * ds + x] = clip_pel((pred[0][c][k] + pred[1][c][k] + offset) >> shiftNum, o->bd);
-          } else { /* copyClip */
-            int l = u->ref_poc[0] >= 0 ? 0 : 1;
-            d[y * ds + x] = clip_pel(pred[l][c][k], o->bd);
-          }
-        }
-    }
-  }
+  for (int i = 0; i < n && !rc; i++) rc = pred_pu(o, pics, n_refs, &pus[i], cur_poc, pred, dy, sdy, dcb, dcr, sdc);
   for (int l = 0; l < 2; l++)
     for (int c = 0; c < 3; c++) free(pred[l][c]);
-  for (int r = 0; r < n_refs; r++)
-    for (int c = 0; c < 3; c++) free(pics[r].buf[c]);
-  free(pics);
+  free_refs(pics, n_refs);
+  return rc;
+}
+
+/* ---- MM-DMVR: InterPrediction::xProcessDMVRProjected (InterPrediction.cpp:2442-2634) ---- */
+
+/* xDMVRCost (:2147-2155): RdCost SAD with subShift 1 (even rows, sum <<= 1), then >> 1 */
+static uint64_t dmvr_cost(const int16_t* p0, const int16_t* p1, int w, int h) {
+  uint64_t sum = 0;
+  for (int y = 0; y < h; y += 2)
+    for (int x = 0; x < w; x++) {
+      int d = p0[y * w + x] - p1[y * w + x];
+      sum += (uint64_t)(d < 0 ? -d : d);
+    }
+  return (sum << 1) >> 1;
+}
+
+static int32_t div_for_maxq7(int64_t N, int64_t D) { /* :1958-1994 */
+  int32_t sign = 0, q = 0;
+  if (N < 0) { sign = 1; N = -N; }
+  D = D << 3;
+  if (N >= D) { N -= D; q++; }
+  q = q << 1;
+  D = D >> 1;
+  if (N >= D) { N -= D; q++; }
+  q = q << 1;
+  if (N >= (D >> 1)) q++;
+  return sign ? -q : q;
+}
+
+static void sub_pel_error_srfc(const uint64_t* sadBuffer, int32_t* deltaMv) { /* :1996-2048 */
+  int64_t numerator, denominator;
+  numerator = (int64_t)((sadBuffer[1] - sadBuffer[3]) << 4);
+  denominator = (int64_t)((sadBuffer[1] + sadBuffer[3] - (sadBuffer[0] << 1)));
+  if (0 != denominator) {
+    if ((sadBuffer[1] != sadBuffer[0]) && (sadBuffer[3] != sadBuffer[0])) deltaMv[0] = div_for_maxq7(numerator, denominator);
+    else deltaMv[0] = (sadBuffer[1] == sadBuffer[0]) ? -8 : 8;
+  }
+  numerator = (int64_t)((sadBuffer[2] - sadBuffer[4]) << 4);
+  denominator = (int64_t)((sadBuffer[2] + sadBuffer[4] - (sadBuffer[0] << 1)));
+  if (0 != denominator) {
+    if ((sadBuffer[2] != sadBuffer[0]) && (sadBuffer[4] != sadBuffer[0])) deltaMv[1] = div_for_maxq7(numerator, denominator);
+    else deltaMv[1] = (sadBuffer[2] == sadBuffer[0]) ? -8 : 8;
+  }
+}
+
+static int clip_mv18(int v) { return v < -(1 << 17) ? -(1 << 17) : (v > (1 << 17) - 1 ? (1 << 17) - 1 : v); }
+
+int orc_pred_dmvr(void* h, int cur_poc, const mm_pu_desc* pus, int n, int n_refs, const int32_t* pocs,
+                  const int16_t* const* ys, const int16_t* const* cbs, const int16_t* const* crs, ptrdiff_t stride_y,
+                  ptrdiff_t stride_c, int16_t* dy, ptrdiff_t sdy, int16_t* dcb, int16_t* dcr, ptrdiff_t sdc,
+                  int32_t* mvd_out) {
+  Orc* o = (Orc*)h;
+  OPic* pics = pad_refs(o, n_refs, pocs, ys, cbs, crs, stride_y, stride_c);
+  int rc = 0, k = 0;
+  int16_t* pred[2][3];
+  for (int l = 0; l < 2; l++)
+    for (int c = 0; c < 3; c++) pred[l][c] = (int16_t*)malloc(sizeof(int16_t) * 128 * 128);
+  int16_t* s0 = (int16_t*)malloc(sizeof(int16_t) * 16 * 16);
+  int16_t* s1 = (int16_t*)malloc(sizeof(int16_t) * 16 * 16);
+  for (int i = 0; i < n && !rc; i++) {
+    const mm_pu_desc* u = &pus[i];
+    const OPic *r0 = NULL, *r1 = NULL;
+    for (int r = 0; r < n_refs; r++) {
+      if (pics[r].poc == u->ref_poc[0]) r0 = &pics[r];
+      if (pics[r].poc == u->ref_poc[1]) r1 = &pics[r];
+    }
+    if (!r0 || !r1) { rc = MM_ERR_NOREF; break; }
+    const int dxs = u->w < 16 ? u->w : 16, dys = u->h < 16 ? u->h : 16, model = u->model[0];
+    for (int y = u->y; y < u->y + u->h && !rc; y += dys)
+      for (int x = u->x; x < u->x + u->w && !rc; x += dxs) {
+        uint64_t sads[25];
+        for (int j = 0; j < 25; j++) sads[j] = UINT64_MAX;
+        int tdx = 0, tdy = 0, notZeroCost = 1;
+        rc = pred_blk_mm(o, 0, r0, x, y, dxs, dys, u->mv[0][0], u->mv[0][1], model, 1, cur_poc, s0);
+        if (!rc) rc = pred_blk_mm(o, 0, r1, x, y, dxs, dys, u->mv[1][0], u->mv[1][1], model, 1, cur_poc, s1);
+        uint64_t minCost = dmvr_cost(s0, s1, dxs, dys);
+        minCost -= (minCost >> 2);
+        if (minCost < (uint64_t)(dxs * dys)) notZeroCost = 0;
+        int best = 12;
+        if (notZeroCost) {
+          sads[12] = minCost;
+          for (int j = 0; j < 25 && !rc; j++) {
+            const int ox = j % 5 - 2, oy = j / 5 - 2;
+            rc = pred_blk_mm(o, 0, r0, x, y, dxs, dys, u->mv[0][0] + ox * 16, u->mv[0][1] + oy * 16, model, 1, cur_poc, s0);
+            if (!rc) rc = pred_blk_mm(o, 0, r1, x, y, dxs, dys, u->mv[1][0] - ox * 16, u->mv[1][1] - oy * 16, model, 1, cur_poc, s1);
+            if (sads[j] == UINT64_MAX) sads[j] = dmvr_cost(s0, s1, dxs, dys);
+            if (sads[j] < minCost) { minCost = sads[j]; best = j; }
+          }
+          tdx = (best % 5 - 2) << 4;
+          tdy = (best / 5 - 2) << 4;
+          if (abs(tdx) != 32 && abs(tdy) != 32) {
+            uint64_t sb[5] = {sads[best], sads[best - 1], sads[best - 5], sads[best + 1], sads[best + 5]};
+            int32_t d[2] = {0, 0};
+            sub_pel_error_srfc(sb, d);
+            tdx += d[0];
+            tdy += d[1];
+          }
+        }
+        if (mvd_out) { mvd_out[2 * k] = tdx; mvd_out[2 * k + 1] = tdy; }
+        k++;
+        mm_pu_desc sp = *u;
+        sp.x = x; sp.y = y; sp.w = dxs; sp.h = dys;
+        sp.mv[0][0] = clip_mv18(u->mv[0][0] + tdx); sp.mv[0][1] = clip_mv18(u->mv[0][1] + tdy);
+        sp.mv[1][0] = clip_mv18(u->mv[1][0] - tdx); sp.mv[1][1] = clip_mv18(u->mv[1][1] - tdy);
+        if (!rc) rc = pred_pu(o, pics, n_refs, &sp, cur_poc, pred, dy, sdy, dcb, dcr, sdc);
+      }
+  }
+  free(s0);
+  free(s1);
+  for (int l = 0; l < 2; l++)
+    for (int c = 0; c < 3; c++) free(pred[l][c]);
+  free_refs(pics, n_refs);
   return rc;
 }
 

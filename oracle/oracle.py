@@ -34,6 +34,9 @@ def load():
                              ctypes.c_ssize_t]
     lib.orc_filter.argtypes = [c_int, c_int, c_int, c_void_p, ctypes.c_ssize_t, c_void_p, ctypes.c_ssize_t, c_int,
                                c_int, c_int, c_int, c_int]
+    lib.orc_pred_dmvr.argtypes = [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                  ctypes.c_ssize_t, ctypes.c_ssize_t, c_void_p, ctypes.c_ssize_t, c_void_p, c_void_p,
+                                  ctypes.c_ssize_t, c_void_p]
     lib.orc_sad_window.argtypes = [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                    ctypes.c_ssize_t, c_void_p, ctypes.c_ssize_t, c_void_p]
     return lib
@@ -90,6 +93,28 @@ class Oracle:
         if rc:
             raise RuntimeError(f"oracle predict failed: {rc}")
         return dy, dcb, dcr
+
+    def predict_dmvr(self, cur_poc, pus, refs, W, H):
+        """MM-DMVR PUs (xProcessDMVRProjected): predicted planes and the per-sub-PU L0 deltas."""
+        pus = np.ascontiguousarray(pus)
+        pocs = sorted(refs)
+        ys = [np.ascontiguousarray(refs[p][0]) for p in pocs]
+        cbs = [np.ascontiguousarray(refs[p][1]) for p in pocs]
+        crs = [np.ascontiguousarray(refs[p][2]) for p in pocs]
+        dy = np.zeros((H, W), dtype=np.int16)
+        dcb = np.zeros((H // 2, W // 2), dtype=np.int16)
+        dcr = np.zeros((H // 2, W // 2), dtype=np.int16)
+        nsub = int(sum(((int(u["w"]) + 15) // 16) * ((int(u["h"]) + 15) // 16) for u in pus))
+        mvd = np.zeros((max(nsub, 1), 2), dtype=np.int32)
+        pa = np.array(pocs, dtype=np.int32)
+        rc = self.lib.orc_pred_dmvr(self.h, cur_poc, c_void_p(pus.ctypes.data), len(pus), len(pocs),
+                                    c_void_p(pa.ctypes.data), _ptr_array(ys), _ptr_array(cbs), _ptr_array(crs),
+                                    ys[0].shape[1], cbs[0].shape[1], c_void_p(dy.ctypes.data), W,
+                                    c_void_p(dcb.ctypes.data), c_void_p(dcr.ctypes.data), W // 2,
+                                    c_void_p(mvd.ctypes.data))
+        if rc:
+            raise RuntimeError(f"oracle predict_dmvr failed: {rc}")
+        return (dy, dcb, dcr), mvd[:nsub]
 
     def sad_window(self, cur_poc, blocks, range_, step, refs, org):
         """Encoder candidate windows: uint32 SADs [n_blocks, (2*range+1)**2].  refs: poc -> luma."""

@@ -94,25 +94,10 @@ extern "C" int twin_reproject(const mm_seq_params* p, int n_epi, const int32_t* 
   return 0;
 }
 
-// Device-planned prediction (mm_pred_device), run sequentially: classify every PU, count per
-// bucket, place PUs/jobs with per-bucket cursors (arrival order = list order), then the setup /
-// reprojection / MC bodies over the planned lists.
-extern "C" int twin_pred(const mm_seq_params* p, int n_epi, const int32_t* epi, int cur_poc, const mm_pu_desc* pus,
-                         int n, int n_refs, const int32_t* pocs, const int16_t* const* ys, const int16_t* const* cbs,
-                         const int16_t* const* crs, int stride_y, int stride_c, int16_t* dy, int sdy, int16_t* dcb,
-                         int16_t* dcr, int sdc) {
+// The device-planned prediction path (mm_devplan.h + mm_pipeline.h bodies), run sequentially.
+static int twin_pred_list(const Twin& t, const mmdev::PicTables& tab, const mm_pu_desc* pus, int n, int16_t* dy,
+                          int sdy, int16_t* dcb, int16_t* dcr, int sdc) {
   using namespace mmdev;
-  Twin t;
-  make_twin(p, &t);
-  EpipoleMap em = epi_of(n_epi, epi);
-  std::vector<std::pair<int, RefDev>> refs;
-  for (int i = 0; i < n_refs; i++)
-    refs.emplace_back(pocs[i], RefDev{ys[i], cbs ? cbs[i] : nullptr, crs ? crs[i] : nullptr, stride_y, stride_c});
-  std::sort(refs.begin(), refs.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
-  PicTables tab;
-  std::string err;
-  int rc = build_pic_tables(seq_info(*p), em, cur_poc, refs, &tab, &err);
-  if (rc) return rc;
   std::vector<PuPlan> plans(n);
   PlanCounters cnt{};
   for (int i = 0; i < n; i++) {
@@ -158,6 +143,28 @@ extern "C" int twin_pred(const mm_seq_params* p, int n_epi, const int32_t* epi, 
     mc_thread(g, find_item(pu_off.data(), pu_chunk.data(), g, m.n_pus), t.geo, taps, dpus.data(), jobs.data(), r.data(),
               tab.ref, dy, sdy, dcb, dcr, sdc);
   return 0;
+}
+
+// Device-planned prediction (mm_pred_device), run sequentially: classify every PU, count per
+// bucket, place PUs/jobs with per-bucket cursors (arrival order = list order), then the setup /
+// reprojection / MC bodies over the planned lists.
+extern "C" int twin_pred(const mm_seq_params* p, int n_epi, const int32_t* epi, int cur_poc, const mm_pu_desc* pus,
+                         int n, int n_refs, const int32_t* pocs, const int16_t* const* ys, const int16_t* const* cbs,
+                         const int16_t* const* crs, int stride_y, int stride_c, int16_t* dy, int sdy, int16_t* dcb,
+                         int16_t* dcr, int sdc) {
+  using namespace mmdev;
+  Twin t;
+  make_twin(p, &t);
+  EpipoleMap em = epi_of(n_epi, epi);
+  std::vector<std::pair<int, RefDev>> refs;
+  for (int i = 0; i < n_refs; i++)
+    refs.emplace_back(pocs[i], RefDev{ys[i], cbs ? cbs[i] : nullptr, crs ? crs[i] : nullptr, stride_y, stride_c});
+  std::sort(refs.begin(), refs.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+  PicTables tab;
+  std::string err;
+  int rc = build_pic_tables(seq_info(*p), em, cur_poc, refs, &tab, &err);
+  if (rc) return rc;
+  return twin_pred_list(t, tab, pus, n, dy, sdy, dcb, dcr, sdc);
 }
 
 // Host emulation of the device interior filter's tap-pair regrouping (mm_filter.h PackedTaps):
@@ -272,4 +279,49 @@ extern "C" int twin_sad_window(const mm_seq_params* p, int n_epi, const int32_t*
     }
   }
   return 0;
+}
+
+// MM-DMVR (mm_pred_dmvr): the product's planner and mm_dmvr.h bodies, then the refined sub-PUs
+// through the device-planned prediction path.
+extern "C" int twin_pred_dmvr(const mm_seq_params* p, int n_epi, const int32_t* epi, int cur_poc,
+                              const mm_pu_desc* pus, int n, int n_refs, const int32_t* pocs,
+                              const int16_t* const* ys, const int16_t* const* cbs, const int16_t* const* crs,
+                              int stride_y, int stride_c, int16_t* dy, int sdy, int16_t* dcb, int16_t* dcr, int sdc,
+                              int32_t* mvd_out) {
+  using namespace mmdev;
+  using namespace mmdmvr;
+  Twin t;
+  make_twin(p, &t);
+  EpipoleMap em = epi_of(n_epi, epi);
+  std::vector<std::pair<int, RefDev>> refs;
+  for (int i = 0; i < n_refs; i++)
+    refs.emplace_back(pocs[i], RefDev{ys[i], cbs ? cbs[i] : nullptr, crs ? crs[i] : nullptr, stride_y, stride_c});
+  std::sort(refs.begin(), refs.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+  PicTables tab;
+  std::string err;
+  int rc = build_pic_tables(seq_info(*p), em, cur_poc, refs, &tab, &err);
+  if (rc) return rc;
+  DmvrPlan plan;
+  rc = plan_dmvr(seq_info(*p), tab, pus, n, &plan, &err);
+  if (rc) return rc;
+  const int ns = (int)plan.sub.size();
+  std::vector<BlockSetup> setups((size_t)ns * N_OFF * 2);
+#pragma omp parallel for schedule(static)
+  for (int j = 0; j < ns * N_OFF * 2; j++) dmvr_setup_thread(j, t.sc, plan.sub.data(), tab.ged, setups.data());
+  std::vector<uint32_t> costs((size_t)ns * N_OFF, 0);
+  const Taps taps{LUMA_T, CHROMA_T, nullptr};
+  MpaCache c = cache_of(t);
+#pragma omp parallel for schedule(static, 256)
+  for (long g = 0; g < plan.n_elems; g++) {
+    int idx;
+    const int si = find_item(plan.off.data(), plan.chunk.data(), (int)g, ns);
+    uint32_t v = dmvr_cost_thread((int)g, si, t.sc, t.geo, taps, plan.sub.data(), setups.data(), c, tab.ref, &idx);
+#pragma omp atomic
+    costs[idx] += v;
+  }
+  std::vector<mm_pu_desc> refined(ns);
+  std::vector<int32_t> mvd(2 * (size_t)ns);
+  for (int s = 0; s < ns; s++) dmvr_decide_thread(s, plan.sub.data(), costs.data(), refined.data(), mvd.data());
+  if (mvd_out) std::copy(mvd.begin(), mvd.end(), mvd_out);
+  return twin_pred_list(t, tab, refined.data(), ns, dy, sdy, dcb, dcr, sdc);
 }

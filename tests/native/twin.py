@@ -17,6 +17,9 @@ def load():
     lib.twin_reproject.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]
     lib.twin_pred.argtypes = [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p,
                               c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int]
+    lib.twin_pred_dmvr.argtypes = [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
+                                   c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int,
+                                   c_void_p]
     lib.twin_sad_window.argtypes = [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
                                     c_void_p, c_int, c_void_p, c_int, c_void_p]
     return lib
@@ -80,3 +83,25 @@ def sad_window(params, cur_poc, blocks, range_, step, refs, org, epipoles=()):
     if rc:
         raise RuntimeError(f"twin sad_window failed: {rc}")
     return out
+
+
+def predict_dmvr(params, cur_poc, pus, refs, W, H, epipoles=()):
+    lib = load()
+    pus = np.ascontiguousarray(pus)
+    pocs = sorted(refs)
+    arrs = [[np.ascontiguousarray(refs[p][k]) for p in pocs] for k in range(3)]
+    ptrs = [(c_void_p * len(pocs))(*[a.ctypes.data for a in arrs[k]]) for k in range(3)]
+    dy = np.zeros((H, W), dtype=np.int16)
+    dcb = np.zeros((H // 2, W // 2), dtype=np.int16)
+    dcr = np.zeros((H // 2, W // 2), dtype=np.int16)
+    nsub = int(sum(((int(u["w"]) + 15) // 16) * ((int(u["h"]) + 15) // 16) for u in pus))
+    mvd = np.zeros((max(nsub, 1), 2), dtype=np.int32)
+    pa = np.array(pocs, dtype=np.int32)
+    n_epi, ea = _epi(epipoles)
+    rc = lib.twin_pred_dmvr(ctypes.addressof(params), n_epi, c_void_p(ea.ctypes.data), cur_poc,
+                            c_void_p(pus.ctypes.data), len(pus), len(pocs), c_void_p(pa.ctypes.data), ptrs[0], ptrs[1],
+                            ptrs[2], arrs[0][0].shape[1], arrs[1][0].shape[1], c_void_p(dy.ctypes.data), W,
+                            c_void_p(dcb.ctypes.data), c_void_p(dcr.ctypes.data), W // 2, c_void_p(mvd.ctypes.data))
+    if rc:
+        raise RuntimeError(f"twin predict_dmvr failed: {rc}")
+    return (dy, dcb, dcr), mvd[:nsub]

@@ -347,3 +347,23 @@ def test_sad_window_c5_full_window_vs_twin():
     assert np.array_equal(got, want), np.argwhere(got != want)[:5]
     # the search picks the same best candidate per block
     assert np.array_equal(got.argmin(axis=1), want.argmin(axis=1))
+
+
+@pytest.mark.parametrize("w,h", [(256, 128), (1024, 512)])
+def test_pred_dmvr_vs_oracle(w, h):
+    """MM-DMVR on the GPU == the oracle: refined per-sub-PU deltas and predicted planes."""
+    models = ME_ALL
+    cfg = W.Config("T", w, h, tuple(models), 1, "test")
+    params = mm360.seq_params(w, h, models)
+    pus = W.dmvr_pu_list(cfg, frame=2)
+    refs = {poc: W.ref_planes(w, h, poc) for poc in W.REF_POCS}
+    want, want_mvd = Oracle(params, EPI).predict_dmvr(W.CUR_POC, pus, refs, w, h)
+    with _ctx(params) as ctx:
+        for poc, (y, cb, cr) in refs.items():
+            ctx.upload_ref(poc, y, cb, cr)
+        dst = _planes(cfg)
+        mvd = ctx.predict_dmvr(W.CUR_POC, pus, *dst)
+    assert np.array_equal(mvd, want_mvd), np.argwhere(mvd != want_mvd)[:5]
+    for name, t, x in zip(("y", "cb", "cr"), dst, want):
+        got = t.cpu().numpy()
+        assert np.array_equal(got, x), describe_mismatch(name, got, x)

@@ -1,0 +1,189 @@
+// mm_dmvr.h -- MM decoder-side motion vector refinement (host + device bodies).
+//
+// InterPrediction::xProcessDMVRProjected (CommonLib/InterPrediction.cpp:2442-2634), reached from
+// xPredInterBi -> xProcessDMVRMM (:2225-2237) for bi PUs that pass PU::checkDMVRCondition
+// (UnitTools.cpp:1698-1726).  Per sub-PU of min(w,16) x min(h,16) luma samples:
+//   1. luma 14-bit predictions of both lists at the merge MVs, cost = xDMVRCost (SAD over the even
+//      rows, :2147-2155); minCost = cost - cost/4; minCost < dx*dy ends the search (no refinement);
+//   2. one iteration over the 25 mirrored integer offsets of m_pSearchOffset (InterPrediction.h:107):
+//      L0 at merge0 + off, L1 at merge1 - off, cost per offset, first strict minimum in scan order
+//      (the centre entry holds the adjusted minCost);
+//   3. parabolic sub-pel refinement from the 5 costs around the best offset unless it lies on the
+//      window border (xDMVRSubPixelErrorSurface :2157-2175, xSubPelErrorSrfc :1996-2048);
+//   4. the sub-PU is predicted as a bi PU at merge0 + mvd / merge1 - mvd (all components, addAvg).
+// Steps 1-3 run here (k_dmvr_setup, k_dmvr_cost, k_dmvr_decide); step 4 is the ordinary
+// device-planned prediction path run on the refined sub-PU list.
+#pragma once
+#include "../../include/mm360.h"
+#include "mm_pipeline.h"
+
+namespace mmdmvr {
+using namespace mmpipe;
+
+constexpr int N_OFF = 25;  // (2 * DMVR_NUM_ITERATION + 1)^2, CommonDef.h:365-370
+
+struct SubPuDev {
+  int x, y, w, h;      // luma sub-PU
+  int mv[2][2];        // merge MVs, 1/16
+  int ref_poc[2];
+  int slot[2];
+  int ged_idx[2];      // GED rotation per list (-1 if not GED)
+  int model;           // both lists (checkDMVRCondition: equal models)
+  int n, rows;         // luma 4x4 sub-blocks, Eigen rows
+  int elem_off;        // first cost element: N_OFF * n per sub-PU
+};
+
+// m_pSearchOffset[i] = (i % 5 - 2, i / 5 - 2)
+MM_HD int off_x(int i) { return i % 5 - 2; }
+MM_HD int off_y(int i) { return i / 5 - 2; }
+
+// job = (sub-PU s, offset o, list l) -> setups[(s * N_OFF + o) * 2 + l]
+MM_HD void dmvr_setup_thread(int t, const SeqConst& sc, const SubPuDev* sp, const M3* ged, BlockSetup* out) {
+  const int l = t & 1, so = t >> 1, s = so / N_OFF, o = so - s * N_OFF;
+  const SubPuDev& u = sp[s];
+  const int sgn = l ? -1 : 1;
+  const int mvh = u.mv[l][0] + sgn * (off_x(o) << 4), mvv = u.mv[l][1] + sgn * (off_y(o) << 4);
+  block_setup(&out[t], sc, u.model, true, u.x, u.y, u.w, u.h, mvh, mvv, u.ged_idx[l] >= 0 ? &ged[u.ged_idx[l]] : nullptr);
+}
+
+// element = (sub-PU, offset, luma 4x4 sub-block): both lists' 14-bit predictions and this
+// sub-block's share of xDMVRCost (SAD over the even rows of the sub-PU, which are the even rows of
+// each 4x4 sub-block).  *cost_index = s * N_OFF + o.
+MM_HD uint32_t dmvr_cost_thread(int g, int si, const SeqConst& sc, const Geometry& geo, const Taps& taps,
+                                const SubPuDev* sp, const BlockSetup* setups, const MpaCache& cache,
+                                const RefDev* refs, int* cost_index) {
+  const SubPuDev& u = sp[si];
+  const int local = g - u.elem_off;
+  const int o = local / u.n, e = local - o * u.n;
+  *cost_index = si * N_OFF + o;
+  const int col = e / u.rows, row = e - col * u.rows;
+  const float gx = (float)(u.x + 4 * col) + sc.off, gy = (float)(u.y + 4 * row) + sc.off;
+  const bool mpa = u.model >= MPA_FRONT_BACK && u.model <= MPA_TOP_BOTTOM;
+  float px = 0.0f, py = 0.0f;
+  bool vip = false;
+  if (mpa) {
+    const int ci = ((u.y >> 2) + row) * cache.cols + (u.x >> 2) + col;
+    const int pl = u.model - MPA_FRONT_BACK;
+    px = cache.px[pl][ci];
+    py = cache.py[pl][ci];
+    vip = cache.vip[pl][ci] != 0;
+  }
+  int16_t p[2][16];
+#pragma unroll
+  for (int l = 0; l < 2; l++) {
+    int32_t fx, fy;
+    reproject_element(sc, setups[(si * N_OFF + o) * 2 + l], gx, gy, packet_lane(e, u.n), mpa, px, py, vip, 0, &fx, &fy);
+    const int xPos = fx >> 4, yPos = fy >> 4, xFrac = fx & 15, yFrac = fy & 15;
+    const RefDev r = refs[u.slot[l]];
+    if (sb_out_of_range(xPos, yPos, geo.W, geo.H, geo.maxCUw, geo.maxCUh, 4, 4)) {
+      for (int i = 0; i < 16; i++) p[l][i] = 0;
+    } else if (window_interior<8, 4, 4>(xPos, yPos, geo.W, geo.H)) {
+#if defined(__HIP_DEVICE_COMPILE__)
+      predict_subblock_interior<8, 4, 4>(r.y, r.stride_y, xPos, yPos, taps.packed->lh[xFrac][(xPos - 3) & 1],
+                                         taps.packed->lv[yFrac], true, geo.bd, p[l]);
+#else
+      predict_subblock_interior<8, 4, 4>(r.y, r.stride_y, xPos, yPos, taps.luma[xFrac], taps.luma[yFrac], true, geo.bd,
+                                         p[l]);
+#endif
+    } else {
+      predict_subblock<8, 4, 4>(r.y, r.stride_y, geo.W, geo.H, xPos, yPos, taps.luma[xFrac], taps.luma[yFrac], true,
+                                geo.bd, p[l]);
+    }
+  }
+  uint32_t sum = 0;
+#pragma unroll
+  for (int rr = 0; rr < 4; rr += 2)
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int d = (int)p[0][rr * 4 + k] - (int)p[1][rr * 4 + k];
+      sum += (uint32_t)(d < 0 ? -d : d);
+    }
+  return sum;
+}
+
+// div_for_maxq7 (InterPrediction.cpp:1958-1994)
+MM_HD int div_for_maxq7(long long N, long long D) {
+  int sign = 0, q = 0;
+  if (N < 0) {
+    sign = 1;
+    N = -N;
+  }
+  D = D << 3;
+  if (N >= D) {
+    N -= D;
+    q++;
+  }
+  q = q << 1;
+  D = D >> 1;
+  if (N >= D) {
+    N -= D;
+    q++;
+  }
+  q = q << 1;
+  if (N >= (D >> 1)) q++;
+  return sign ? -q : q;
+}
+
+// xSubPelErrorSrfc (InterPrediction.cpp:1996-2048); sad: centre, left, top, right, bottom
+MM_HD void sub_pel_error_surface(const unsigned long long* sad, int* delta) {
+  for (int axis = 0; axis < 2; axis++) {
+    const unsigned long long a = sad[1 + axis], b = sad[3 + axis];  // (-1, +1) neighbours
+    const long long num = (long long)((a - b) << 4);
+    const long long den = (long long)(a + b - (sad[0] << 1));
+    if (den != 0) {
+      if (a != sad[0] && b != sad[0])
+        delta[axis] = div_for_maxq7(num, den);
+      else
+        delta[axis] = (a == sad[0]) ? -8 : 8;
+    }
+  }
+}
+
+MM_HD int clip_mv_storage(int v) {  // Mv::clipToStorageBitDepth, MV_BITS = 18
+  const int lo = -(1 << 17), hi = (1 << 17) - 1;
+  return v < lo ? lo : (v > hi ? hi : v);
+}
+
+// thread per sub-PU: the refinement decision and the refined bi descriptor
+MM_HD void dmvr_decide_thread(int s, const SubPuDev* sp, const uint32_t* costs, mm_pu_desc* out, int32_t* mvd) {
+  const SubPuDev& u = sp[s];
+  const uint32_t* c = costs + (size_t)s * N_OFF;
+  unsigned long long sad[N_OFF];
+  for (int i = 0; i < N_OFF; i++) sad[i] = c[i];
+  int tdx = 0, tdy = 0;  // total delta, 1/16
+  unsigned long long minCost = sad[12] - (sad[12] >> 2);
+  if (minCost >= (unsigned long long)(u.w * u.h)) {  // else: notZeroCost = false, no refinement
+    sad[12] = minCost;
+    int best = 12;
+    for (int i = 0; i < N_OFF; i++)
+      if (sad[i] < minCost) {
+        minCost = sad[i];
+        best = i;
+      }
+    tdx = off_x(best) << 4;
+    tdy = off_y(best) << 4;
+    if (tdx != 32 && tdx != -32 && tdy != 32 && tdy != -32) {
+      const unsigned long long sb[5] = {sad[best], sad[best - 1], sad[best - 5], sad[best + 1], sad[best + 5]};
+      int d[2] = {0, 0};
+      sub_pel_error_surface(sb, d);
+      tdx += d[0];
+      tdy += d[1];
+    }
+  }
+  mm_pu_desc& o = out[s];
+  o.x = u.x;
+  o.y = u.y;
+  o.w = u.w;
+  o.h = u.h;
+  o.mv[0][0] = clip_mv_storage(u.mv[0][0] + tdx);
+  o.mv[0][1] = clip_mv_storage(u.mv[0][1] + tdy);
+  o.mv[1][0] = clip_mv_storage(u.mv[1][0] - tdx);
+  o.mv[1][1] = clip_mv_storage(u.mv[1][1] - tdy);
+  o.ref_poc[0] = u.ref_poc[0];
+  o.ref_poc[1] = u.ref_poc[1];
+  o.model[0] = o.model[1] = u.model;
+  mvd[2 * s] = tdx;
+  mvd[2 * s + 1] = tdy;
+}
+
+}  // namespace mmdmvr

@@ -257,6 +257,51 @@ __global__ void __launch_bounds__(256) k_me_sad(SeqConst sc, Geometry geo, MeWin
   if (active && (lane == 63 || inext != idx)) atomicAdd(&sads[idx], v);
 }
 
+// --------------------------------------------------------------------------------------------
+// MM-DMVR (mm_pred_dmvr, mm_dmvr.h)
+// --------------------------------------------------------------------------------------------
+using namespace mmdmvr;
+
+__global__ void __launch_bounds__(256) k_dmvr_setup(SeqConst sc, const SubPuDev* __restrict__ sp, int n_jobs,
+                                                    const PicTables t, BlockSetup* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_jobs) return;
+  dmvr_setup_thread(i, sc, sp, t.ged, out);
+}
+
+__global__ void __launch_bounds__(256) k_dmvr_cost(SeqConst sc, Geometry geo, const SubPuDev* __restrict__ sp,
+                                                   int n_sub, const int* __restrict__ off, const int* __restrict__ chunk,
+                                                   int n_elems, const BlockSetup* __restrict__ setups, MpaCache cache,
+                                                   const PicTables t, uint32_t* __restrict__ costs) {
+  const int g = xcd_block() * blockDim.x + threadIdx.x;
+  const int lane = __lane_id();
+  if (g - lane >= n_elems) return;
+  const int si = wave_find_item(off, chunk, g, n_sub);
+  const bool active = g < n_elems;
+  int idx = -1 - lane;
+  uint32_t v = 0;
+  if (active) {
+    const Taps taps{c_luma_taps, c_chroma_taps, &c_packed_taps};
+    v = dmvr_cost_thread(g, si, sc, geo, taps, sp, setups, cache, t.ref, &idx);
+  }
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t vu = __shfl_up(v, d);
+    const int iu = __shfl_up(idx, d);
+    if (lane >= d && iu == idx) v += vu;
+  }
+  const int inext = __shfl_down(idx, 1);
+  if (active && (lane == 63 || inext != idx)) atomicAdd(&costs[idx], v);
+}
+
+__global__ void __launch_bounds__(256) k_dmvr_decide(const SubPuDev* __restrict__ sp, int n_sub,
+                                                     const uint32_t* __restrict__ costs, mm_pu_desc* __restrict__ out,
+                                                     int32_t* __restrict__ mvd) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_sub) return;
+  dmvr_decide_thread(s, sp, costs, out, mvd);
+}
+
 // InterpolationFilter::filter<N, isVertical, isFirst, isLast> / filterCopy on a raw block
 // (parity API mm_filter; InterpolationFilter.cpp:392-644)
 __global__ void k_filter(int comp, int vertical, const int16_t* src, int src_stride, int16_t* dst, int dst_stride,
@@ -354,6 +399,11 @@ struct mm_ctx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::map<int, RefHost> orgs;  // original luma pictures for mm_sad_window
   DevBuf<MeBlockDev> d_me_blocks;
+  DevBuf<SubPuDev> d_dmvr_sub;
+  DevBuf<int> d_dmvr_off, d_dmvr_chunk, d_dmvr_mvd;
+  DevBuf<uint32_t> d_dmvr_cost;
+  DevBuf<BlockSetup> d_dmvr_setup;
+  DevBuf<mm_pu_desc> d_dmvr_pus;
   DevBuf<int> d_me_off, d_me_chunk;
   bool stage_timing = false;
   hipEvent_t ev_stage[3] = {nullptr, nullptr, nullptr};  // after planning, setup, reprojection
@@ -508,6 +558,13 @@ int mm_destroy(mm_ctx* c) {
   c->d_ged.release();
   for (auto& kv : c->orgs) (void)hipFree(kv.second.y);
   c->d_me_blocks.release();
+  c->d_dmvr_sub.release();
+  c->d_dmvr_off.release();
+  c->d_dmvr_chunk.release();
+  c->d_dmvr_mvd.release();
+  c->d_dmvr_cost.release();
+  c->d_dmvr_setup.release();
+  c->d_dmvr_pus.release();
   c->d_me_off.release();
   c->d_me_chunk.release();
   for (auto& e : c->ev_stage)
@@ -776,6 +833,46 @@ int mm_sad_window(mm_ctx* c, int cur_poc, const mm_me_block* blocks, int n, int 
   HIPCHK(c, hipEventRecord(c->ev1, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return MM_OK;
+}
+
+int mm_pred_dmvr(mm_ctx* c, int cur_poc, const mm_pu_desc* pus, int n, int16_t* dy, ptrdiff_t sdy, int16_t* dcb,
+                 int16_t* dcr, ptrdiff_t sdc, int32_t* mvd_out) {
+  if (!c || n < 0 || (n > 0 && !pus) || !dy || (c->geo.chroma && (!dcb || !dcr))) return MM_ERR_ARG;
+  if (n == 0) return MM_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  std::vector<std::pair<int, RefDev>> refs;
+  for (auto& kv : c->refs)
+    refs.emplace_back(kv.first, RefDev{kv.second.y, kv.second.cb, kv.second.cr, kv.second.stride_y, kv.second.stride_c});
+  PicTables t;
+  std::string err;
+  int rc = build_pic_tables(seq_info(c->prm), c->epipoles, cur_poc, refs, &t, &err);
+  if (rc) return fail(c, rc, err);
+  DmvrPlan plan;
+  rc = plan_dmvr(seq_info(c->prm), t, pus, n, &plan, &err);
+  if (rc) return fail(c, rc, err);
+  const int ns = (int)plan.sub.size(), nj = ns * N_OFF * 2, ne = (int)plan.n_elems;
+  RCCHK(upload(c, c->d_dmvr_sub, plan.sub));
+  RCCHK(upload(c, c->d_dmvr_off, plan.off));
+  RCCHK(upload(c, c->d_dmvr_chunk, plan.chunk));
+  HIPCHK(c, c->d_dmvr_setup.ensure(nj));
+  HIPCHK(c, c->d_dmvr_cost.ensure((size_t)ns * N_OFF));
+  HIPCHK(c, c->d_dmvr_pus.ensure(ns));
+  HIPCHK(c, c->d_dmvr_mvd.ensure(2 * (size_t)ns));
+  HIPCHK(c, hipMemsetAsync(c->d_dmvr_cost.p, 0, (size_t)ns * N_OFF * sizeof(uint32_t), c->stream));
+  hipLaunchKernelGGL(k_dmvr_setup, dim3((nj + 255) / 256), dim3(256), 0, c->stream, c->sc, c->d_dmvr_sub.p, nj, t,
+                     c->d_dmvr_setup.p);
+  hipLaunchKernelGGL(k_dmvr_cost, dim3(round_grid((ne + 255) / 256)), dim3(256), 0, c->stream, c->sc, c->geo,
+                     c->d_dmvr_sub.p, ns, c->d_dmvr_off.p, c->d_dmvr_chunk.p, ne, c->d_dmvr_setup.p, make_cache(c), t,
+                     c->d_dmvr_cost.p);
+  hipLaunchKernelGGL(k_dmvr_decide, dim3((ns + 255) / 256), dim3(256), 0, c->stream, c->d_dmvr_sub.p, ns,
+                     c->d_dmvr_cost.p, c->d_dmvr_pus.p, c->d_dmvr_mvd.p);
+  HIPCHK(c, hipGetLastError());
+  // step 4: the refined sub-PUs are ordinary bi PUs for the device-planned prediction path
+  RCCHK(launch_device_plan(c, cur_poc, c->d_dmvr_pus.p, ns, dy, sdy, dcb, dcr, sdc));
+  if (mvd_out)
+    HIPCHK(c, hipMemcpyAsync(mvd_out, c->d_dmvr_mvd.p, 2 * (size_t)ns * sizeof(int32_t), hipMemcpyDeviceToHost,
+                             c->stream));
+  return read_status(c, nullptr);
 }
 
 int mm_set_stage_timing(mm_ctx* c, int on) {

@@ -19,6 +19,7 @@
 #include "../../include/mm360.h"
 #include "mm_devplan.h"
 #include "mm_me.h"
+#include "mm_dmvr.h"
 #include "mm_pipeline.h"
 
 namespace mmplan {
@@ -298,6 +299,83 @@ inline int plan_me_window(const SeqInfo& s, const mmdev::PicTables& t, const mm_
   }
   if (!cur.blocks.empty()) batches->push_back(std::move(cur));
   for (auto& bt : *batches) build_chunks(bt.blk_off, (int)bt.n_elems, &bt.chunk);
+  return MM_OK;
+}
+
+// ---- MM-DMVR (mm_pred_dmvr) -------------------------------------------------------------------
+// Sub-PUs of min(w,16) x min(h,16) in the reference's raster order (InterPrediction.cpp:2481-2484)
+// for PUs that satisfy the parts of PU::checkDMVRCondition the descriptors carry (bi, equal
+// models, w >= 8, h >= 8, w*h >= 128; UnitTools.cpp:1698-1726) -- the rest of the condition
+// (merge mode, equal POC distances, weights) is the caller's decision.
+struct DmvrPlan {
+  std::vector<mmdmvr::SubPuDev> sub;
+  std::vector<int> off, chunk;  // cost-element offsets per sub-PU, 64-element chunk starts
+  long n_elems = 0;
+};
+
+inline int plan_dmvr(const SeqInfo& s, const mmdev::PicTables& t, const mm_pu_desc* pus, int n, DmvrPlan* p,
+                     std::string* err) {
+  *p = DmvrPlan();
+  for (int i = 0; i < n; i++) {
+    const mm_pu_desc& u = pus[i];
+    if (u.w < 8 || u.h < 8 || u.w * u.h < 128 || u.w > 128 || u.h > 128 || (u.w & 3) || (u.h & 3) ||
+        (u.w > 16 && (u.w & 15)) || (u.h > 16 && (u.h & 15)) || (u.x & 3) ||
+        (u.y & 3) || u.x < 0 || u.y < 0 || u.x > s.W - u.w || u.y > s.H - u.h || u.ref_poc[0] < 0 || u.ref_poc[1] < 0 ||
+        u.model[0] != u.model[1]) {
+      *err = "DMVR PU " + std::to_string(i) + ": needs bi prediction, equal models and w, h >= 8, w*h >= 128";
+      return MM_ERR_ARG;
+    }
+    const int m = u.model[0];
+    if (m <= CLASSIC || m >= NUM_MODELS || !(t.active & (1u << m))) {
+      *err = "DMVR PU " + std::to_string(i) + ": invalid, CLASSIC or inactive motion model";
+      return MM_ERR_MODEL;
+    }
+    mmdmvr::SubPuDev base{};
+    for (int l = 0; l < 2; l++) {
+      int slot = -1;
+      for (int k = 0; k < t.n_slots; k++)
+        if (t.poc[k] == u.ref_poc[l]) slot = k;
+      if (slot < 0) {
+        *err = "DMVR PU " + std::to_string(i) + ": reference POC " + std::to_string(u.ref_poc[l]) + " not uploaded";
+        return MM_ERR_NOREF;
+      }
+      base.slot[l] = slot;
+      base.ref_poc[l] = u.ref_poc[l];
+      base.mv[l][0] = u.mv[l][0];
+      base.mv[l][1] = u.mv[l][1];
+      base.ged_idx[l] = -1;
+      if (m == GEODESIC_CAMPOSE) {
+        if (t.ged_cam[slot] < 0) {
+          *err = "DMVR PU " + std::to_string(i) + ": no epipole for (curPOC, refPOC)";
+          return MM_ERR_NOEPIPOLE;
+        }
+        base.ged_idx[l] = t.ged_cam[slot];
+      } else if (m >= GEODESIC_X && m <= GEODESIC_Z) {
+        base.ged_idx[l] = m - GEODESIC_X;
+      }
+    }
+    base.model = m;
+    const int dx = std::min(u.w, 16), dy = std::min(u.h, 16);
+    for (int y = u.y; y < u.y + u.h; y += dy)
+      for (int x = u.x; x < u.x + u.w; x += dx) {
+        mmdmvr::SubPuDev d = base;
+        d.x = x;
+        d.y = y;
+        d.w = dx;
+        d.h = dy;
+        d.n = (dx / 4) * (dy / 4);
+        d.rows = dy / 4;
+        d.elem_off = (int)p->n_elems;
+        p->off.push_back(d.elem_off);
+        p->n_elems += (long)mmdmvr::N_OFF * d.n;
+        p->sub.push_back(d);
+      }
+  }
+  if (p->n_elems >= (1L << 31)) {
+    *err = "DMVR list too large for one call";
+    return MM_ERR_ARG;
+  }
+  build_chunks(p->off, (int)p->n_elems, &p->chunk);
   return MM_OK;
 }
 

@@ -49,7 +49,7 @@ EXPORTED_SYMBOLS = (
     "mm_create", "mm_destroy", "mm_set_stream", "mm_synchronize", "mm_last_error", "mm_get_version",
     "mm_set_epipole", "mm_upload_ref", "mm_release_ref", "mm_reproject", "mm_pred",
     "mm_pred_device", "mm_pred_status", "mm_pred_prepare", "mm_pred_run", "mm_filter", "mm_last_timing",
-    "mm_set_stage_timing", "mm_last_stage_timing", "mm_upload_org", "mm_sad_window",
+    "mm_set_stage_timing", "mm_last_stage_timing", "mm_upload_org", "mm_sad_window", "mm_pred_dmvr",
 )
 
 
@@ -130,6 +130,7 @@ def load_library() -> ctypes.CDLL:
         "mm_last_timing": (c_int, [vp, POINTER(c_float)]),
         "mm_set_stage_timing": (c_int, [vp, c_int]),
         "mm_upload_org": (c_int, [vp, c_int, vp, ctypes.c_ssize_t, c_int]),
+        "mm_pred_dmvr": (c_int, [vp, c_int, vp, c_int, vp, ctypes.c_ssize_t, vp, vp, ctypes.c_ssize_t, vp]),
         "mm_sad_window": (c_int, [vp, c_int, vp, c_int, c_int, c_int, vp]),
         "mm_last_stage_timing": (c_int, [vp, POINTER(c_float)]),
     }
@@ -257,6 +258,20 @@ class MMContext:
                                      c_void_p(_ptr(dst_cb)) if dst_cb is not None else None,
                                      c_void_p(_ptr(dst_cr)) if dst_cr is not None else None,
                                      dst_cb.stride(0) if dst_cb is not None else 0))
+
+    def predict_dmvr(self, cur_poc: int, pus: np.ndarray, dst_y, dst_cb=None, dst_cr=None) -> np.ndarray:
+        """MM-DMVR PUs (xProcessDMVRProjected): refined bi prediction into the device planes;
+        returns the L0 MV delta (1/16 luma) of every <= 16x16 sub-PU, PU after PU, raster order."""
+        pus = np.ascontiguousarray(pus, dtype=PU_DTYPE)
+        nsub = int(sum(((int(u["w"]) + 15) // 16) * ((int(u["h"]) + 15) // 16) for u in pus))
+        mvd = np.zeros((max(nsub, 1), 2), dtype=np.int32)
+        self._check(self.lib.mm_pred_dmvr(self.h, cur_poc, c_void_p(pus.ctypes.data), len(pus),
+                                          c_void_p(_ptr(dst_y)), dst_y.stride(0),
+                                          c_void_p(_ptr(dst_cb)) if dst_cb is not None else None,
+                                          c_void_p(_ptr(dst_cr)) if dst_cr is not None else None,
+                                          dst_cb.stride(0) if dst_cb is not None else 0,
+                                          c_void_p(mvd.ctypes.data)))
+        return mvd[:nsub]
 
     def predict_device(self, cur_poc: int, d_pus, dst_y, dst_cb=None, dst_cr=None):
         """Whole picture path on the device from a device-resident PU list: `d_pus` is a CUDA

@@ -219,3 +219,32 @@ def me_blocks(width: int, height: int, models: Sequence[int], grid: int = 16, se
     if max_blocks is not None and len(out) > max_blocks:
         out = out[rng.choice(len(out), size=max_blocks, replace=False)]
     return out
+
+
+def dmvr_pu_list(cfg: Config, frame: int = 0, ctu: int = 128) -> np.ndarray:
+    """MM-DMVR PUs: the seeded CTU split's leaves that satisfy the
+    descriptor part of PU::checkDMVRCondition (w, h >= 8, w*h >= 128), bi-predicted from POCs 0
+    and 16 (equal distances around POC 8) with one model for both lists; not pre-split -- DMVR
+    splits into <= 16x16 sub-PUs itself."""
+    rng = np.random.default_rng(0x4D4D3000 + 977 * frame + cfg.width)
+    leaves: List[Tuple[int, int, int, int]] = []
+    for y0 in range(0, cfg.height, ctu):
+        for x0 in range(0, cfg.width, ctu):
+            _split_ctu(rng, x0, y0, min(ctu, cfg.width - x0), min(ctu, cfg.height - y0), leaves)
+    rows = []
+    for (x, y, w, h) in leaves:
+        if w < 8 or h < 8 or w * h < 128:
+            continue
+        m = int(cfg.models[rng.integers(0, len(cfg.models))])
+        mv0 = [int(rng.integers(-24, 25)) * 16 + int(rng.integers(0, 16)),
+               int(rng.integers(-24, 25)) * 16 + int(rng.integers(0, 16))]
+        mv1 = [-mv0[0] + int(rng.integers(-8, 9)), -mv0[1] + int(rng.integers(-8, 9))]
+        rows.append((x, y, w, h, [mv0, mv1], (REF_POCS[0], REF_POCS[1]), (m, m)))
+    from . import PU_DTYPE
+    out = np.zeros(len(rows), dtype=PU_DTYPE)
+    for i, (x, y, w, h, mvs, refs, ms) in enumerate(rows):
+        out[i]["x"], out[i]["y"], out[i]["w"], out[i]["h"] = x, y, w, h
+        out[i]["mv"] = np.array(mvs, dtype=np.int32)
+        out[i]["ref_poc"] = refs
+        out[i]["model"] = ms
+    return out
