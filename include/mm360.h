@@ -18,6 +18,7 @@
  *                       (addAvg / copyClip)               SRC/InterPrediction.cpp:1584-1679
  *   mm_filter        <- InterpolationFilter::filterHor/filterVer  SRC/InterpolationFilter.h:123-128
  *   mm_pred_dmvr     <- InterPrediction::xProcessDMVRProjected  SRC/InterPrediction.cpp:2442-2634
+ *   mm_mvp_convert   <- MVReprojection::motionVectorInDesiredMotionModel  SRC/MVReprojection.cpp:168-217
  *   mm_sad_window    <- InterSearch::xMVReprojectionInterpolation + RdCost::xGetSAD per candidate
  *                       (EncoderLib/InterSearch.cpp:6277-6385, 363-443; SRC/RdCost.cpp:482-517)
  *   mm_upload_org    <- the original picture (pcPatternKey) the encoder SAD compares against
@@ -103,6 +104,19 @@ typedef struct mm_me_block {
                                   (RdCost::setDistParam subShiftMode 2, RdCost.cpp:296-303) */
 } mm_me_block;
 
+/* One MM-MVP conversion: MVReprojection::motionVectorInDesiredMotionModel arguments
+ * (MVReprojection.h:60-64, MVReprojection.cpp:168-217). */
+typedef struct mm_mvp_query {
+  int32_t pos_x, pos_y;                    /* position whose shift the MVs must agree on */
+  int32_t mv_hor, mv_ver;                  /* candidate MV (shift_hor / shift_ver fractional bits) */
+  int32_t model_orig, model_desired;       /* mm_model_id, CLASSIC allowed */
+  int32_t shift_hor, shift_ver;
+  int32_t cur_poc_orig, ref_poc_orig;      /* epipole of the candidate (GEODESIC_CAMPOSE) */
+  int32_t cur_poc_desired, ref_poc_desired;
+  int32_t cand_x, cand_y, cand_w, cand_h;  /* candidate block (MotionInfo::blockPos/blockSize) */
+  int32_t cur_x, cur_y, cur_w, cur_h;      /* current block */
+} mm_mvp_query;
+
 typedef struct mm_ctx mm_ctx;
 
 /* Lifecycle */
@@ -166,6 +180,11 @@ int mm_pred_run(mm_ctx* ctx, int16_t* dst_y, ptrdiff_t dst_stride_y, int16_t* ds
 int mm_pred_dmvr(mm_ctx* ctx, int cur_poc, const mm_pu_desc* pus, int n, int16_t* dst_y,
                  ptrdiff_t dst_stride_y, int16_t* dst_cb, int16_t* dst_cr, ptrdiff_t dst_stride_c,
                  int32_t* mvd_out);
+
+/* MM-MVP, batched: motionVectorInDesiredMotionModel for n queries (the candidate's modelMotion
+ * at `pos` on a 1x1 array, then the desired model's motionVectorForEquivalentPixelShiftAt,
+ * NaN -> zero MV, std::round to fixed point).  mv_out (host): 2 int32 per query.  Synchronous. */
+int mm_mvp_convert(mm_ctx* ctx, const mm_mvp_query* queries, int n, int32_t* mv_out);
 
 /* Single-block interpolation (InterpolationFilter::filterHor/filterVer on the device), for
  * parity tests of the integer pel pipeline.  comp 0 = luma 8-tap (16 phases), else chroma 4-tap

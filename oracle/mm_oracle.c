@@ -1112,3 +1112,193 @@ int orc_sad_window(void* h, int cur_poc, const mm_me_block* blocks, int n, int r
   free(pics);
   return rc;
 }
+
+/* ==========================================================================================
+ * MM-MVP: MVReprojection::motionVectorInDesiredMotionModel (MVReprojection.cpp:168-217)
+ * ========================================================================================== */
+
+/* scalar EquirectangularProjection::fromSphere(Array3TCoord) (Projection.cpp, scalar overload) */
+static void erp_from_sphere1(const Orc* o, float X, float Y, float Z, float* x, float* y) {
+  float R, th, ph;
+  c2s_scalar(X, Y, Z, &R, &th, &ph);
+  ph = ph > 0 ? ph - 2.0f * PI_F : ph;
+  *x = -(ph / (2.0f * PI_F)) * (float)o->W - 0.0f;
+  *y = (th / PI_F) * (float)o->H - 0.0f;
+}
+
+/* scalar MotionPlaneAdaptiveMotionModel::toPerspective (:137-161) with the scalar
+ * PerspectiveProjection::fromSphere (optical centre 0) */
+static void mpa_to_perspective1(const Orc* o, int plane, float x, float y, float* px, float* py, int* vip) {
+  float X, Y, Z;
+  erp_to_sphere1(o, x, y, &X, &Y, &Z);
+  float mx, my, mz;
+  if (plane == 1) { mx = X; my = Y; mz = Z; }
+  else if (plane == 2) { mx = Y; my = -X; mz = Z; }
+  else { mx = -Z; my = Y; mz = X; }
+  float R, th, ph;
+  c2s_scalar(my, -mz, -mx, &R, &th, &ph);
+  float polarR = o->focal * tanf(th);
+  *px = polarR * cosf(ph) + 0.0f;
+  *py = polarR * sinf(ph) + 0.0f;
+  *vip = polarR < 0;
+}
+
+static void rot_apply(const float* M, float x, float y, float z, float* ox, float* oy, float* oz) {
+  *ox = dot3(M[0], x, M[1], y, M[2], z);
+  *oy = dot3(M[3], x, M[4], y, M[5], z);
+  *oz = dot3(M[6], x, M[7], y, M[8], z);
+}
+
+/* <Model>::motionVectorForEquivalentPixelShiftAt, scalar code of each model file */
+static void equivalent_mv(const Orc* o, int model, const float* Rm, float px, float py, float sx, float sy, float cx,
+                          float cy, float* mvx, float* mvy) {
+  float R, th, ph;
+  switch (model) {
+    case 0: *mvx = sx - px; *mvy = sy - py; return;
+    case 1: case 2: case 3: {
+      float ox, oy, qx, qy;
+      int vo, vq;
+      mpa_to_perspective1(o, model, px, py, &ox, &oy, &vo);
+      mpa_to_perspective1(o, model, sx, sy, &qx, &qy, &vq);
+      if (vo != vq) { *mvx = 0; *mvy = 0; return; }
+      float sgn = vq ? -1.0f : 1.0f;
+      *mvx = (qx - ox) * sgn;
+      *mvy = (qy - oy) * sgn;
+      return;
+    }
+    case 4: {
+      float X, Y, Z, thc, phc;
+      erp_to_sphere1(o, cx, cy, &X, &Y, &Z);
+      c2s_scalar(X, Y, Z, &R, &thc, &phc);
+      const float epsC = (float)M_PI_2 - thc, alphaC = phc;
+      float xs[2], ys[2];
+      float pts[2][2] = {{px, py}, {sx, sy}};
+      for (int k = 0; k < 2; k++) {
+        erp_to_sphere1(o, pts[k][0], pts[k][1], &X, &Y, &Z);
+        c2s_scalar(X, Y, Z, &R, &th, &ph);
+        float eps = (float)M_PI_2 - th, dA = ph - alphaC;
+        float cosPsi = sinf(epsC) * sinf(eps) + cosf(epsC) * cosf(eps) * cosf(dA);
+        ys[k] = (sinf(eps) * cosf(epsC) - sinf(epsC) * cosf(eps) * cosf(dA)) / cosPsi;
+        xs[k] = (sinf(dA) * cosf(eps)) / cosPsi;
+      }
+      *mvx = (xs[0] - xs[1]) / o->res;
+      *mvy = (ys[0] - ys[1]) / o->res;
+      return;
+    }
+    case 5: {
+      float Xc, Yc, Zc, X, Y, Z, Xm, Ym, Zm, ox, oy;
+      erp_to_sphere1(o, cx, cy, &Xc, &Yc, &Zc);
+      erp_to_sphere1(o, px, py, &X, &Y, &Z);
+      erp_to_sphere1(o, sx, sy, &Xm, &Ym, &Zm);
+      erp_from_sphere1(o, Xm - X + Xc, Ym - Y + Yc, Zm - Z + Zc, &ox, &oy);
+      *mvx = ox - cx;
+      *mvy = oy - cy;
+      return;
+    }
+    case 6: {
+      float X, Y, Z, thc, phc;
+      erp_to_sphere1(o, cx, cy, &X, &Y, &Z);
+      c2s_scalar(X, Y, Z, &R, &thc, &phc);
+      const float uz[3] = {0, 0, 1}, uy[3] = {0, 1, 0};
+      float uphi[9], uth[9], M[9];
+      angle_axis(-phc, uz, uphi);
+      angle_axis((float)(M_PI_2 - thc), uy, uth);
+      matmul3(uth, uphi, M);
+      float a[3], b[3], t1, p1, t2, p2;
+      erp_to_sphere1(o, px, py, &X, &Y, &Z);
+      rot_apply(M, X, Y, Z, &a[0], &a[1], &a[2]);
+      erp_to_sphere1(o, sx, sy, &X, &Y, &Z);
+      rot_apply(M, X, Y, Z, &b[0], &b[1], &b[2]);
+      c2s_scalar(a[0], a[1], a[2], &R, &t1, &p1);
+      c2s_scalar(b[0], b[1], b[2], &R, &t2, &p2);
+      *mvx = (p1 - p2) / o->res;
+      *mvy = (t2 - t1) / o->res;
+      return;
+    }
+    default: { /* 7..10 geodesic */
+      float X, Y, Z, a[3], t1, p1, t2, p2;
+      erp_to_sphere1(o, px, py, &X, &Y, &Z);
+      rot_apply(Rm, X, Y, Z, &a[0], &a[1], &a[2]);
+      c2s_scalar(a[0], a[1], a[2], &R, &t1, &p1);
+      erp_to_sphere1(o, sx, sy, &X, &Y, &Z);
+      rot_apply(Rm, X, Y, Z, &a[0], &a[1], &a[2]);
+      c2s_scalar(a[0], a[1], a[2], &R, &t2, &p2);
+      if (o->ged_flavor == 0) {
+        *mvx = (t2 - t1) / o->res;
+      } else {
+        float tc, pc;
+        erp_to_sphere1(o, cx, cy, &X, &Y, &Z);
+        rot_apply(Rm, X, Y, Z, &a[0], &a[1], &a[2]);
+        c2s_scalar(a[0], a[1], a[2], &R, &tc, &pc);
+        float dTheta = t2 - t1;
+        float k = sinf(dTheta + t1) / sinf(dTheta);
+        float dThetaC = atanf(sinf(tc) / (k - cosf(tc)));
+        *mvx = dThetaC / o->res;
+      }
+      *mvy = (p2 - p1) / o->res;
+      return;
+    }
+  }
+}
+
+int orc_mvp(void* h, const mm_mvp_query* qs, int n, int32_t* out) {
+  Orc* o = (Orc*)h;
+  for (int i = 0; i < n; i++) {
+    const mm_mvp_query* q = &qs[i];
+    int32_t* r = out + 2 * i;
+    if (q->mv_hor == 0 && q->mv_ver == 0) { r[0] = r[1] = 0; continue; }
+    float eo[3] = {0, 0, 0}, ed[3] = {0, 0, 0};
+    int have_o = 0, have_d = 0;
+    if (q->model_orig == 10) { if (find_epipole(o, q->cur_poc_orig, q->ref_poc_orig, eo)) return MM_ERR_NOEPIPOLE; have_o = 1; }
+    if (q->model_desired == 10) { if (find_epipole(o, q->cur_poc_desired, q->ref_poc_desired, ed)) return MM_ERR_NOEPIPOLE; have_d = 1; }
+    if (q->model_desired == q->model_orig &&
+        (q->model_desired != 10 || (have_o && have_d && eo[0] == ed[0] && eo[1] == ed[1] && eo[2] == ed[2]))) {
+      r[0] = q->mv_hor;
+      r[1] = q->mv_ver;
+      continue;
+    }
+    const float mvX = (float)(q->mv_hor >> q->shift_hor) + (float)(q->mv_hor & ((1 << q->shift_hor) - 1)) / (float)(1 << q->shift_hor);
+    const float mvY = (float)(q->mv_ver >> q->shift_ver) + (float)(q->mv_ver & ((1 << q->shift_ver) - 1)) / (float)(1 << q->shift_ver);
+    const float ccx = (float)q->cand_x + ((float)q->cand_w - 1) / 2.0f, ccy = (float)q->cand_y + ((float)q->cand_h - 1) / 2.0f;
+    float gx = (float)q->pos_x, gy = (float)q->pos_y, sx, sy;
+    float Rm[9];
+    switch (q->model_orig) { /* the candidate's modelMotion on a 1x1 array */
+      case 0: sx = gx + mvX; sy = gy + mvY; break;
+      case 1: case 2: case 3: {
+        float ppx, ppy;
+        unsigned char vip;
+        mpa_to_perspective_arr(o, q->model_orig, &gx, &gy, &ppx, &ppy, &vip, 1);
+        float sgn = vip ? -1.0f : 1.0f;
+        ppx = ppx + mvX * sgn;
+        ppy = ppy + mvY * sgn;
+        mpa_to_projection_arr(o, q->model_orig, &ppx, &ppy, &vip, &sx, &sy, 1);
+      } break;
+      case 4: tan_model(o, &gx, &gy, 1, mvX, mvY, ccx, ccy, &sx, &sy); break;
+      case 5: t3d_model(o, &gx, &gy, 1, mvX, mvY, ccx, ccy, &sx, &sy); break;
+      case 6: rot_model(o, &gx, &gy, 1, mvX, mvY, ccx, ccy, &sx, &sy); break;
+      default: {
+        float e[3] = {1, 0, 0};
+        if (q->model_orig == 8) { e[0] = 0; e[1] = 1; }
+        else if (q->model_orig == 9) { e[0] = 0; e[2] = 1; }
+        else if (q->model_orig == 10) { e[0] = eo[0]; e[1] = eo[1]; e[2] = eo[2]; }
+        ged_set_epipole(e, Rm);
+        ged_model(o, Rm, &gx, &gy, 1, mvX, mvY, ccx, ccy, &sx, &sy);
+      }
+    }
+    if (q->model_desired >= 7) {
+      float e[3] = {1, 0, 0};
+      if (q->model_desired == 8) { e[0] = 0; e[1] = 1; }
+      else if (q->model_desired == 9) { e[0] = 0; e[2] = 1; }
+      else if (q->model_desired == 10) { e[0] = ed[0]; e[1] = ed[1]; e[2] = ed[2]; }
+      ged_set_epipole(e, Rm);
+    }
+    const float cx = (float)q->cur_x + ((float)q->cur_w - 1) / 2.0f, cy = (float)q->cur_y + ((float)q->cur_h - 1) / 2.0f;
+    float ex, ey;
+    equivalent_mv(o, q->model_desired, Rm, (float)q->pos_x, (float)q->pos_y, sx, sy, cx, cy, &ex, &ey);
+    if (isnan(ex) || isnan(ey)) { r[0] = r[1] = 0; continue; }
+    float rx = roundf(ex * (float)(1 << q->shift_hor)), ry = roundf(ey * (float)(1 << q->shift_ver));
+    r[0] = _mm_cvtt_ss2si(_mm_set_ss(rx));
+    r[1] = _mm_cvtt_ss2si(_mm_set_ss(ry));
+  }
+  return 0;
+}

@@ -37,6 +37,7 @@ def load():
     lib.orc_pred_dmvr.argtypes = [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                   ctypes.c_ssize_t, ctypes.c_ssize_t, c_void_p, ctypes.c_ssize_t, c_void_p, c_void_p,
                                   ctypes.c_ssize_t, c_void_p]
+    lib.orc_mvp.argtypes = [c_void_p, c_void_p, c_int, c_void_p]
     lib.orc_sad_window.argtypes = [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                    ctypes.c_ssize_t, c_void_p, ctypes.c_ssize_t, c_void_p]
     return lib
@@ -115,6 +116,15 @@ class Oracle:
         if rc:
             raise RuntimeError(f"oracle predict_dmvr failed: {rc}")
         return (dy, dcb, dcr), mvd[:nsub]
+
+    def mvp(self, queries):
+        """MM-MVP conversions: int32 [n, 2]."""
+        q = np.ascontiguousarray(queries)
+        out = np.zeros((max(len(q), 1), 2), dtype=np.int32)
+        rc = self.lib.orc_mvp(self.h, c_void_p(q.ctypes.data), len(q), c_void_p(out.ctypes.data))
+        if rc:
+            raise RuntimeError(f"oracle mvp failed: {rc}")
+        return out[:len(q)]
 
     def sad_window(self, cur_poc, blocks, range_, step, refs, org):
         """Encoder candidate windows: uint32 SADs [n_blocks, (2*range+1)**2].  refs: poc -> luma."""

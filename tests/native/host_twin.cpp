@@ -325,3 +325,19 @@ extern "C" int twin_pred_dmvr(const mm_seq_params* p, int n_epi, const int32_t* 
   if (mvd_out) std::copy(mvd.begin(), mvd.end(), mvd_out);
   return twin_pred_list(t, tab, refined.data(), ns, dy, sdy, dcb, dcr, sdc);
 }
+
+// MM-MVP (mm_mvp_convert) through the product's planner and mm_mvp.h bodies.
+extern "C" int twin_mvp(const mm_seq_params* p, int n_epi, const int32_t* epi, const mm_mvp_query* q, int n,
+                        int32_t* out) {
+  Twin t;
+  make_twin(p, &t);
+  EpipoleMap em = epi_of(n_epi, epi);
+  std::vector<mmmvp::MvpQueryDev> qs;
+  std::vector<M3> ged;
+  std::string err;
+  int rc = plan_mvp(seq_info(*p), em, q, n, &qs, &ged, &err);
+  if (rc) return rc;
+#pragma omp parallel for schedule(static)
+  for (int i = 0; i < n; i++) mmmvp::mvp_thread(i, t.sc, qs.data(), ged.data(), out);
+  return 0;
+}

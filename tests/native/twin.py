@@ -20,6 +20,7 @@ def load():
     lib.twin_pred_dmvr.argtypes = [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int,
                                    c_void_p]
+    lib.twin_mvp.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]
     lib.twin_sad_window.argtypes = [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
                                     c_void_p, c_int, c_void_p, c_int, c_void_p]
     return lib
@@ -105,3 +106,15 @@ def predict_dmvr(params, cur_poc, pus, refs, W, H, epipoles=()):
     if rc:
         raise RuntimeError(f"twin predict_dmvr failed: {rc}")
     return (dy, dcb, dcr), mvd[:nsub]
+
+
+def mvp(params, queries, epipoles=()):
+    lib = load()
+    q = np.ascontiguousarray(queries)
+    out = np.zeros((max(len(q), 1), 2), dtype=np.int32)
+    n_epi, ea = _epi(epipoles)
+    rc = lib.twin_mvp(ctypes.addressof(params), n_epi, c_void_p(ea.ctypes.data), c_void_p(q.ctypes.data), len(q),
+                      c_void_p(out.ctypes.data))
+    if rc:
+        raise RuntimeError(f"twin mvp failed: {rc}")
+    return out[:len(q)]

@@ -367,3 +367,14 @@ def test_pred_dmvr_vs_oracle(w, h):
     for name, t, x in zip(("y", "cb", "cr"), dst, want):
         got = t.cpu().numpy()
         assert np.array_equal(got, x), describe_mismatch(name, got, x)
+
+
+def test_mvp_convert_vs_oracle():
+    """Batched MM-MVP on the GPU == the oracle for every model pair (incl. CLASSIC), both epipoles."""
+    from test_mvp import ALL as MVP_ALL, EPI2
+    params = mm360.seq_params(2048, 1024, MVP_ALL)
+    q = W.mvp_queries(2048, 1024, MVP_ALL, 20000, seed=21)
+    want = Oracle(params, EPI2).mvp(q)
+    with _ctx(params, EPI2) as ctx:
+        got = ctx.mvp_convert(q)
+    assert np.array_equal(got, want), np.argwhere((got != want).any(axis=1))[:5]

@@ -302,6 +302,16 @@ __global__ void __launch_bounds__(256) k_dmvr_decide(const SubPuDev* __restrict_
   dmvr_decide_thread(s, sp, costs, out, mvd);
 }
 
+// --------------------------------------------------------------------------------------------
+// MM-MVP (mm_mvp_convert, mm_mvp.h)
+// --------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_mvp(SeqConst sc, const mmmvp::MvpQueryDev* __restrict__ q, int n,
+                                             const M3* __restrict__ ged, int32_t* __restrict__ out) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  mmmvp::mvp_thread(t, sc, q, ged, out);
+}
+
 // InterpolationFilter::filter<N, isVertical, isFirst, isLast> / filterCopy on a raw block
 // (parity API mm_filter; InterpolationFilter.cpp:392-644)
 __global__ void k_filter(int comp, int vertical, const int16_t* src, int src_stride, int16_t* dst, int dst_stride,
@@ -403,6 +413,8 @@ struct mm_ctx {
   DevBuf<int> d_dmvr_off, d_dmvr_chunk, d_dmvr_mvd;
   DevBuf<uint32_t> d_dmvr_cost;
   DevBuf<BlockSetup> d_dmvr_setup;
+  DevBuf<mmmvp::MvpQueryDev> d_mvp_q;
+  DevBuf<int32_t> d_mvp_out;
   DevBuf<mm_pu_desc> d_dmvr_pus;
   DevBuf<int> d_me_off, d_me_chunk;
   bool stage_timing = false;
@@ -564,6 +576,8 @@ int mm_destroy(mm_ctx* c) {
   c->d_dmvr_mvd.release();
   c->d_dmvr_cost.release();
   c->d_dmvr_setup.release();
+  c->d_mvp_q.release();
+  c->d_mvp_out.release();
   c->d_dmvr_pus.release();
   c->d_me_off.release();
   c->d_me_chunk.release();
@@ -873,6 +887,26 @@ int mm_pred_dmvr(mm_ctx* c, int cur_poc, const mm_pu_desc* pus, int n, int16_t* 
     HIPCHK(c, hipMemcpyAsync(mvd_out, c->d_dmvr_mvd.p, 2 * (size_t)ns * sizeof(int32_t), hipMemcpyDeviceToHost,
                              c->stream));
   return read_status(c, nullptr);
+}
+
+int mm_mvp_convert(mm_ctx* c, const mm_mvp_query* q, int n, int32_t* mv_out) {
+  if (!c || n < 0 || (n > 0 && (!q || !mv_out))) return MM_ERR_ARG;
+  if (n == 0) return MM_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  std::vector<mmmvp::MvpQueryDev> qs;
+  std::vector<M3> ged;
+  std::string err;
+  int rc = plan_mvp(seq_info(c->prm), c->epipoles, q, n, &qs, &ged, &err);
+  if (rc) return fail(c, rc, err);
+  RCCHK(upload(c, c->d_mvp_q, qs));
+  RCCHK(upload(c, c->d_ged, ged));
+  HIPCHK(c, c->d_mvp_out.ensure(2 * (size_t)n));
+  hipLaunchKernelGGL(k_mvp, dim3((n + 255) / 256), dim3(256), 0, c->stream, c->sc, c->d_mvp_q.p, n, c->d_ged.p,
+                     c->d_mvp_out.p);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(mv_out, c->d_mvp_out.p, 2 * (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return MM_OK;
 }
 
 int mm_set_stage_timing(mm_ctx* c, int on) {

@@ -98,9 +98,9 @@ MM_HD void erp_from_sphere(V3 p, const SeqConst& s, Math m, bool arr, float* ox,
 // ------------------------------------------------------------------------------------------
 // PerspectiveProjection, optical centre (0,0) (Projection.cpp:119-211 in SURVEY numbering)
 // ------------------------------------------------------------------------------------------
-MM_HD void persp_from_sphere(V3 s3, float f, Math m, float* ox, float* oy, bool* vip) {
+MM_HD void persp_from_sphere(V3 s3, float f, Math m, float* ox, float* oy, bool* vip, bool arr = true) {
   V3 rot = {s3.y, -s3.z, -s3.x};
-  V3 sp = cart_to_sph(rot, m, true);
+  V3 sp = cart_to_sph(rot, m, arr);
   float polarR = f * g_tanf(sp.y);
   *ox = polarR * m.cos(sp.z) + 0.0f;
   *oy = polarR * m.sin(sp.z) + 0.0f;
@@ -122,7 +122,7 @@ MM_HD V3 persp_to_sphere(float x, float y, bool vip, float f, Math m) {
 
 // MotionPlaneAdaptiveMotionModel::toPerspective (array, MotionPlaneAdaptiveMotionModel.cpp:111-135)
 MM_HD void mpa_to_perspective(int plane, float gx, float gy, const SeqConst& s, Math m, float* px,
-                              float* py, bool* vip) {
+                              float* py, bool* vip, bool arr = true) {
   V3 sph = erp_to_sphere(gx, gy, s, m);
   V3 q;
   if (plane == MPA_FRONT_BACK)
@@ -131,7 +131,7 @@ MM_HD void mpa_to_perspective(int plane, float gx, float gy, const SeqConst& s, 
     q = {sph.y, -sph.x, sph.z};
   else
     q = {-sph.z, sph.y, sph.x};
-  persp_from_sphere(q, s.focal, m, px, py, vip);
+  persp_from_sphere(q, s.focal, m, px, py, vip, arr);
 }
 
 // MotionPlaneAdaptiveMotionModel::toProjection (array, MotionPlaneAdaptiveMotionModel.cpp:163-187)
@@ -244,12 +244,22 @@ struct BlockSetup {
 };
 
 MM_HD float mv_to_float(int32_t v) { return (float)(v >> 4) + (float)(v & 15) / 16.0f; }
+// MV as floating point with `shift` fractional bits (MVReprojection.cpp:123-124, 185-186)
+MM_HD float mv_to_float_shift(int32_t v, int shift) {
+  return (float)(v >> shift) + (float)(v & ((1 << shift) - 1)) / (float)(1 << shift);
+}
 
+MM_HD void block_setup_f(BlockSetup* b, const SeqConst& s, int model, bool luma, int pos_x, int pos_y, int size_w,
+                         int size_h, float mvx, float mvy, const M3* ged_rot);
 MM_HD void block_setup(BlockSetup* b, const SeqConst& s, int model, bool luma, int pos_x, int pos_y,
                        int size_w, int size_h, int32_t mv_hor, int32_t mv_ver, const M3* ged_rot) {
+  block_setup_f(b, s, model, luma, pos_x, pos_y, size_w, size_h, mv_to_float(mv_hor), mv_to_float(mv_ver), ged_rot);
+}
+MM_HD void block_setup_f(BlockSetup* b, const SeqConst& s, int model, bool luma, int pos_x, int pos_y, int size_w,
+                         int size_h, float mvx, float mvy, const M3* ged_rot) {
   b->model = model;
-  b->mvx = mv_to_float(mv_hor);
-  b->mvy = mv_to_float(mv_ver);
+  b->mvx = mvx;
+  b->mvy = mvy;
   b->cx = (float)pos_x + ((float)size_w - 1.0f) / 2.0f;
   b->cy = (float)pos_y + ((float)size_h - 1.0f) / 2.0f;
   b->identity = 0;
@@ -319,11 +329,18 @@ MM_HD void block_setup(BlockSetup* b, const SeqConst& s, int model, bool luma, i
 //   pers*    : MPA luma only -- the frame-cache perspective coordinates of this element
 //   chroma_shift : 0 for luma, 1 for 4:2:0 chroma; fixed precision = 4 + chroma_shift bits
 // ------------------------------------------------------------------------------------------
-MM_HD void reproject_element(const SeqConst& s, const BlockSetup& b, float gx, float gy, bool packet,
-                             bool mpa_cached, float pers_x, float pers_y, bool pers_vip,
-                             int chroma_shift, int32_t* fx, int32_t* fy) {
+// <Model>::modelMotion[Cached] of one element: the moved position as computed (before the NaN
+// fallback, offset removal and rounding).  CLASSIC (TranslationalMotionModel::modelMotion,
+// TranslationalMotionModel.cpp:8-13) adds the MV.
+MM_HD void model_motion_element(const SeqConst& s, const BlockSetup& b, float gx, float gy, bool packet,
+                                bool mpa_cached, float pers_x, float pers_y, bool pers_vip, float* omx, float* omy) {
   const Math m{packet};
   float mx = gx, my = gy;
+  if (b.model == CLASSIC) {
+    *omx = gx + b.mvx;
+    *omy = gy + b.mvy;
+    return;
+  }
   if (!b.identity) {
     switch (b.model) {
       case MPA_FRONT_BACK:
@@ -394,6 +411,15 @@ MM_HD void reproject_element(const SeqConst& s, const BlockSetup& b, float gx, f
         break;
     }
   }
+  *omx = mx;
+  *omy = my;
+}
+
+MM_HD void reproject_element(const SeqConst& s, const BlockSetup& b, float gx, float gy, bool packet,
+                             bool mpa_cached, float pers_x, float pers_y, bool pers_vip,
+                             int chroma_shift, int32_t* fx, int32_t* fy) {
+  float mx, my;
+  model_motion_element(s, b, gx, gy, packet, mpa_cached, pers_x, pers_y, pers_vip, &mx, &my);
   // NaN -> unmoved (MVReprojection.cpp:151-154), remove offset, rescale, round to fixed point
   if (isnanf_(mx) || isnanf_(my)) {
     mx = gx;

@@ -20,6 +20,7 @@
 #include "mm_devplan.h"
 #include "mm_me.h"
 #include "mm_dmvr.h"
+#include "mm_mvp.h"
 #include "mm_pipeline.h"
 
 namespace mmplan {
@@ -376,6 +377,66 @@ inline int plan_dmvr(const SeqInfo& s, const mmdev::PicTables& t, const mm_pu_de
     return MM_ERR_ARG;
   }
   build_chunks(p->off, (int)p->n_elems, &p->chunk);
+  return MM_OK;
+}
+
+// ---- MM-MVP (mm_mvp_convert) -------------------------------------------------------------------
+// Validates the queries (models active; CLASSIC is always active) and resolves the GED rotations
+// of both sides: fixed epipoles for GEODESIC_X/Y/Z, EpipoleList::findEpipole for CAMPOSE.
+inline int plan_mvp(const SeqInfo& s, const EpipoleMap& epi, const mm_mvp_query* q, int n,
+                    std::vector<mmmvp::MvpQueryDev>* out, std::vector<M3>* ged, std::string* err) {
+  out->clear();
+  ged->clear();
+  const V3 fixed[3] = {{1.0f, 0.0f, 0.0f}, {0.0f, 1.0f, 0.0f}, {0.0f, 0.0f, 1.0f}};
+  for (int i = 0; i < 3; i++) ged->push_back(ged_rotation(fixed[i]));
+  std::map<std::array<int32_t, 3>, int> cam;
+  auto resolve = [&](int model, int cur, int ref, int* idx, std::array<int32_t, 3>* e) -> int {
+    *idx = -1;
+    if (model >= GEODESIC_X && model <= GEODESIC_Z) *idx = model - GEODESIC_X;
+    if (model != GEODESIC_CAMPOSE) return MM_OK;
+    if (!find_epipole(epi, cur, ref, e)) return MM_ERR_NOEPIPOLE;
+    auto it = cam.find(*e);
+    if (it == cam.end()) {
+      V3 v = {fixed_to_float((*e)[0], 24), fixed_to_float((*e)[1], 24), fixed_to_float((*e)[2], 24)};
+      ged->push_back(ged_rotation(v));
+      it = cam.emplace(*e, (int)ged->size() - 1).first;
+    }
+    *idx = it->second;
+    return MM_OK;
+  };
+  for (int i = 0; i < n; i++) {
+    const mm_mvp_query& x = q[i];
+    for (int m : {x.model_orig, x.model_desired})
+      if (m < CLASSIC || m >= NUM_MODELS || !((s.prm.active_models | 1u) & (1u << m))) {
+        *err = "MVP query " + std::to_string(i) + ": invalid or inactive motion model";
+        return MM_ERR_MODEL;
+      }
+    if (x.shift_hor < 0 || x.shift_hor > 8 || x.shift_ver < 0 || x.shift_ver > 8 || x.cand_w <= 0 || x.cand_h <= 0 ||
+        x.cur_w <= 0 || x.cur_h <= 0) {
+      *err = "MVP query " + std::to_string(i) + ": invalid precision or block size";
+      return MM_ERR_ARG;
+    }
+    mmmvp::MvpQueryDev d;
+    d.q = x;
+    std::array<int32_t, 3> eo{}, ed{};
+    int rc = resolve(x.model_orig, x.cur_poc_orig, x.ref_poc_orig, &d.ged_orig, &eo);
+    if (!rc) rc = resolve(x.model_desired, x.cur_poc_desired, x.ref_poc_desired, &d.ged_desired, &ed);
+    // the early return compares the two CAMPOSE epipoles (MVReprojection.cpp:177-181); only
+    // evaluated there when both models are GEODESIC_CAMPOSE
+    d.same_epipole = 0;
+    if (x.model_orig == GEODESIC_CAMPOSE && x.model_desired == GEODESIC_CAMPOSE && !rc) d.same_epipole = eo == ed;
+    if (rc) {
+      // a missing epipole only matters when the conversion reaches the model (zero MVs and equal
+      // non-GED models return before)
+      const bool needed = !(x.mv_hor == 0 && x.mv_ver == 0);
+      if (needed) {
+        *err = "MVP query " + std::to_string(i) + ": no epipole for (curPOC, refPOC)";
+        return MM_ERR_NOEPIPOLE;
+      }
+      d.ged_orig = d.ged_desired = -1;
+    }
+    out->push_back(d);
+  }
   return MM_OK;
 }
 

@@ -49,7 +49,7 @@ EXPORTED_SYMBOLS = (
     "mm_create", "mm_destroy", "mm_set_stream", "mm_synchronize", "mm_last_error", "mm_get_version",
     "mm_set_epipole", "mm_upload_ref", "mm_release_ref", "mm_reproject", "mm_pred",
     "mm_pred_device", "mm_pred_status", "mm_pred_prepare", "mm_pred_run", "mm_filter", "mm_last_timing",
-    "mm_set_stage_timing", "mm_last_stage_timing", "mm_upload_org", "mm_sad_window", "mm_pred_dmvr",
+    "mm_set_stage_timing", "mm_last_stage_timing", "mm_upload_org", "mm_sad_window", "mm_pred_dmvr", "mm_mvp_convert",
 )
 
 
@@ -77,7 +77,12 @@ PU_DTYPE = np.dtype([("x", "<i4"), ("y", "<i4"), ("w", "<i4"), ("h", "<i4"), ("m
                      ("ref_poc", "<i4", (2,)), ("model", "<i4", (2,))])
 ME_BLOCK_DTYPE = np.dtype([("x", "<i4"), ("y", "<i4"), ("w", "<i4"), ("h", "<i4"), ("mv_hor", "<i4"),
                            ("mv_ver", "<i4"), ("model", "<i4"), ("ref_poc", "<i4"), ("sub_shift", "<i4")])
+MVP_QUERY_DTYPE = np.dtype([(n, "<i4") for n in (
+    "pos_x", "pos_y", "mv_hor", "mv_ver", "model_orig", "model_desired", "shift_hor", "shift_ver", "cur_poc_orig",
+    "ref_poc_orig", "cur_poc_desired", "ref_poc_desired", "cand_x", "cand_y", "cand_w", "cand_h", "cur_x", "cur_y",
+    "cur_w", "cur_h")])
 assert BLOCK_DTYPE.itemsize == 40 and PU_DTYPE.itemsize == 48 and ME_BLOCK_DTYPE.itemsize == 36
+assert MVP_QUERY_DTYPE.itemsize == 80
 
 
 def active_mask(models: Sequence[int]) -> int:
@@ -130,6 +135,7 @@ def load_library() -> ctypes.CDLL:
         "mm_last_timing": (c_int, [vp, POINTER(c_float)]),
         "mm_set_stage_timing": (c_int, [vp, c_int]),
         "mm_upload_org": (c_int, [vp, c_int, vp, ctypes.c_ssize_t, c_int]),
+        "mm_mvp_convert": (c_int, [vp, vp, c_int, vp]),
         "mm_pred_dmvr": (c_int, [vp, c_int, vp, c_int, vp, ctypes.c_ssize_t, vp, vp, ctypes.c_ssize_t, vp]),
         "mm_sad_window": (c_int, [vp, c_int, vp, c_int, c_int, c_int, vp]),
         "mm_last_stage_timing": (c_int, [vp, POINTER(c_float)]),
@@ -258,6 +264,13 @@ class MMContext:
                                      c_void_p(_ptr(dst_cb)) if dst_cb is not None else None,
                                      c_void_p(_ptr(dst_cr)) if dst_cr is not None else None,
                                      dst_cb.stride(0) if dst_cb is not None else 0))
+
+    def mvp_convert(self, queries: np.ndarray) -> np.ndarray:
+        """Batched MVReprojection::motionVectorInDesiredMotionModel: int32 [n, 2] MVs."""
+        q = np.ascontiguousarray(queries, dtype=MVP_QUERY_DTYPE)
+        out = np.zeros((max(len(q), 1), 2), dtype=np.int32)
+        self._check(self.lib.mm_mvp_convert(self.h, c_void_p(q.ctypes.data), len(q), c_void_p(out.ctypes.data)))
+        return out[:len(q)]
 
     def predict_dmvr(self, cur_poc: int, pus: np.ndarray, dst_y, dst_cb=None, dst_cr=None) -> np.ndarray:
         """MM-DMVR PUs (xProcessDMVRProjected): refined bi prediction into the device planes;

@@ -248,3 +248,31 @@ def dmvr_pu_list(cfg: Config, frame: int = 0, ctu: int = 128) -> np.ndarray:
         out[i]["ref_poc"] = refs
         out[i]["model"] = ms
     return out
+
+
+def mvp_queries(width: int, height: int, models: Sequence[int], n: int, seed: int = 7) -> np.ndarray:
+    """Seeded MM-MVP conversions: every ordered pair of {CLASSIC} + models,
+    neighbour positions around random current blocks (incl. the poles and the ERP seam), MVs in
+    1/16 pel, some zero MVs and identical model pairs (the early returns)."""
+    from . import MVP_QUERY_DTYPE
+    rng = np.random.default_rng(0x4D4D4000 + seed)
+    allm = [0] + [int(m) for m in models]
+    q = np.zeros(n, dtype=MVP_QUERY_DTYPE)
+    for i in range(n):
+        w, h = [int(v) for v in rng.choice([8, 16, 32, 64], size=2)]
+        x = int(rng.integers(0, width // 4)) * 4
+        y = int(rng.integers(0, height // 4)) * 4
+        if i % 11 == 0:
+            y = 0 if i % 2 else height - 4  # poles
+        if i % 13 == 0:
+            x = width - 4  # seam
+        cw, ch = [int(v) for v in rng.choice([8, 16, 32], size=2)]
+        cx, cy = x - cw, y - ch  # candidate: above-left neighbour
+        mv = [int(v) for v in rng.integers(-64 * 16, 64 * 16, size=2)]
+        if i % 17 == 0:
+            mv = [0, 0]
+        mo, md = int(rng.choice(allm)), int(rng.choice(allm))
+        shift = 4 if i % 5 else 2
+        q[i] = (x, y, mv[0], mv[1], mo, md, shift, shift, CUR_POC, REF_POCS[i % 2], CUR_POC, REF_POCS[(i // 2) % 2],
+                cx, cy, cw, ch, x, y, w, h)
+    return q
