@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="length of the CPU baseline sample")
     ap.add_argument("--kernel-steps", type=int, default=10, help="extra steps timed per launch with HIP events")
     ap.add_argument("--lib", default=None, help="alternative build of libmm360.so (A/B experiments)")
+    ap.add_argument("--coherent-mv", action="store_true",
+                    help="experiment: one MV for every PU and list (spatially coherent motion)")
     ap.add_argument("--uniform-model", type=int, default=None,
                     help="per-model workload: all PUs 16x16 with this MotionModelID (SURVEY 8(d))")
     args = ap.parse_args()
@@ -68,6 +70,9 @@ def main():
         pus = W.pu_list(cfg, frame=rank, uniform=True, uniform_model=args.uniform_model)
     else:
         pus = W.pu_list(cfg, frame=rank)
+    if args.coherent_mv:
+        pus["mv"][:, 0, :] = (85, -43)
+        pus["mv"][:, 1, :] = (-37, 91)
     area = W.luma_area(pus)
     alg_bytes = W.algorithmic_bytes(pus)
 

@@ -131,17 +131,24 @@ static int twin_pred_list(const Twin& t, const mmdev::PicTables& tab, const mm_p
   std::vector<BlockSetup> setups(m.n_jobs);
 #pragma omp parallel for schedule(static)
   for (int i = 0; i < m.n_jobs; i++) setup_thread(i, t.sc, jobs.data(), tab.ged, setups.data());
-  std::vector<int32_t> r(2 * (size_t)std::max(m.n_elems, 1));
+  std::vector<mm_int4> lum[2];
+  std::vector<mm_int2> chr[2];
+  McIn mc;
+  for (int l = 0; l < 2; l++) {
+    lum[l].assign(std::max(m.n_sb, 1), mm_int4{});
+    chr[l].assign(std::max(m.n_sb, 1), mm_int2{});
+    mc.lum[l] = lum[l].data();
+    mc.chr[l] = chr[l].data();
+  }
   MpaCache c = cache_of(t);
 #pragma omp parallel for schedule(static, 256)
   for (int g = 0; g < m.n_elems; g++)
-    reproj_thread(g, find_item(job_off.data(), job_chunk.data(), g, m.n_jobs), t.sc, jobs.data(), job_off.data(),
-                  setups.data(), c, r.data());
+    reproj_thread_mc(g, find_item(job_off.data(), job_chunk.data(), g, m.n_jobs), t.sc, jobs.data(), job_off.data(),
+                     setups.data(), c, mc);
   const Taps taps{LUMA_T, CHROMA_T, nullptr};
 #pragma omp parallel for schedule(static, 256)
   for (int g = 0; g < m.n_sb; g++)
-    mc_thread(g, find_item(pu_off.data(), pu_chunk.data(), g, m.n_pus), t.geo, taps, dpus.data(), jobs.data(), r.data(),
-              tab.ref, dy, sdy, dcb, dcr, sdc);
+    mc_thread_rec(g, m.sb_base[1], m.sb_base[2], t.geo, taps, mc, tab.ref, dy, sdy, dcb, dcr, sdc);
   return 0;
 }
 

@@ -222,6 +222,11 @@ MM_HD void emit_pu(const mm_pu_desc& u, const PuPlan& p, int pu_idx, int sb_off,
     j.n = jp.n;
     j.rows = jp.rows;
     j.offset = job_elem_off[i];
+    j.sb_base = sb_off;
+    j.pu_cols = u.w / 4;
+    j.list = jp.list;
+    j.slot = p.slot[jp.list];
+    j.alias = jp.comp == 0 ? p.alias[jp.list] : 0;
     jobs[job_idx[i]] = j;
     job_off[job_idx[i]] = job_elem_off[i];
     write_chunks(job_chunk, job_idx[i], job_elem_off[i], jp.n);

@@ -191,29 +191,22 @@ __global__ void __launch_bounds__(256) k_setup_dev(SeqConst sc, const PlanMeta* 
 __global__ void __launch_bounds__(256) k_reproj_dev(SeqConst sc, const PlanMeta* __restrict__ meta,
                                                     const JobDev* __restrict__ jobs, const int* __restrict__ job_offsets,
                                                     const int* __restrict__ chunk_start,
-                                                    const BlockSetup* __restrict__ setups, MpaCache cache,
-                                                    int32_t* __restrict__ out) {
+                                                    const BlockSetup* __restrict__ setups, MpaCache cache, McIn mc) {
   const int g = xcd_block() * blockDim.x + threadIdx.x;
   const int n_elems = meta->n_elems;
   if (g - (int)__lane_id() >= n_elems) return;  // whole wave past the end
   const int ji = wave_find_item(job_offsets, chunk_start, g, meta->n_jobs);
   if (g >= n_elems) return;
-  reproj_thread(g, ji, sc, jobs, job_offsets, setups, cache, out);
+  reproj_thread_mc(g, ji, sc, jobs, job_offsets, setups, cache, mc);
 }
 
-__global__ void __launch_bounds__(256) k_mc_dev(Geometry geo, const PlanMeta* __restrict__ meta,
-                                                const PuDev* __restrict__ pus, const int* __restrict__ pu_offsets,
-                                                const int* __restrict__ chunk_start, const JobDev* __restrict__ jobs,
-                                                const int32_t* __restrict__ reproj, const PicTables t,
-                                                int16_t* __restrict__ dst_y, int dsy, int16_t* __restrict__ dst_cb,
-                                                int16_t* __restrict__ dst_cr, int dsc) {
+__global__ void __launch_bounds__(256) k_mc_dev(Geometry geo, const PlanMeta* __restrict__ meta, McIn mc,
+                                                const PicTables t, int16_t* __restrict__ dst_y, int dsy,
+                                                int16_t* __restrict__ dst_cb, int16_t* __restrict__ dst_cr, int dsc) {
   const int g = xcd_block() * blockDim.x + threadIdx.x;
-  const int n_sb = meta->n_sb;
-  if (g - (int)__lane_id() >= n_sb) return;  // whole wave past the end
-  const int pi = wave_find_item(pu_offsets, chunk_start, g, meta->n_pus);
-  if (g >= n_sb) return;
+  if (g >= meta->n_sb) return;
   const Taps taps{c_luma_taps, c_chroma_taps, &c_packed_taps};
-  mc_thread(g, pi, geo, taps, pus, jobs, reproj, t.ref, dst_y, dsy, dst_cb, dst_cr, dsc);
+  mc_thread_rec(g, meta->sb_base[1], meta->sb_base[2], geo, taps, mc, t.ref, dst_y, dsy, dst_cb, dst_cr, dsc);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -402,6 +395,8 @@ struct mm_ctx {
   DevBuf<mm_pu_desc> d_pu_in;  // PU list copied in by mm_pred / mm_pred_prepare
   DevBuf<PlanCounters> d_cnt;
   DevBuf<PlanMeta> d_meta;
+  DevBuf<mm_int4> d_mc_lum[2];
+  DevBuf<mm_int2> d_mc_chr[2];
   PlanCaps caps{};
   int prep_poc = 0, prep_n = 0;
   bool prepared = false;
@@ -565,6 +560,10 @@ int mm_destroy(mm_ctx* c) {
   c->d_reproj.release();
   c->d_pus.release();
   c->d_pu_in.release();
+  for (int l = 0; l < 2; l++) {
+    c->d_mc_lum[l].release();
+    c->d_mc_chr[l].release();
+  }
   c->d_cnt.release();
   c->d_meta.release();
   c->d_ged.release();
@@ -685,6 +684,10 @@ static int ensure_plan_buffers(mm_ctx* c, int n) {
   HIPCHK(c, c->d_reproj.ensure(2 * (size_t)k.elems));
   HIPCHK(c, c->d_cnt.ensure(1));
   HIPCHK(c, c->d_meta.ensure(1));
+  for (int l = 0; l < 2; l++) {
+    HIPCHK(c, c->d_mc_lum[l].ensure(k.sb));
+    HIPCHK(c, c->d_mc_chr[l].ensure(k.sb));
+  }
   return MM_OK;
 }
 
@@ -717,11 +720,16 @@ static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, in
   hipLaunchKernelGGL(k_setup_dev, dim3(gs), dim3(256), 0, c->stream, c->sc, c->d_meta.p, c->d_jobs.p, t,
                      c->d_setup.p);
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[1], c->stream));
+  McIn mc;
+  for (int l = 0; l < 2; l++) {
+    mc.lum[l] = c->d_mc_lum[l].p;
+    mc.chr[l] = c->d_mc_chr[l].p;
+  }
   hipLaunchKernelGGL(k_reproj_dev, dim3(gr), dim3(256), 0, c->stream, c->sc, c->d_meta.p, c->d_jobs.p,
-                     c->d_job_off.p, c->d_job_chunk.p, c->d_setup.p, make_cache(c), c->d_reproj.p);
+                     c->d_job_off.p, c->d_job_chunk.p, c->d_setup.p, make_cache(c), mc);
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[2], c->stream));
-  hipLaunchKernelGGL(k_mc_dev, dim3(gm), dim3(256), 0, c->stream, geo, c->d_meta.p, c->d_pus.p, c->d_pu_off.p,
-                     c->d_pu_chunk.p, c->d_jobs.p, c->d_reproj.p, t, dy, (int)sdy, dcb, dcr, (int)sdc);
+  hipLaunchKernelGGL(k_mc_dev, dim3(gm), dim3(256), 0, c->stream, geo, c->d_meta.p, mc, t, dy, (int)sdy, dcb, dcr,
+                     (int)sdc);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipEventRecord(c->ev1, c->stream));
   c->status_pending = true;

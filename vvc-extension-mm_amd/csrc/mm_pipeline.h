@@ -29,6 +29,24 @@ struct JobDev {
   int n;        // elements = (cw/sbw)*(ch/sbh)
   int rows;     // ch/sbh (Eigen column-major rows)
   int offset;   // first element in the result array
+  // device-planned prediction: where k_mc finds this job's results (McIn, one record per luma
+  // 4x4 sub-block of the PU, row-major from sb_base)
+  int sb_base, pu_cols, list, slot, alias;  // alias: MPA chroma == luma, fill both records
+};
+
+// Per-luma-sub-block inputs of k_mc, written by the reprojection of a device-planned picture so
+// that k_mc reads them with one coalesced load per list instead of chasing PU -> job -> result:
+// lum[l][g] = (xPos/xFrac fixed point X, Y, PU id << 5 | reference slot, oy << 16 | ox) and chr[l][g] = the
+// chroma X, Y (1/32 pel) of list l for luma sub-block g.
+struct alignas(16) mm_int4 {
+  int x, y, z, w;
+};
+struct alignas(8) mm_int2 {
+  int x, y;
+};
+struct McIn {
+  mm_int4* lum[2];
+  mm_int2* chr[2];
 };
 
 struct PuDev {
@@ -107,6 +125,45 @@ MM_HD void mpa_cache_thread(int t, const SeqConst& sc, int plane, int cols, int 
   vip[t] = v ? 1 : 0;
 }
 
+// The reprojection of one element of a device-planned job, stored in k_mc's record layout.
+MM_HD void reproj_thread_mc(int g, int ji, const SeqConst& sc, const JobDev* jobs, const int* job_offsets,
+                            const BlockSetup* setups, const MpaCache& cache, const McIn& mc) {
+  const JobDev& j = jobs[ji];
+  const int local = g - job_offsets[ji];
+  const int col = local / j.rows, row = local - col * j.rows;
+  const float gx = (float)(j.x + 4 * col) + sc.off;
+  const float gy = (float)(j.y + 4 * row) + sc.off;
+  const bool mpa_cached = (j.comp == 0) && (j.model >= MPA_FRONT_BACK && j.model <= MPA_TOP_BOTTOM);
+  float px = 0.0f, py = 0.0f;
+  bool vip = false;
+  if (mpa_cached) {
+    const int ci = ((j.y >> 2) + row) * cache.cols + (j.x >> 2) + col;
+    const int pl = j.model - MPA_FRONT_BACK;
+    px = cache.px[pl][ci];
+    py = cache.py[pl][ci];
+    vip = cache.vip[pl][ci] != 0;
+  }
+  int32_t fx, fy;
+  reproject_element(sc, setups[ji], gx, gy, packet_lane(local, j.n), mpa_cached, px, py, vip, j.comp ? 1 : 0, &fx,
+                    &fy);
+  // chroma 2x2 sub-block (row, col) belongs to luma 4x4 sub-block (row, col) of the same PU
+  const int sb = j.sb_base + row * j.pu_cols + col;
+  mm_int2 xy;
+  xy.x = fx;
+  xy.y = fy;
+  if (j.comp == 0) {
+    mm_int4 r;
+    r.x = fx;
+    r.y = fy;
+    r.z = (j.sb_base << 5) | j.slot;  // reference slot (< 32) and the PU's id (its first sub-block)
+    r.w = ((j.y + 4 * row) << 16) | (j.x + 4 * col);
+    mc.lum[j.list][sb] = r;
+    if (j.alias) mc.chr[j.list][sb] = xy;
+  } else {
+    mc.chr[j.list][sb] = xy;
+  }
+}
+
 MM_HD void setup_thread(int t, const SeqConst& sc, const JobDev* jobs, const M3* ged, BlockSetup* out) {
   const JobDev j = jobs[t];
   const int cs = j.comp ? 1 : 0;
@@ -160,6 +217,100 @@ MM_HD void store_row(int16_t* d, const int16_t* v, int vec) {
 #endif
   (void)vec;
   for (int c = 0; c < N; c++) d[c] = v[c];
+}
+
+// One luma 4x4 sub-block and its two 4:2:0 chroma 2x2 sub-blocks from the McIn records (device-
+// planned pictures): g's class comes from the bucket bounds (bi, then uni L0, then uni L1).
+MM_HD void mc_thread_rec(int g, int uni_l0_start, int uni_l1_start, const Geometry& geo, const Taps& taps,
+                         const McIn& mc, const RefDev* refs, int16_t* dst_y, int dsy, int16_t* dst_cb,
+                         int16_t* dst_cr, int dsc) {
+  const bool bi = g < uni_l0_start;
+  const int uni_list = g < uni_l1_start ? 0 : 1;
+  const bool used[2] = {bi || uni_list == 0, bi || uni_list == 1};
+  mm_int4 L[2];
+  mm_int2 C[2];
+#pragma unroll
+  for (int l = 0; l < 2; l++) {
+    if (!used[l]) continue;
+    L[l] = mc.lum[l][g];
+    if (geo.chroma) C[l] = mc.chr[l][g];
+  }
+  const int pos = used[0] ? L[0].w : L[1].w;
+  const int ox = pos & 0xffff, oy = pos >> 16;
+  int16_t pl[2][16];
+#pragma unroll
+  for (int l = 0; l < 2; l++) {
+    if (!used[l]) continue;
+    const int32_t fx = L[l].x, fy = L[l].y;
+    const int xPos = fx >> 4, yPos = fy >> 4, xFrac = fx & 15, yFrac = fy & 15;
+    const RefDev r = refs[L[l].z & 31];
+    if (sb_out_of_range(xPos, yPos, geo.W, geo.H, geo.maxCUw, geo.maxCUh, 4, 4)) {
+      for (int i = 0; i < 16; i++) pl[l][i] = 0;
+    } else if (window_interior<8, 4, 4>(xPos, yPos, geo.W, geo.H)) {
+#if defined(__HIP_DEVICE_COMPILE__)
+      predict_subblock_interior<8, 4, 4>(r.y, r.stride_y, xPos, yPos, taps.packed->lh[xFrac][(xPos - 3) & 1],
+                                         taps.packed->lv[yFrac], bi, geo.bd, pl[l]);
+#else
+      predict_subblock_interior<8, 4, 4>(r.y, r.stride_y, xPos, yPos, taps.luma[xFrac], taps.luma[yFrac], bi, geo.bd,
+                                         pl[l]);
+#endif
+    } else {
+      predict_subblock<8, 4, 4>(r.y, r.stride_y, geo.W, geo.H, xPos, yPos, taps.luma[xFrac], taps.luma[yFrac], bi,
+                                geo.bd, pl[l]);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    int16_t o[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const int i = r * 4 + c;
+      o[c] = bi ? add_avg(pl[0][i], pl[1][i], geo.bd) : (uni_list == 0 ? pl[0][i] : pl[1][i]);
+    }
+    store_row<4>(dst_y + (long)(oy + r) * dsy + ox, o, geo.vec_store);
+  }
+  if (!geo.chroma) return;
+  int16_t pcb[2][4], pcr[2][4];
+#pragma unroll
+  for (int l = 0; l < 2; l++) {
+    if (!used[l]) continue;
+    const int32_t fx = C[l].x, fy = C[l].y;
+    const int xPos = fx >> 5, yPos = fy >> 5, xFrac = fx & 31, yFrac = fy & 31;
+    const RefDev r = refs[L[l].z & 31];
+    if (sb_out_of_range(xPos, yPos, geo.Wc, geo.Hc, geo.maxCUwc, geo.maxCUhc, 2, 2)) {
+      for (int i = 0; i < 4; i++) pcb[l][i] = pcr[l][i] = 0;
+    } else if (window_interior<4, 2, 2>(xPos, yPos, geo.Wc, geo.Hc)) {
+#if defined(__HIP_DEVICE_COMPILE__)
+      const uint32_t* ht = taps.packed->ch[xFrac][(xPos - 1) & 1];
+      const uint32_t* vt = taps.packed->cv[yFrac];
+      predict_subblock_interior<4, 2, 2>(r.cb, r.stride_c, xPos, yPos, ht, vt, bi, geo.bd, pcb[l]);
+      predict_subblock_interior<4, 2, 2>(r.cr, r.stride_c, xPos, yPos, ht, vt, bi, geo.bd, pcr[l]);
+#else
+      predict_subblock_interior<4, 2, 2>(r.cb, r.stride_c, xPos, yPos, taps.chroma[xFrac], taps.chroma[yFrac], bi,
+                                         geo.bd, pcb[l]);
+      predict_subblock_interior<4, 2, 2>(r.cr, r.stride_c, xPos, yPos, taps.chroma[xFrac], taps.chroma[yFrac], bi,
+                                         geo.bd, pcr[l]);
+#endif
+    } else {
+      predict_subblock<4, 2, 2>(r.cb, r.stride_c, geo.Wc, geo.Hc, xPos, yPos, taps.chroma[xFrac], taps.chroma[yFrac],
+                                bi, geo.bd, pcb[l]);
+      predict_subblock<4, 2, 2>(r.cr, r.stride_c, geo.Wc, geo.Hc, xPos, yPos, taps.chroma[xFrac], taps.chroma[yFrac],
+                                bi, geo.bd, pcr[l]);
+    }
+  }
+  const int cx = ox >> 1, cy = oy >> 1;
+#pragma unroll
+  for (int r = 0; r < 2; r++) {
+    int16_t ob[2], orr[2];
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+      const int i = r * 2 + c;
+      ob[c] = bi ? add_avg(pcb[0][i], pcb[1][i], geo.bd) : (uni_list == 0 ? pcb[0][i] : pcb[1][i]);
+      orr[c] = bi ? add_avg(pcr[0][i], pcr[1][i], geo.bd) : (uni_list == 0 ? pcr[0][i] : pcr[1][i]);
+    }
+    store_row<2>(dst_cb + (long)(cy + r) * dsc + cx, ob, geo.vec_store);
+    store_row<2>(dst_cr + (long)(cy + r) * dsc + cx, orr, geo.vec_store);
+  }
 }
 
 // One luma 4x4 sub-block (and its two 4:2:0 chroma 2x2 sub-blocks) of one PU: both lists,
