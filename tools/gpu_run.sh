@@ -17,7 +17,7 @@ run() {  # name limit cmd...
 }
 for step in "$@"; do
   case $step in
-    tests) run gpu_tests 900 python -m pytest tests -x -q -m gpu ;;
+    tests) run gpu_tests 900 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
