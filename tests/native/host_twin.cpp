@@ -22,6 +22,7 @@ struct Twin {
   Geometry geo;
   std::vector<float> px[3], py[3];
   std::vector<uint8_t> vip[3];
+  std::vector<float> sph[3], tan3[3];  // frame-grid sphere points / TAN terms (k_sph_cache)
 };
 
 static void make_twin(const mm_seq_params* p, Twin* t) {
@@ -45,6 +46,20 @@ static void make_twin(const mm_seq_params* p, Twin* t) {
       mpa_cache_thread(i, t->sc, MPA_FRONT_BACK + pl, cols, rows, t->px[pl].data(), t->py[pl].data(),
                        t->vip[pl].data());
   }
+  const uint32_t sph_models = (1u << TANGENTIAL) | (1u << THREE_D_TRANSLATIONAL) | (1u << ROTATIONAL) |
+                              (1u << GEODESIC_X) | (1u << GEODESIC_Y) | (1u << GEODESIC_Z) | (1u << GEODESIC_CAMPOSE);
+  if (p->active_models & sph_models) {
+    const bool tan = p->active_models & (1u << TANGENTIAL);
+    for (int k = 0; k < 3; k++) {
+      t->sph[k].resize(n);
+      if (tan) t->tan3[k].resize(n);
+    }
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < n; i++)
+      sph_cache_thread(i, t->sc, cols, t->sph[0].data(), t->sph[1].data(), t->sph[2].data(),
+                       tan ? t->tan3[0].data() : nullptr, tan ? t->tan3[1].data() : nullptr,
+                       tan ? t->tan3[2].data() : nullptr);
+  }
 }
 
 static MpaCache cache_of(const Twin& t) {
@@ -56,6 +71,16 @@ static MpaCache cache_of(const Twin& t) {
   }
   c.cols = t.geo.W / 4;
   c.rows = t.geo.H / 4;
+  if (!t.sph[0].empty()) {
+    c.sx = t.sph[0].data();
+    c.sy = t.sph[1].data();
+    c.sz = t.sph[2].data();
+  }
+  if (!t.tan3[0].empty()) {
+    c.ta = t.tan3[0].data();
+    c.tse = t.tan3[1].data();
+    c.tce = t.tan3[2].data();
+  }
   return c;
 }
 
@@ -103,7 +128,7 @@ static int twin_pred_list(const Twin& t, const mmdev::PicTables& tab, const mm_p
   for (int i = 0; i < n; i++) {
     classify_pu(pus[i], tab, &plans[i]);
     if (plans[i].code) return plans[i].code;
-    cnt.pu_tot[plans[i].cls] += pack_count(1, plans[i].n_sb);
+    cnt.pu_tot[plans[i].key] += pack_count(1, plans[i].n_sb);
     for (int k = 0; k < 4; k++)
       if (plans[i].job[k].valid) cnt.job_tot[plans[i].job[k].key] += pack_count(1, plans[i].job[k].n);
   }
@@ -115,8 +140,8 @@ static int twin_pred_list(const Twin& t, const mmdev::PicTables& tab, const mm_p
   std::vector<int> job_off(m.n_jobs), job_chunk(m.n_elems / 64 + 1);
   for (int i = 0; i < n; i++) {
     const PuPlan& pp = plans[i];
-    const unsigned long long bp = cnt.pu_cur[pp.cls];
-    cnt.pu_cur[pp.cls] += pack_count(1, pp.n_sb);
+    const unsigned long long bp = cnt.pu_cur[pp.key];
+    cnt.pu_cur[pp.key] += pack_count(1, pp.n_sb);
     int jidx[4] = {0, 0, 0, 0}, joff[4] = {0, 0, 0, 0};
     for (int k = 0; k < 4; k++) {
       if (!pp.job[k].valid) continue;
@@ -125,7 +150,7 @@ static int twin_pred_list(const Twin& t, const mmdev::PicTables& tab, const mm_p
       joff[k] = m.elem_base[key] + packed_elems(cnt.job_cur[key]);
       cnt.job_cur[key] += pack_count(1, pp.job[k].n);
     }
-    emit_pu(pus[i], pp, m.pu_base[pp.cls] + packed_items(bp), m.sb_base[pp.cls] + packed_elems(bp), jidx, joff,
+    emit_pu(pus[i], pp, m.pu_base[pp.key] + packed_items(bp), m.sb_base[pp.key] + packed_elems(bp), jidx, joff,
             dpus.data(), pu_off.data(), pu_chunk.data(), jobs.data(), job_off.data(), job_chunk.data());
   }
   std::vector<BlockSetup> setups(m.n_jobs);
@@ -148,7 +173,7 @@ static int twin_pred_list(const Twin& t, const mmdev::PicTables& tab, const mm_p
   const Taps taps{LUMA_T, CHROMA_T, nullptr};
 #pragma omp parallel for schedule(static, 256)
   for (int g = 0; g < m.n_sb; g++)
-    mc_thread_rec(g, m.sb_base[1], m.sb_base[2], t.geo, taps, mc, tab.ref, dy, sdy, dcb, dcr, sdc);
+    mc_thread_rec(g, sb_class(g, m.sb_base), t.geo, taps, mc, tab.ref, dy, sdy, dcb, dcr, sdc);
   return 0;
 }
 

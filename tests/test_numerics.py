@@ -10,16 +10,16 @@ import pytest
 
 from helpers import GOLDEN, ROOT
 
-CHECK = "/tmp/mm360_check_numerics"
-
 
 @pytest.fixture(scope="module")
-def checker():
+def checker(tmp_path_factory):
+    # one binary per test process (pytest -n workers must not overwrite each other's executable)
+    check = str(tmp_path_factory.mktemp("numerics") / "mm360_check_numerics")
     src = os.path.join(ROOT, "tools", "check_numerics.cpp")
     inc = os.path.join(ROOT, "vvc-extension-mm_amd", "csrc")
     subprocess.check_call(["g++", "-O2", "-std=c++17", "-mfma", "-msse4.1", "-ffp-contract=off", "-fopenmp",
-                           "-I", inc, src, "-o", CHECK, "-lm"])
-    return CHECK
+                           "-I", inc, src, "-o", check, "-lm"])
+    return check
 
 
 @pytest.mark.parametrize("fn", ["sinf", "cosf", "atanf", "acosf", "asinf", "tanf", "roundf", "dsin", "dcos",

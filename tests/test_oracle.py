@@ -72,7 +72,7 @@ def test_twin_reproject_edge_cases():
     assert np.array_equal(o, t), describe_mismatch(blocks, o, t)
 
 
-@pytest.mark.parametrize("cfg_name", ["C1", "C2"])
+@pytest.mark.parametrize("cfg_name", ["C1", "C2", "C3"])
 def test_twin_pred_matches_oracle(cfg_name):
     cfg = W.CONFIGS[cfg_name]
     params = mm360.seq_params(cfg.width, cfg.height, cfg.models)

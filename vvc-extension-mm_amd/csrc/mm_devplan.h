@@ -23,7 +23,17 @@ namespace mmdev {
 using namespace mmpipe;
 
 constexpr int MAX_SLOTS = 16;  // reference pictures addressable by one picture (2 lists x 8)
-constexpr int N_PU_KEYS = 3;   // bi, uni L0, uni L1
+// PU buckets: class (bi, uni L0, uni L1) x sub-block alignment.  PUs whose sub-block count is a
+// multiple of 4 come first (buckets 0-2), so every aligned group of 4 consecutive sub-blocks
+// (a lane quad of k_mc) lies inside one PU; the rest (4x8 / 8x4 / 4x4 ...) follow (buckets 3-5).
+constexpr int N_PU_KEYS = 6;
+MM_HD int pu_key(int cls, int n_sb) { return cls + ((n_sb & 3) ? 3 : 0); }
+// class of flat luma sub-block g from the bucket bases (PlanMeta::sb_base)
+MM_HD int sb_class(int g, const int* sb_base) {
+  int k = N_PU_KEYS - 1;
+  while (k > 0 && g < sb_base[k]) k--;
+  return k % 3;
+}
 constexpr int N_JOB_KEYS = 64;
 
 // Per-picture constant tables, passed by value as kernel arguments.
@@ -60,6 +70,7 @@ struct JobPlan {
 struct PuPlan {
   int code;     // MM_OK or the error this PU raises
   int cls;      // 0 bi, 1 uni L0, 2 uni L1
+  int key;      // PU bucket (pu_key)
   int n_sb;     // luma 4x4 sub-blocks
   int slot[2];
   JobPlan job[4];   // [2 * list + comp]; fixed slots keep the struct in registers
@@ -89,6 +100,7 @@ MM_HD void classify_pu(const mm_pu_desc& u, const PicTables& t, PuPlan* p) {
   p->code = MM_OK;
   for (int k = 0; k < 4; k++) p->job[k].valid = 0;
   p->cls = 0;
+  p->key = 0;
   p->n_sb = 0;
   p->slot[0] = p->slot[1] = -1;
   p->alias[0] = p->alias[1] = 0;
@@ -152,6 +164,7 @@ MM_HD void classify_pu(const mm_pu_desc& u, const PicTables& t, PuPlan* p) {
   }
   p->cls = (p->slot[0] >= 0 && p->slot[1] >= 0) ? 0 : (p->slot[0] >= 0 ? 1 : 2);
   p->n_sb = (u.w / 4) * (u.h / 4);
+  p->key = pu_key(p->cls, p->n_sb);
 }
 
 MM_HD unsigned long long status_word(int pu_index, int code) {

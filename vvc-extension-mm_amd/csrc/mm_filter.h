@@ -242,12 +242,21 @@ __device__ __forceinline__ int dot2_seed_(uint32_t a, uint32_t b, int seed) {
 //    pairs (one v_perm each) for the vertical pass, which uses the even/odd tap sets the same way.
 // ht: 2 * NQ H tap pairs (even outputs, odd outputs) for this window's phase and parity;
 // vt: NP + NQ V tap pairs (even rows, odd rows).
-template <int NT, int SBW, int SBH>
-__device__ __forceinline__ void predict_subblock_interior(const int16_t* __restrict__ ref, int stride, int xPos, int yPos,
-                                                          const uint32_t* __restrict__ ht,
-                                                          const uint32_t* __restrict__ vt, bool bi, int bd,
-                                                          int16_t* out) {
-  constexpr int R = SBH + NT - 1, H0 = NT / 2 - 1;
+// Window rows from a reference plane in global memory: row r starts at base + r * stride_dw.
+struct GlobalRows {
+  const uint32_t* base;  // dword holding the even sample at or below the window's first column
+  int stride_dw;
+  template <int ND>
+  __device__ __forceinline__ void load(int r, uint32_t* d) const {
+    load_dwords<ND>(base + (long)r * stride_dw, d);
+  }
+};
+
+// The same filter arithmetic over any row source (GlobalRows, or an LDS image of the window).
+template <int NT, int SBW, int SBH, class Rows>
+__device__ __forceinline__ void predict_rows(const Rows& rows, const uint32_t* __restrict__ ht,
+                                             const uint32_t* __restrict__ vt, bool bi, int bd, int16_t* out) {
+  constexpr int R = SBH + NT - 1;
   constexpr int L = SBW + NT - 1;
   constexpr int ND = (L + 2) / 2;  // dwords loaded per row (L + 1 samples from the even base)
   constexpr int NP = NT / 2;       // tap pairs of an even V output
@@ -265,15 +274,13 @@ __device__ __forceinline__ void predict_subblock_interior(const int16_t* __restr
   }
 #pragma unroll
   for (int k = 0; k < NP; k++) ve[k] = vt[k];
-  const int x0 = xPos - H0;
   uint32_t tmp[R + 1][SBW];  // H outputs; only the low 16 bits are used
 #pragma unroll
   for (int c = 0; c < SBW; c++) tmp[R][c] = 0u;
 #pragma unroll
   for (int r = 0; r < R; r++) {
-    const uint32_t* p = reinterpret_cast<const uint32_t*>(ref + (long)(yPos + r - H0) * stride + (x0 & ~1));
     uint32_t d[ND];
-    load_dwords<ND>(p, d);
+    rows.template load<ND>(r, d);
 #pragma unroll
     for (int c = 0; c < SBW; c++) {
       const uint32_t* tp = (c & 1) ? ho : he;
@@ -305,6 +312,16 @@ __device__ __forceinline__ void predict_subblock_interior(const int16_t* __restr
       out[r * SBW + c] = (int16_t)v;
     }
   }
+}
+template <int NT, int SBW, int SBH>
+__device__ __forceinline__ void predict_subblock_interior(const int16_t* __restrict__ ref, int stride, int xPos, int yPos,
+                                                          const uint32_t* __restrict__ ht,
+                                                          const uint32_t* __restrict__ vt, bool bi, int bd,
+                                                          int16_t* out) {
+  constexpr int H0 = NT / 2 - 1;
+  const int x0 = xPos - H0;
+  const GlobalRows rows{reinterpret_cast<const uint32_t*>(ref + (long)(yPos - H0) * stride + (x0 & ~1)), stride >> 1};
+  predict_rows<NT, SBW, SBH>(rows, ht, vt, bi, bd, out);
 }
 #else
 // predict_subblock for an interior window (host): same arithmetic, window rows read with wide loads

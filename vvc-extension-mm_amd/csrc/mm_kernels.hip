@@ -27,8 +27,20 @@
 #include <vector>
 
 #include "../../include/mm360.h"
+#include "mm_mc_lds.h"
 #include "mm_pipeline.h"
 #include "mm_plan.h"
+
+// k_mc_dev stages the quads' reference windows through LDS (mm_mc_lds.h); 0 = per-lane loads
+#ifndef MM_MC_STAGED
+#define MM_MC_STAGED 0
+#endif
+// Packet lanes of TAN / 3DT / ROT / GED read their sphere point from a frame-grid cache
+// (k_sph_cache).  Off by default: the 14-28 MB cache costs more in L2 / Infinity-Cache pressure
+// (k_reproj_dev +5 us, k_mc_dev +6 us at C3) than the 4 packet sin/cos per element it saves.
+#ifndef MM_SPH_CACHE
+#define MM_SPH_CACHE 0
+#endif
 
 using namespace mmpipe;
 
@@ -44,6 +56,13 @@ __global__ void k_mpa_cache(SeqConst sc, int plane, int cols, int rows, float* p
   int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= cols * rows) return;
   mpa_cache_thread(t, sc, plane, cols, rows, px, py, vip);
+}
+
+__global__ void k_sph_cache(SeqConst sc, int cols, int n, float* sx, float* sy, float* sz, float* ta, float* tse,
+                            float* tce) {
+  int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  sph_cache_thread(t, sc, cols, sx, sy, sz, ta, tse, tce);
 }
 
 __global__ void k_setup(SeqConst sc, const JobDev* __restrict__ jobs, int n_jobs, const M3* __restrict__ ged,
@@ -88,7 +107,12 @@ __device__ __forceinline__ int xcd_block() {
   return grp * (8 * XCD_RUN) + (r & 7) * XCD_RUN + (r >> 3);
 }
 
-__global__ void __launch_bounds__(256) k_plan_count(const mm_pu_desc* __restrict__ pus, int n, const PicTables t,
+// Planning blocks are 1024 threads wide: each block ends with one global atomic per bucket, and
+// those land on the same ~70 addresses from every block, so fewer, wider blocks cut the
+// serialised memory-side atomics per address 4x.
+constexpr int PLAN_BLOCK = 1024;
+
+__global__ void __launch_bounds__(PLAN_BLOCK) k_plan_count(const mm_pu_desc* __restrict__ pus, int n, const PicTables t,
                                                     PlanCounters* __restrict__ cnt) {
   __shared__ unsigned long long s_pu[N_PU_KEYS], s_job[N_JOB_KEYS], s_status;
   const int tid = threadIdx.x;
@@ -104,7 +128,7 @@ __global__ void __launch_bounds__(256) k_plan_count(const mm_pu_desc* __restrict
     if (p.code != MM_OK) {
       atomicMax(&s_status, status_word(i, p.code));
     } else {
-      atomicAdd(&s_pu[p.cls], pack_count(1, p.n_sb));
+      atomicAdd(&s_pu[p.key], pack_count(1, p.n_sb));
 #pragma unroll
       for (int k = 0; k < 4; k++)
         if (p.job[k].valid) atomicAdd(&s_job[p.job[k].key], pack_count(1, p.job[k].n));
@@ -116,8 +140,11 @@ __global__ void __launch_bounds__(256) k_plan_count(const mm_pu_desc* __restrict
   if (tid == 0 && s_status) atomicMax(&cnt->status, s_status);
 }
 
-__global__ void __launch_bounds__(256) k_plan_place(const mm_pu_desc* __restrict__ pus, int n, const PicTables t,
-                                                    PlanCounters* __restrict__ cnt, PlanMeta* __restrict__ meta,
+// `next` is the other counter set of the ping-pong pair: block 0 zeroes it for the next picture, so
+// no memset launch precedes k_plan_count.
+__global__ void __launch_bounds__(PLAN_BLOCK) k_plan_place(const mm_pu_desc* __restrict__ pus, int n, const PicTables t,
+                                                    PlanCounters* __restrict__ cnt, PlanCounters* __restrict__ next,
+                                                    PlanMeta* __restrict__ meta,
                                                     PlanCaps caps, PuDev* __restrict__ d_pus, int* __restrict__ pu_off,
                                                     int* __restrict__ pu_chunk, JobDev* __restrict__ jobs,
                                                     int* __restrict__ job_off, int* __restrict__ job_chunk) {
@@ -126,10 +153,53 @@ __global__ void __launch_bounds__(256) k_plan_place(const mm_pu_desc* __restrict
   __shared__ PlanMeta s_meta;
   __shared__ int s_ok;
   const int tid = threadIdx.x;
+  if (blockIdx.x == 0) {
+    constexpr int NW = (int)(sizeof(PlanCounters) / sizeof(unsigned long long));
+    static_assert(NW <= PLAN_BLOCK, "one thread per counter word");
+    if (tid < NW) reinterpret_cast<unsigned long long*>(next)[tid] = 0ull;
+  }
   if (tid < N_PU_KEYS) s_pu[tid] = 0;
   if (tid < N_JOB_KEYS) s_job[tid] = 0;
+  // PlanMeta = exclusive prefix of the bucket totals: wave 0 loads all 64 job totals at once and
+  // scans them across lanes (a serial loop of dependent loads would cost every block ~70 memory
+  // latencies)
+  static_assert(N_JOB_KEYS == 64, "one lane per job bucket");
+  if (tid < 64) {
+    const unsigned long long v = cnt->job_tot[tid];
+    const int items = packed_items(v), elems = packed_elems(v);
+    int si = items, se = elems;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int ui = __shfl_up(si, d), ue = __shfl_up(se, d);
+      if (tid >= d) {
+        si += ui;
+        se += ue;
+      }
+    }
+    s_meta.job_base[tid] = si - items;
+    s_meta.elem_base[tid] = se - elems;
+    if (tid == 63) {
+      s_meta.n_jobs = si;
+      s_meta.n_elems = se;
+    }
+    if (tid == 0) {
+      unsigned long long pt[N_PU_KEYS];
+#pragma unroll
+      for (int k = 0; k < N_PU_KEYS; k++) pt[k] = cnt->pu_tot[k];
+      int acc = 0, sacc = 0;
+#pragma unroll
+      for (int k = 0; k < N_PU_KEYS; k++) {
+        s_meta.pu_base[k] = acc;
+        s_meta.sb_base[k] = sacc;
+        acc += packed_items(pt[k]);
+        sacc += packed_elems(pt[k]);
+      }
+      s_meta.n_pus = acc;
+      s_meta.n_sb = sacc;
+    }
+  }
+  __syncthreads();
   if (tid == 0) {
-    plan_meta(*cnt, &s_meta);
     s_ok = s_meta.n_pus <= caps.pus && s_meta.n_sb <= caps.sb && s_meta.n_jobs <= caps.jobs &&
            s_meta.n_elems <= caps.elems;
     if (blockIdx.x == 0) {
@@ -152,7 +222,7 @@ __global__ void __launch_bounds__(256) k_plan_place(const mm_pu_desc* __restrict
     u = pus[i];
     classify_pu(u, t, &p);
     if (p.code == MM_OK) {
-      lp = atomicAdd(&s_pu[p.cls], pack_count(1, p.n_sb));
+      lp = atomicAdd(&s_pu[p.key], pack_count(1, p.n_sb));
 #pragma unroll
       for (int k = 0; k < 4; k++)
         if (p.job[k].valid) lj[k] = atomicAdd(&s_job[p.job[k].key], pack_count(1, p.job[k].n));
@@ -163,9 +233,9 @@ __global__ void __launch_bounds__(256) k_plan_place(const mm_pu_desc* __restrict
   if (tid < N_JOB_KEYS && s_job[tid]) g_job[tid] = atomicAdd(&cnt->job_cur[tid], s_job[tid]);
   __syncthreads();
   if (p.code != MM_OK) return;
-  const unsigned long long bp = g_pu[p.cls] + lp;
-  const int pu_idx = s_meta.pu_base[p.cls] + packed_items(bp);
-  const int sb_off = s_meta.sb_base[p.cls] + packed_elems(bp);
+  const unsigned long long bp = g_pu[p.key] + lp;
+  const int pu_idx = s_meta.pu_base[p.key] + packed_items(bp);
+  const int sb_off = s_meta.sb_base[p.key] + packed_elems(bp);
   int jidx[4], joff[4];
 #pragma unroll
   for (int k = 0; k < 4; k++) {
@@ -180,12 +250,25 @@ __global__ void __launch_bounds__(256) k_plan_place(const mm_pu_desc* __restrict
   emit_pu(u, p, pu_idx, sb_off, jidx, joff, d_pus, pu_off, pu_chunk, jobs, job_off, job_chunk);
 }
 
+// The 256 setups of a block are contiguous in `out`: each thread builds its BlockSetup in LDS and
+// the block then streams the whole 22.5 KB image out with 16-byte stores, instead of 22 scattered
+// dword stores per thread into 88-byte strided records (every one a partial cache line).
 __global__ void __launch_bounds__(256) k_setup_dev(SeqConst sc, const PlanMeta* __restrict__ meta,
                                                    const JobDev* __restrict__ jobs, const PicTables t,
                                                    BlockSetup* __restrict__ out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= meta->n_jobs) return;
-  setup_thread(i, sc, jobs, t.ged, out);
+  static_assert(sizeof(BlockSetup) % 8 == 0, "BlockSetup image is copied in 8-byte words");
+  __shared__ alignas(16) BlockSetup s_set[256];
+  const int n_jobs = meta->n_jobs;
+  const int base = blockIdx.x * 256;
+  if (base >= n_jobs) return;
+  const int i = base + threadIdx.x;
+  if (i < n_jobs) setup_job(jobs[i], sc, t.ged, &s_set[threadIdx.x]);
+  __syncthreads();
+  const int cnt = min(256, n_jobs - base);
+  const int words = cnt * (int)(sizeof(BlockSetup) / 8);
+  const uint2* src = reinterpret_cast<const uint2*>(s_set);
+  uint2* dst = reinterpret_cast<uint2*>(out + base);
+  for (int w = threadIdx.x; w < words; w += 256) dst[w] = src[w];
 }
 
 __global__ void __launch_bounds__(256) k_reproj_dev(SeqConst sc, const PlanMeta* __restrict__ meta,
@@ -200,13 +283,27 @@ __global__ void __launch_bounds__(256) k_reproj_dev(SeqConst sc, const PlanMeta*
   reproj_thread_mc(g, ji, sc, jobs, job_offsets, setups, cache, mc);
 }
 
-__global__ void __launch_bounds__(256) k_mc_dev(Geometry geo, const PlanMeta* __restrict__ meta, McIn mc,
+#ifdef MM_MC_WAVES_PER_EU
+#define MM_MC_OCC __attribute__((amdgpu_waves_per_eu(MM_MC_WAVES_PER_EU)))
+#else
+#define MM_MC_OCC
+#endif
+__global__ void __launch_bounds__(MM_MC_BLOCK) MM_MC_OCC k_mc_dev(Geometry geo, const PlanMeta* __restrict__ meta, McIn mc,
                                                 const PicTables t, int16_t* __restrict__ dst_y, int dsy,
                                                 int16_t* __restrict__ dst_cb, int16_t* __restrict__ dst_cr, int dsc) {
   const int g = xcd_block() * blockDim.x + threadIdx.x;
-  if (g >= meta->n_sb) return;
+  const int n_sb = meta->n_sb;
   const Taps taps{c_luma_taps, c_chroma_taps, &c_packed_taps};
-  mc_thread_rec(g, meta->sb_base[1], meta->sb_base[2], geo, taps, mc, t.ref, dst_y, dsy, dst_cb, dst_cr, dsc);
+#if MM_MC_STAGED
+  __shared__ uint32_t s_slab[mmlds::MC_BLOCK / 64][mmlds::WAVE_SLAB_DW];  // one slab per wave
+  if (g - (int)__lane_id() >= n_sb) return;  // whole wave past the end
+  const bool valid = g < n_sb;
+  mmlds::mc_thread_lds(g, valid, valid ? sb_class(g, meta->sb_base) : 0, geo, taps, mc, t.ref, dst_y, dsy, dst_cb,
+                       dst_cr, dsc, s_slab[threadIdx.x >> 6]);
+#else
+  if (g >= n_sb) return;
+  mc_thread_rec(g, sb_class(g, meta->sb_base), geo, taps, mc, t.ref, dst_y, dsy, dst_cb, dst_cr, dsc);
+#endif
 }
 
 // --------------------------------------------------------------------------------------------
@@ -384,6 +481,8 @@ struct mm_ctx {
   float* mpa_px[3] = {nullptr, nullptr, nullptr};
   float* mpa_py[3] = {nullptr, nullptr, nullptr};
   uint8_t* mpa_vip[3] = {nullptr, nullptr, nullptr};
+  float* sph[3] = {nullptr, nullptr, nullptr};   // frame-grid sphere points (k_sph_cache)
+  float* tan3[3] = {nullptr, nullptr, nullptr};  // TAN alpha / psin(eps) / pcos(eps)
   Plan plan;  // host plan of the parity API mm_reproject
   DevBuf<JobDev> d_jobs;
   DevBuf<int> d_job_off, d_job_chunk, d_pu_off, d_pu_chunk;
@@ -393,7 +492,9 @@ struct mm_ctx {
   DevBuf<M3> d_ged;
   // device-planned prediction (mm_pred_device / mm_pred_run)
   DevBuf<mm_pu_desc> d_pu_in;  // PU list copied in by mm_pred / mm_pred_prepare
-  DevBuf<PlanCounters> d_cnt;
+  DevBuf<PlanCounters> d_cnt;  // ping-pong pair: a picture counts in d_cnt[cnt_par] and zeroes the other
+  int cnt_par = 0;
+  PlanCounters* last_cnt = nullptr;  // counters of the last device-planned picture (status word)
   DevBuf<PlanMeta> d_meta;
   DevBuf<mm_int4> d_mc_lum[2];
   DevBuf<mm_int2> d_mc_chr[2];
@@ -449,6 +550,16 @@ static MpaCache make_cache(mm_ctx* c) {
   }
   mc.cols = c->geo.W / 4;
   mc.rows = c->geo.H / 4;
+#if MM_SPH_CACHE
+  mc.sx = c->sph[0];
+#else
+  mc.sx = nullptr;
+#endif
+  mc.sy = c->sph[1];
+  mc.sz = c->sph[2];
+  mc.ta = c->tan3[0];
+  mc.tse = c->tan3[1];
+  mc.tce = c->tan3[2];
   return mc;
 }
 
@@ -529,6 +640,22 @@ int mm_create(const mm_seq_params* p, int device, mm_ctx** out_ctx) {
     hipLaunchKernelGGL(k_mpa_cache, dim3((n + 255) / 256), dim3(256), 0, c->stream, c->sc, MPA_FRONT_BACK + pl, cols,
                        rows, c->mpa_px[pl], c->mpa_py[pl], c->mpa_vip[pl]);
   }
+  // Sphere points of the frame grid (+ TAN's per-point terms): the grid-only first step of the
+  // TAN / 3DT / ROT / GED array expressions, evaluated once per sequence (GridTerms)
+  const uint32_t sph_models = (1u << TANGENTIAL) | (1u << THREE_D_TRANSLATIONAL) | (1u << ROTATIONAL) |
+                              (1u << GEODESIC_X) | (1u << GEODESIC_Y) | (1u << GEODESIC_Z) | (1u << GEODESIC_CAMPOSE);
+  if (MM_SPH_CACHE && (p->active_models & sph_models)) {
+    const bool tan = p->active_models & (1u << TANGENTIAL);
+    for (int k = 0; k < 3; k++) {
+      if (hipMalloc(&c->sph[k], n * sizeof(float)) != hipSuccess ||
+          (tan && hipMalloc(&c->tan3[k], n * sizeof(float)) != hipSuccess)) {
+        mm_destroy(c);
+        return MM_ERR_HIP;
+      }
+    }
+    hipLaunchKernelGGL(k_sph_cache, dim3((n + 255) / 256), dim3(256), 0, c->stream, c->sc, cols, n, c->sph[0],
+                       c->sph[1], c->sph[2], c->tan3[0], c->tan3[1], c->tan3[2]);
+  }
   if (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) {
     mm_destroy(c);
     return MM_ERR_HIP;
@@ -547,6 +674,8 @@ int mm_destroy(mm_ctx* c) {
     (void)hipFree(kv.second.cr);
   }
   for (int pl = 0; pl < 3; pl++) {
+    if (c->sph[pl]) (void)hipFree(c->sph[pl]);
+    if (c->tan3[pl]) (void)hipFree(c->tan3[pl]);
     if (c->mpa_px[pl]) (void)hipFree(c->mpa_px[pl]);
     if (c->mpa_py[pl]) (void)hipFree(c->mpa_py[pl]);
     if (c->mpa_vip[pl]) (void)hipFree(c->mpa_vip[pl]);
@@ -682,7 +811,10 @@ static int ensure_plan_buffers(mm_ctx* c, int n) {
   HIPCHK(c, c->d_job_chunk.ensure(k.elems / 64 + 1));
   HIPCHK(c, c->d_setup.ensure(k.jobs));
   HIPCHK(c, c->d_reproj.ensure(2 * (size_t)k.elems));
-  HIPCHK(c, c->d_cnt.ensure(1));
+  if (!c->d_cnt.p) {
+    HIPCHK(c, c->d_cnt.ensure(2));
+    HIPCHK(c, hipMemsetAsync(c->d_cnt.p, 0, 2 * sizeof(PlanCounters), c->stream));  // once per context
+  }
   HIPCHK(c, c->d_meta.ensure(1));
   for (int l = 0; l < 2; l++) {
     HIPCHK(c, c->d_mc_lum[l].ensure(k.sb));
@@ -707,14 +839,15 @@ static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, in
   geo.vec_store = ((uintptr_t)dy % 8 == 0) && (sdy % 4 == 0) &&
                   (!geo.chroma || ((uintptr_t)dcb % 4 == 0 && (uintptr_t)dcr % 4 == 0 && sdc % 2 == 0));
   const PlanCaps& k = c->caps;
-  const int gp = (n + 255) / 256;
+  const int gp = (n + PLAN_BLOCK - 1) / PLAN_BLOCK;
   const int gs = (k.jobs + 255) / 256;
   const int gr = round_grid((k.elems + 255) / 256);
-  const int gm = round_grid((k.sb + 255) / 256);
+  const int gm = round_grid((k.sb + mmlds::MC_BLOCK - 1) / mmlds::MC_BLOCK);
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-  HIPCHK(c, hipMemsetAsync(c->d_cnt.p, 0, sizeof(PlanCounters), c->stream));
-  hipLaunchKernelGGL(k_plan_count, dim3(gp), dim3(256), 0, c->stream, d_in, n, t, c->d_cnt.p);
-  hipLaunchKernelGGL(k_plan_place, dim3(gp), dim3(256), 0, c->stream, d_in, n, t, c->d_cnt.p, c->d_meta.p, k,
+  PlanCounters* cnt = c->d_cnt.p + c->cnt_par;
+  PlanCounters* next = c->d_cnt.p + (c->cnt_par ^ 1);
+  hipLaunchKernelGGL(k_plan_count, dim3(gp), dim3(PLAN_BLOCK), 0, c->stream, d_in, n, t, cnt);
+  hipLaunchKernelGGL(k_plan_place, dim3(gp), dim3(PLAN_BLOCK), 0, c->stream, d_in, n, t, cnt, next, c->d_meta.p, k,
                      c->d_pus.p, c->d_pu_off.p, c->d_pu_chunk.p, c->d_jobs.p, c->d_job_off.p, c->d_job_chunk.p);
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[0], c->stream));
   hipLaunchKernelGGL(k_setup_dev, dim3(gs), dim3(256), 0, c->stream, c->sc, c->d_meta.p, c->d_jobs.p, t,
@@ -728,10 +861,12 @@ static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, in
   hipLaunchKernelGGL(k_reproj_dev, dim3(gr), dim3(256), 0, c->stream, c->sc, c->d_meta.p, c->d_jobs.p,
                      c->d_job_off.p, c->d_job_chunk.p, c->d_setup.p, make_cache(c), mc);
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[2], c->stream));
-  hipLaunchKernelGGL(k_mc_dev, dim3(gm), dim3(256), 0, c->stream, geo, c->d_meta.p, mc, t, dy, (int)sdy, dcb, dcr,
+  hipLaunchKernelGGL(k_mc_dev, dim3(gm), dim3(mmlds::MC_BLOCK), 0, c->stream, geo, c->d_meta.p, mc, t, dy, (int)sdy, dcb, dcr,
                      (int)sdc);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+  c->last_cnt = cnt;
+  c->cnt_par ^= 1;
   c->status_pending = true;
   return MM_OK;
 }
@@ -743,7 +878,7 @@ static int read_status(mm_ctx* c, int* first_bad) {
   if (!c->status_pending) return MM_OK;
   c->status_pending = false;
   unsigned long long w = 0;
-  HIPCHK(c, hipMemcpy(&w, &c->d_cnt.p->status, sizeof(w), hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(&w, &c->last_cnt->status, sizeof(w), hipMemcpyDeviceToHost));
   if (!w) return MM_OK;
   const unsigned long long v = ~w;
   const int code = (int)(v & 0xff), pu = (int)(v >> 8);

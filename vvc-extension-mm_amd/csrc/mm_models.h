@@ -134,6 +134,13 @@ MM_HD void mpa_to_perspective(int plane, float gx, float gy, const SeqConst& s, 
   persp_from_sphere(q, s.focal, m, px, py, vip, arr);
 }
 
+// toPerspective of one element outside the frame cache (MPA chroma blocks that do not alias the
+// luma job, Eigen tail lanes): out of line, the per-picture path rarely takes it
+MM_HD_COLD void mpa_to_perspective_cold(int plane, float gx, float gy, const SeqConst& s, int packet, float* px,
+                                        float* py, bool* vip) {
+  mpa_to_perspective(plane, gx, gy, s, Math{packet}, px, py, vip);
+}
+
 // MotionPlaneAdaptiveMotionModel::toProjection (array, MotionPlaneAdaptiveMotionModel.cpp:163-187)
 MM_HD void mpa_to_projection(int plane, float px, float py, bool vip, const SeqConst& s, Math m,
                              float* ox, float* oy) {
@@ -332,94 +339,119 @@ MM_HD void block_setup_f(BlockSetup* b, const SeqConst& s, int model, bool luma,
 // <Model>::modelMotion[Cached] of one element: the moved position as computed (before the NaN
 // fallback, offset removal and rounding).  CLASSIC (TranslationalMotionModel::modelMotion,
 // TranslationalMotionModel.cpp:8-13) adds the MV.
+// Per-grid-point terms of the block's array expressions that depend on the element's grid
+// position only, precomputed once per sequence for the whole frame grid with packet math
+// (k_sph_cache).  Valid for packet lanes only: a tail lane computes them with scalar libm.
+struct GridTerms {
+  int have_p;    // p = EquirectangularProjection::toSphere(grid)   (TAN/3DT/ROT/GED first step)
+  int have_tan;  // TAN: alpha = phi(p), se/ce = psin/pcos(pi/2 - theta(p))  (TangentialMotionModel.cpp:21-29)
+  V3 p;
+  float alpha, se, ce;
+};
+
 MM_HD void model_motion_element(const SeqConst& s, const BlockSetup& b, float gx, float gy, bool packet,
-                                bool mpa_cached, float pers_x, float pers_y, bool pers_vip, float* omx, float* omy) {
+                                bool mpa_cached, float pers_x, float pers_y, bool pers_vip, float* omx, float* omy,
+                                const GridTerms* gt = nullptr) {
   const Math m{packet};
-  float mx = gx, my = gy;
   if (b.model == CLASSIC) {
     *omx = gx + b.mvx;
     *omy = gy + b.mvy;
     return;
   }
-  if (!b.identity) {
-    switch (b.model) {
-      case MPA_FRONT_BACK:
-      case MPA_LEFT_RIGHT:
-      case MPA_TOP_BOTTOM: {
-        float px, py;
-        bool vip;
-        if (mpa_cached) {
-          px = pers_x;
-          py = pers_y;
-          vip = pers_vip;
-        } else {
-          mpa_to_perspective(b.model, gx, gy, s, m, &px, &py, &vip);
-        }
-        float sign = vip ? -1.0f : 1.0f;
-        px = px + b.mvx * sign;
-        py = py + b.mvy * sign;
-        mpa_to_projection(b.model, px, py, vip, s, m, &mx, &my);
-      } break;
-      case TANGENTIAL: {
-        V3 p = erp_to_sphere(gx, gy, s, m);
+  if (b.identity || b.model >= NUM_MODELS) {
+    *omx = gx;
+    *omy = gy;
+    return;
+  }
+  // Every model ends in EquirectangularProjection::fromSphere of a moved sphere point q; the
+  // switch computes q and the shared tail projects it (one copy of the acosf/atan2f code).
+  const bool mpa = b.model >= MPA_FRONT_BACK && b.model <= MPA_TOP_BOTTOM;
+  const bool tan_cached = gt && gt->have_tan;
+  V3 p = {0.0f, 0.0f, 0.0f};  // toSphere(grid) of TAN / 3DT / ROT / GED
+  if (gt && gt->have_p)
+    p = gt->p;
+  else if (!mpa && !tan_cached)
+    p = erp_to_sphere(gx, gy, s, m);
+  V3 q;
+  switch (b.model) {
+    case MPA_FRONT_BACK:
+    case MPA_LEFT_RIGHT:
+    case MPA_TOP_BOTTOM: {  // MotionPlaneAdaptiveMotionModel.cpp:26-74
+      float px, py;
+      bool vip;
+      if (mpa_cached) {
+        px = pers_x;
+        py = pers_y;
+        vip = pers_vip;
+      } else {
+        mpa_to_perspective_cold(b.model, gx, gy, s, m.packet, &px, &py, &vip);
+      }
+      float sign = vip ? -1.0f : 1.0f;
+      px = px + b.mvx * sign;
+      py = py + b.mvy * sign;
+      // toProjection (:163-187) up to the ERP step
+      V3 c = persp_to_sphere(px, py, vip, s.focal, m);
+      if (b.model == MPA_FRONT_BACK)
+        q = c;
+      else if (b.model == MPA_LEFT_RIGHT)
+        q = {-c.y, c.x, c.z};
+      else
+        q = {c.z, c.y, -c.x};
+    } break;
+    case TANGENTIAL: {  // TangentialMotionModel.cpp:8-48
+      float alpha, se, ce;
+      if (tan_cached) {
+        alpha = gt->alpha;
+        se = gt->se;
+        ce = gt->ce;
+      } else {
         V3 sp = cart_to_sph(p, m, true);
         float eps = PI_2_F - sp.y;
-        float alpha = sp.z;
-        float dA = alpha - b.alphaC;
-        float se = m.sin(eps), ce = m.cos(eps), cdA = m.cos(dA);
-        float cosPsi = b.sE * se + (b.cE * ce) * cdA;
-        float yP = (se * b.cE - (b.sE * ce) * cdA) / cosPsi;
-        float xP = (m.sin(dA) * ce) / cosPsi;
-        float yM = yP - b.mvy * s.res;
-        float xM = xP - b.mvx * s.res;
-        float rho = m.sqrt(xM * xM + yM * yM);
-        float eta = g_atanf(rho);
-        float gamma = (rho * b.cE) * m.cos(eta) - (yM * b.sE) * m.sin(eta);
-        float alphaM = b.alphaC + g_atanf((xM * g_sinf(eta)) / gamma);
-        float epsM = g_asinf(g_cosf(eta) * b.sE + ((yM * g_sinf(eta)) * b.cE) / rho);
-        V3 c = sph_to_cart(1.0f, PI_2_F - epsM, alphaM, m);
-        erp_from_sphere(c, s, m, true, &mx, &my);
-      } break;
-      case THREE_D_TRANSLATIONAL: {
-        V3 p = erp_to_sphere(gx, gy, s, m);
-        V3 q = {p.x + b.d0, p.y + b.d1, p.z + b.d2};
-        erp_from_sphere(q, s, m, true, &mx, &my);
-      } break;
-      case ROTATIONAL: {
-        V3 p = erp_to_sphere(gx, gy, s, m);
-        V3 q = mat_vec(b.M, p);
-        erp_from_sphere(q, s, m, true, &mx, &my);
-      } break;
-      case GEODESIC_X:
-      case GEODESIC_Y:
-      case GEODESIC_Z:
-      case GEODESIC_CAMPOSE: {
-        V3 p = erp_to_sphere(gx, gy, s, m);
-        V3 q = mat_vec(b.M, p);
-        V3 sp = cart_to_sph(q, m, true);
-        float th;
-        if (s.ged_flavor == 1)
-          th = sp.y + g_atanf(g_sinf(sp.y) / (b.k - g_cosf(sp.y)));
-        else
-          th = sp.y + s.res * b.mvx;
-        float ph = sp.z + s.res * b.mvy;
-        V3 c = sph_to_cart(sp.x, th, ph, m);
-        V3 r = matT_vec(b.M, c);
-        erp_from_sphere(r, s, m, true, &mx, &my);
-      } break;
-      default:
-        break;
-    }
+        alpha = sp.z;
+        se = m.sin(eps);
+        ce = m.cos(eps);
+      }
+      float dA = alpha - b.alphaC;
+      float cdA = m.cos(dA);
+      float cosPsi = b.sE * se + (b.cE * ce) * cdA;
+      float yP = (se * b.cE - (b.sE * ce) * cdA) / cosPsi;
+      float xP = (m.sin(dA) * ce) / cosPsi;
+      float yM = yP - b.mvy * s.res;
+      float xM = xP - b.mvx * s.res;
+      float rho = m.sqrt(xM * xM + yM * yM);
+      float eta = g_atanf(rho);
+      float gamma = (rho * b.cE) * m.cos(eta) - (yM * b.sE) * m.sin(eta);
+      float alphaM = b.alphaC + g_atanf((xM * g_sinf(eta)) / gamma);
+      float epsM = g_asinf(g_cosf(eta) * b.sE + ((yM * g_sinf(eta)) * b.cE) / rho);
+      q = sph_to_cart(1.0f, PI_2_F - epsM, alphaM, m);
+    } break;
+    case THREE_D_TRANSLATIONAL:  // ThreeDTranslationalMotionModel.cpp:7-24
+      q = {p.x + b.d0, p.y + b.d1, p.z + b.d2};
+      break;
+    case ROTATIONAL:  // RotationalMotionModel.cpp:66-77
+      q = mat_vec(b.M, p);
+      break;
+    default: {  // GEODESIC_X/Y/Z/CAMPOSE, GeodesicMotionModel.cpp:101-176
+      V3 r = mat_vec(b.M, p);
+      V3 sp = cart_to_sph(r, m, true);
+      float th;
+      if (s.ged_flavor == 1)
+        th = sp.y + g_atanf(g_sinf(sp.y) / (b.k - g_cosf(sp.y)));
+      else
+        th = sp.y + s.res * b.mvx;
+      float ph = sp.z + s.res * b.mvy;
+      V3 c = sph_to_cart(sp.x, th, ph, m);
+      q = matT_vec(b.M, c);
+    } break;
   }
-  *omx = mx;
-  *omy = my;
+  erp_from_sphere(q, s, m, true, omx, omy);
 }
 
 MM_HD void reproject_element(const SeqConst& s, const BlockSetup& b, float gx, float gy, bool packet,
                              bool mpa_cached, float pers_x, float pers_y, bool pers_vip,
-                             int chroma_shift, int32_t* fx, int32_t* fy) {
+                             int chroma_shift, int32_t* fx, int32_t* fy, const GridTerms* gt = nullptr) {
   float mx, my;
-  model_motion_element(s, b, gx, gy, packet, mpa_cached, pers_x, pers_y, pers_vip, &mx, &my);
+  model_motion_element(s, b, gx, gy, packet, mpa_cached, pers_x, pers_y, pers_vip, &mx, &my, gt);
   // NaN -> unmoved (MVReprojection.cpp:151-154), remove offset, rescale, round to fixed point
   if (isnanf_(mx) || isnanf_(my)) {
     mx = gx;

@@ -20,9 +20,22 @@
 #if defined(__HIPCC__) || defined(__HIP__)
 #define MM_HD __host__ __device__ __forceinline__
 #define MM_HD_CONST __device__ __constant__
+// Rare paths (huge-argument reductions, double-double fallbacks, scalar libm for Eigen tail
+// lanes).  MM_COLD_NOINLINE=1 keeps them out of line (4-5x smaller kernels), but the calls cost
+// more than the instruction-cache misses they save (measured: k_reproj_dev +10 us at C3), so
+// they are inlined by default.
+#ifndef MM_COLD_NOINLINE
+#define MM_COLD_NOINLINE 0
+#endif
+#if MM_COLD_NOINLINE
+#define MM_HD_COLD __host__ __device__ __attribute__((noinline))
+#else
+#define MM_HD_COLD __host__ __device__ __forceinline__
+#endif
 #else
 #define MM_HD inline
 #define MM_HD_CONST static const
+#define MM_HD_COLD inline
 #endif
 
 #include "mm_rsqrtps_table.h"
@@ -134,7 +147,7 @@ MM_HD uint32_t inv_pio4_(int i) {
   }
 }
 
-MM_HD double reduce_large_(uint32_t xi, int* np) {
+MM_HD_COLD double reduce_large_(uint32_t xi, int* np) {
   int idx = (xi >> 26) & 15;
   int shift = (xi >> 23) & 7;
   uint64_t n, res0, res1, res2;
@@ -254,6 +267,8 @@ MM_HD float g_atanf(float x) {
   return (hx < 0) ? -z : z;
 }
 
+MM_HD_COLD float g_atanf_cold(float x) { return g_atanf(x); }
+
 // glibc 2.35 atan2f (sysdeps/ieee754/flt-32/e_atan2f.c)
 MM_HD float g_atan2f(float y, float x) {
   const float tiny = 1.0e-30f, pi_o_4 = 7.8539818525e-01f, pi_o_2 = 1.5707963705e+00f,
@@ -265,7 +280,7 @@ MM_HD float g_atan2f(float y, float x) {
   hy = (int32_t)asu(y);
   iy = hy & 0x7fffffff;
   if ((ix > 0x7f800000) || (iy > 0x7f800000)) return x + y;
-  if (hx == 0x3f800000) return g_atanf(y);
+  if (hx == 0x3f800000) return g_atanf_cold(y);  // x == 1
   m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
   if (iy == 0) {
     switch (m) {
@@ -560,7 +575,7 @@ MM_HD dd_ dd_reduce_pio2_(double x, int* q) {
   s = dd_add_(s, {-k * pio2_3, 0.0});
   return s;
 }
-MM_HD float sinf_via_double_dd(float xf) {
+MM_HD_COLD float sinf_via_double_dd(float xf) {
   double x = xf;
   if (xf == 0.0f) return xf;
   int q;
@@ -574,7 +589,7 @@ MM_HD float sinf_via_double_dd(float xf) {
   }
   return (float)(v.hi + v.lo);
 }
-MM_HD float cosf_via_double_dd(float xf) {
+MM_HD_COLD float cosf_via_double_dd(float xf) {
   double x = xf;
   int q;
   dd_ r = dd_reduce_pio2_(x, &q);
@@ -764,10 +779,13 @@ MM_HD float e_psqrt(float x) {
 
 // Packet-or-scalar selection (Eigen LinearVectorizedTraversal on a 16-byte aligned
 // destination: elements [0, n - n%4) use packets, the tail uses the scalar functors).
+// Scalar sinf/cosf of an Eigen tail lane (out of line: tail lanes are rare, call sites many)
+MM_HD_COLD float g_sinf_tail(float x) { return g_sinf(x); }
+MM_HD_COLD float g_cosf_tail(float x) { return g_cosf(x); }
 struct Math {
   int packet;  // int, not bool: an i1 member defeats SROA and lands in LDS
-  MM_HD float sin(float x) const { return packet ? e_psin(x) : g_sinf(x); }
-  MM_HD float cos(float x) const { return packet ? e_pcos(x) : g_cosf(x); }
+  MM_HD float sin(float x) const { return packet ? e_psin(x) : g_sinf_tail(x); }
+  MM_HD float cos(float x) const { return packet ? e_pcos(x) : g_cosf_tail(x); }
   MM_HD float sqrt(float x) const { return packet ? e_psqrt(x) : sqrtf_(x); }
 };
 MM_HD bool packet_lane(int index, int n) { return index < n - (n & 3); }

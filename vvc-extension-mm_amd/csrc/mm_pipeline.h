@@ -56,12 +56,57 @@ struct PuDev {
   int sb_offset;    // first luma sub-block of this PU in the k_mc enumeration
 };
 
+// Frame-grid caches, row-major [j][i] over the (W/4) x (H/4) grid x = 4i + off, y = 4j + off:
+//  * MPA perspective coordinates per plane (MotionPlaneAdaptiveMotionModel::fillCache);
+//  * the sphere point of every grid position and TAN's per-point terms (GridTerms), packet math,
+//    used by packet lanes of TAN / 3DT / ROT / GED blocks (null when no such model is active).
 struct MpaCache {
   const float* px[3];
   const float* py[3];
   const uint8_t* vip[3];
   int cols, rows;  // W/4, H/4
+  const float* sx;
+  const float* sy;
+  const float* sz;
+  const float* ta;   // TAN alpha
+  const float* tse;  // TAN psin(eps)
+  const float* tce;  // TAN pcos(eps)
 };
+
+// k_sph_cache: GridTerms of grid point t (packet math, as every element of an N % 4 == 0 block)
+MM_HD void sph_cache_thread(int t, const SeqConst& sc, int cols, float* sx, float* sy, float* sz, float* ta, float* tse,
+                            float* tce) {
+  const int j = t / cols, i = t - j * cols;
+  const Math m{1};
+  const V3 p = erp_to_sphere(4.0f * (float)i + sc.off, 4.0f * (float)j + sc.off, sc, m);
+  sx[t] = p.x;
+  sy[t] = p.y;
+  sz[t] = p.z;
+  if (ta) {
+    const V3 sp = cart_to_sph(p, m, true);
+    const float eps = PI_2_F - sp.y;
+    ta[t] = sp.z;
+    tse[t] = m.sin(eps);
+    tce[t] = m.cos(eps);
+  }
+}
+
+// Grid terms of element (row, col) of job j when it is a packet lane and the caches hold them.
+MM_HD void load_grid_terms(const MpaCache& cache, const JobDev& j, int row, int col, bool packet, GridTerms* gt) {
+  gt->have_p = gt->have_tan = 0;
+  if (!packet || !cache.sx) return;
+  const int ci = ((j.y >> 2) + row) * cache.cols + (j.x >> 2) + col;
+  if (j.model == TANGENTIAL) {
+    if (!cache.ta) return;
+    gt->have_tan = 1;
+    gt->alpha = cache.ta[ci];
+    gt->se = cache.tse[ci];
+    gt->ce = cache.tce[ci];
+  } else if (j.model >= THREE_D_TRANSLATIONAL && j.model <= GEODESIC_CAMPOSE) {
+    gt->have_p = 1;
+    gt->p = {cache.sx[ci], cache.sy[ci], cache.sz[ci]};
+  }
+}
 
 struct Geometry {
   int W, H, Wc, Hc;
@@ -125,12 +170,24 @@ MM_HD void mpa_cache_thread(int t, const SeqConst& sc, int plane, int cols, int 
   vip[t] = v ? 1 : 0;
 }
 
+#ifndef MM_REPROJ_ROWMAJOR
+#define MM_REPROJ_ROWMAJOR 1
+#endif
 // The reprojection of one element of a device-planned job, stored in k_mc's record layout.
 MM_HD void reproj_thread_mc(int g, int ji, const SeqConst& sc, const JobDev* jobs, const int* job_offsets,
                             const BlockSetup* setups, const MpaCache& cache, const McIn& mc) {
   const JobDev& j = jobs[ji];
+  // Elements are enumerated row-major over the block (the records k_mc reads and the frame-cache
+  // entries are then contiguous across lanes); Eigen's column-major index still decides packet
+  // vs tail.  pu_cols = cw / sbw for luma and for 4:2:0 chroma alike.
   const int local = g - job_offsets[ji];
+#if MM_REPROJ_ROWMAJOR
+  const int row = local / j.pu_cols, col = local - row * j.pu_cols;
+  const int eig = col * j.rows + row;
+#else
   const int col = local / j.rows, row = local - col * j.rows;
+  const int eig = local;
+#endif
   const float gx = (float)(j.x + 4 * col) + sc.off;
   const float gy = (float)(j.y + 4 * row) + sc.off;
   const bool mpa_cached = (j.comp == 0) && (j.model >= MPA_FRONT_BACK && j.model <= MPA_TOP_BOTTOM);
@@ -143,9 +200,11 @@ MM_HD void reproj_thread_mc(int g, int ji, const SeqConst& sc, const JobDev* job
     py = cache.py[pl][ci];
     vip = cache.vip[pl][ci] != 0;
   }
+  const bool packet = packet_lane(eig, j.n);
+  GridTerms gt;
+  load_grid_terms(cache, j, row, col, packet, &gt);
   int32_t fx, fy;
-  reproject_element(sc, setups[ji], gx, gy, packet_lane(local, j.n), mpa_cached, px, py, vip, j.comp ? 1 : 0, &fx,
-                    &fy);
+  reproject_element(sc, setups[ji], gx, gy, packet, mpa_cached, px, py, vip, j.comp ? 1 : 0, &fx, &fy, &gt);
   // chroma 2x2 sub-block (row, col) belongs to luma 4x4 sub-block (row, col) of the same PU
   const int sb = j.sb_base + row * j.pu_cols + col;
   mm_int2 xy;
@@ -164,11 +223,13 @@ MM_HD void reproj_thread_mc(int g, int ji, const SeqConst& sc, const JobDev* job
   }
 }
 
-MM_HD void setup_thread(int t, const SeqConst& sc, const JobDev* jobs, const M3* ged, BlockSetup* out) {
-  const JobDev j = jobs[t];
+MM_HD void setup_job(const JobDev& j, const SeqConst& sc, const M3* ged, BlockSetup* out) {
   const int cs = j.comp ? 1 : 0;
-  block_setup(&out[t], sc, j.model, j.comp == 0, j.x >> cs, j.y >> cs, j.cw, j.ch, j.mv_hor, j.mv_ver,
+  block_setup(out, sc, j.model, j.comp == 0, j.x >> cs, j.y >> cs, j.cw, j.ch, j.mv_hor, j.mv_ver,
               j.ged_idx >= 0 ? &ged[j.ged_idx] : nullptr);
+}
+MM_HD void setup_thread(int t, const SeqConst& sc, const JobDev* jobs, const M3* ged, BlockSetup* out) {
+  setup_job(jobs[t], sc, ged, &out[t]);
 }
 
 // ji = the job holding flat element g (find_item / wave_find_item)
@@ -220,12 +281,11 @@ MM_HD void store_row(int16_t* d, const int16_t* v, int vec) {
 }
 
 // One luma 4x4 sub-block and its two 4:2:0 chroma 2x2 sub-blocks from the McIn records (device-
-// planned pictures): g's class comes from the bucket bounds (bi, then uni L0, then uni L1).
-MM_HD void mc_thread_rec(int g, int uni_l0_start, int uni_l1_start, const Geometry& geo, const Taps& taps,
-                         const McIn& mc, const RefDev* refs, int16_t* dst_y, int dsy, int16_t* dst_cb,
-                         int16_t* dst_cr, int dsc) {
-  const bool bi = g < uni_l0_start;
-  const int uni_list = g < uni_l1_start ? 0 : 1;
+// planned pictures); cls = 0 bi, 1 uni L0, 2 uni L1 (sb_class of g's PU bucket).
+MM_HD void mc_thread_rec(int g, int cls, const Geometry& geo, const Taps& taps, const McIn& mc, const RefDev* refs,
+                         int16_t* dst_y, int dsy, int16_t* dst_cb, int16_t* dst_cr, int dsc) {
+  const bool bi = cls == 0;
+  const int uni_list = cls == 2 ? 1 : 0;
   const bool used[2] = {bi || uni_list == 0, bi || uni_list == 1};
   mm_int4 L[2];
   mm_int2 C[2];
