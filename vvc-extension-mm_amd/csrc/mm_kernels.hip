@@ -27,14 +27,9 @@
 #include <vector>
 
 #include "../../include/mm360.h"
-#include "mm_mc_lds.h"
 #include "mm_pipeline.h"
 #include "mm_plan.h"
 
-// k_mc_dev stages the quads' reference windows through LDS (mm_mc_lds.h); 0 = per-lane loads
-#ifndef MM_MC_STAGED
-#define MM_MC_STAGED 0
-#endif
 // Packet lanes of TAN / 3DT / ROT / GED read their sphere point from a frame-grid cache
 // (k_sph_cache).  Off by default: the 14-28 MB cache costs more in L2 / Infinity-Cache pressure
 // (k_reproj_dev +5 us, k_mc_dev +6 us at C3) than the 4 packet sin/cos per element it saves.
@@ -283,27 +278,30 @@ __global__ void __launch_bounds__(256) k_reproj_dev(SeqConst sc, const PlanMeta*
   reproj_thread_mc(g, ji, sc, jobs, job_offsets, setups, cache, mc);
 }
 
-#ifdef MM_MC_WAVES_PER_EU
-#define MM_MC_OCC __attribute__((amdgpu_waves_per_eu(MM_MC_WAVES_PER_EU)))
-#else
-#define MM_MC_OCC
+// The tap-pair tables (4 KB) are copied into LDS once per workgroup: every lane indexes them by
+// its own phase, and from __constant__ memory those lookups are ~16 vector loads per wave that
+// compete with the reference-window loads for the texture-address path.
+#ifndef MM_MC_LDS_TAPS
+#define MM_MC_LDS_TAPS 1
 #endif
-__global__ void __launch_bounds__(MM_MC_BLOCK) MM_MC_OCC k_mc_dev(Geometry geo, const PlanMeta* __restrict__ meta, McIn mc,
+__global__ void __launch_bounds__(256) k_mc_dev(Geometry geo, const PlanMeta* __restrict__ meta, McIn mc,
                                                 const PicTables t, int16_t* __restrict__ dst_y, int dsy,
                                                 int16_t* __restrict__ dst_cb, int16_t* __restrict__ dst_cr, int dsc) {
   const int g = xcd_block() * blockDim.x + threadIdx.x;
   const int n_sb = meta->n_sb;
-  const Taps taps{c_luma_taps, c_chroma_taps, &c_packed_taps};
-#if MM_MC_STAGED
-  __shared__ uint32_t s_slab[mmlds::MC_BLOCK / 64][mmlds::WAVE_SLAB_DW];  // one slab per wave
-  if (g - (int)__lane_id() >= n_sb) return;  // whole wave past the end
-  const bool valid = g < n_sb;
-  mmlds::mc_thread_lds(g, valid, valid ? sb_class(g, meta->sb_base) : 0, geo, taps, mc, t.ref, dst_y, dsy, dst_cb,
-                       dst_cr, dsc, s_slab[threadIdx.x >> 6]);
+#if MM_MC_LDS_TAPS
+  __shared__ PackedTaps s_taps;
+  static_assert(sizeof(PackedTaps) % 16 == 0 && sizeof(PackedTaps) / 16 <= 256, "one 16-byte word per thread");
+  if (g - (int)threadIdx.x >= n_sb) return;  // whole workgroup past the end
+  if (threadIdx.x < sizeof(PackedTaps) / 16)
+    reinterpret_cast<uint4*>(&s_taps)[threadIdx.x] = reinterpret_cast<const uint4*>(&c_packed_taps)[threadIdx.x];
+  __syncthreads();
+  const Taps taps{c_luma_taps, c_chroma_taps, &s_taps};
 #else
+  const Taps taps{c_luma_taps, c_chroma_taps, &c_packed_taps};
+#endif
   if (g >= n_sb) return;
   mc_thread_rec(g, sb_class(g, meta->sb_base), geo, taps, mc, t.ref, dst_y, dsy, dst_cb, dst_cr, dsc);
-#endif
 }
 
 // --------------------------------------------------------------------------------------------
@@ -842,7 +840,7 @@ static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, in
   const int gp = (n + PLAN_BLOCK - 1) / PLAN_BLOCK;
   const int gs = (k.jobs + 255) / 256;
   const int gr = round_grid((k.elems + 255) / 256);
-  const int gm = round_grid((k.sb + mmlds::MC_BLOCK - 1) / mmlds::MC_BLOCK);
+  const int gm = round_grid((k.sb + 255) / 256);
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
   PlanCounters* cnt = c->d_cnt.p + c->cnt_par;
   PlanCounters* next = c->d_cnt.p + (c->cnt_par ^ 1);
@@ -861,7 +859,7 @@ static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, in
   hipLaunchKernelGGL(k_reproj_dev, dim3(gr), dim3(256), 0, c->stream, c->sc, c->d_meta.p, c->d_jobs.p,
                      c->d_job_off.p, c->d_job_chunk.p, c->d_setup.p, make_cache(c), mc);
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[2], c->stream));
-  hipLaunchKernelGGL(k_mc_dev, dim3(gm), dim3(mmlds::MC_BLOCK), 0, c->stream, geo, c->d_meta.p, mc, t, dy, (int)sdy, dcb, dcr,
+  hipLaunchKernelGGL(k_mc_dev, dim3(gm), dim3(256), 0, c->stream, geo, c->d_meta.p, mc, t, dy, (int)sdy, dcb, dcr,
                      (int)sdc);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipEventRecord(c->ev1, c->stream));
