@@ -45,6 +45,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="length of the CPU baseline sample")
     ap.add_argument("--kernel-steps", type=int, default=10, help="extra steps timed per launch with HIP events")
     ap.add_argument("--lib", default=None, help="alternative build of libmm360.so (A/B experiments)")
+    ap.add_argument("--stripes", type=int, default=None, help="mm_set_stripes (default: the library's)")
     ap.add_argument("--coherent-mv", action="store_true",
                     help="experiment: one MV for every PU and list (spatially coherent motion)")
     ap.add_argument("--uniform-model", type=int, default=None,
@@ -78,6 +79,8 @@ def main():
 
     ctx = mm360.MMContext(params, device=local)
     ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    if args.stripes:
+        ctx.set_stripes(args.stripes)
     ctx.set_epipole(W.CUR_POC, -1, W.GED_EPIPOLE_Q24)
     for poc in W.REF_POCS:
         y, cb, cr = W.ref_planes(cfg.width, cfg.height, poc)

@@ -220,6 +220,14 @@ int mm_last_timing(mm_ctx* ctx, float* ms_total);
 int mm_set_stage_timing(mm_ctx* ctx, int on);
 int mm_last_stage_timing(mm_ctx* ctx, float ms[4]);
 
+/* Stripe pipelining of mm_pred_device / mm_pred_run (default 1, 1..64): the PU list is cut into
+ * `stripes` contiguous ranges that are planned and predicted independently, alternating between
+ * the context stream and an internal auxiliary stream that forks from and joins back into it, so
+ * that one stripe's latency-bound planning kernels overlap another stripe's interpolation.  PUs
+ * write disjoint samples: results do not depend on the setting.  Stage timing forces one stripe.
+ * (No reference counterpart: the reference predicts PU by PU.) */
+int mm_set_stripes(mm_ctx* ctx, int stripes);
+
 #ifdef __cplusplus
 }
 #endif

@@ -102,17 +102,19 @@ __device__ __forceinline__ int xcd_block() {
   return grp * (8 * XCD_RUN) + (r & 7) * XCD_RUN + (r >> 3);
 }
 
-// Planning blocks are 1024 threads wide: each block ends with one global atomic per bucket, and
-// those land on the same ~70 addresses from every block, so fewer, wider blocks cut the
-// serialised memory-side atomics per address 4x.
+// Planning runs in 1024-thread blocks without global atomics: k_plan_count writes each block's
+// bucket counts to its own row of `blk`; every k_plan_place block sums the column of each bucket
+// (the bucket total) and the part of it above its own row (its offset inside the bucket).  PUs
+// therefore land in their buckets in input order, block by block.
 constexpr int PLAN_BLOCK = 1024;
+constexpr int N_KEYS = N_PU_KEYS + N_JOB_KEYS;  // one row of `blk`: PU buckets, then job buckets
 
-__global__ void __launch_bounds__(PLAN_BLOCK) k_plan_count(const mm_pu_desc* __restrict__ pus, int n, const PicTables t,
-                                                    PlanCounters* __restrict__ cnt) {
-  __shared__ unsigned long long s_pu[N_PU_KEYS], s_job[N_JOB_KEYS], s_status;
+__global__ void __launch_bounds__(PLAN_BLOCK) k_plan_count(const mm_pu_desc* __restrict__ pus, int n, int pu_base,
+                                                    const PicTables t, PlanCounters* __restrict__ cnt,
+                                                    unsigned long long* __restrict__ blk) {
+  __shared__ unsigned long long s_cnt[N_KEYS], s_status;
   const int tid = threadIdx.x;
-  if (tid < N_PU_KEYS) s_pu[tid] = 0;
-  if (tid < N_JOB_KEYS) s_job[tid] = 0;
+  if (tid < N_KEYS) s_cnt[tid] = 0;
   if (tid == 0) s_status = 0;
   __syncthreads();
   const int i = blockIdx.x * blockDim.x + tid;
@@ -121,24 +123,24 @@ __global__ void __launch_bounds__(PLAN_BLOCK) k_plan_count(const mm_pu_desc* __r
     PuPlan p;
     classify_pu(u, t, &p);
     if (p.code != MM_OK) {
-      atomicMax(&s_status, status_word(i, p.code));
+      atomicMax(&s_status, status_word(pu_base + i, p.code));
     } else {
-      atomicAdd(&s_pu[p.key], pack_count(1, p.n_sb));
+      atomicAdd(&s_cnt[p.key], pack_count(1, p.n_sb));
 #pragma unroll
       for (int k = 0; k < 4; k++)
-        if (p.job[k].valid) atomicAdd(&s_job[p.job[k].key], pack_count(1, p.job[k].n));
+        if (p.job[k].valid) atomicAdd(&s_cnt[N_PU_KEYS + p.job[k].key], pack_count(1, p.job[k].n));
     }
   }
   __syncthreads();
-  if (tid < N_PU_KEYS && s_pu[tid]) atomicAdd(&cnt->pu_tot[tid], s_pu[tid]);
-  if (tid < N_JOB_KEYS && s_job[tid]) atomicAdd(&cnt->job_tot[tid], s_job[tid]);
+  if (tid < N_KEYS) blk[(long)blockIdx.x * N_KEYS + tid] = s_cnt[tid];
   if (tid == 0 && s_status) atomicMax(&cnt->status, s_status);
 }
 
-// `next` is the other counter set of the ping-pong pair: block 0 zeroes it for the next picture, so
-// no memset launch precedes k_plan_count.
+// `next` is the other counter set of the ping-pong pair: block 0 zeroes its status word for the
+// next picture, so no memset launch precedes k_plan_count.
 __global__ void __launch_bounds__(PLAN_BLOCK) k_plan_place(const mm_pu_desc* __restrict__ pus, int n, const PicTables t,
                                                     PlanCounters* __restrict__ cnt, PlanCounters* __restrict__ next,
+                                                    const unsigned long long* __restrict__ blk, int n_blocks,
                                                     PlanMeta* __restrict__ meta,
                                                     PlanCaps caps, PuDev* __restrict__ d_pus, int* __restrict__ pu_off,
                                                     int* __restrict__ pu_chunk, JobDev* __restrict__ jobs,
@@ -148,19 +150,53 @@ __global__ void __launch_bounds__(PLAN_BLOCK) k_plan_place(const mm_pu_desc* __r
   __shared__ PlanMeta s_meta;
   __shared__ int s_ok;
   const int tid = threadIdx.x;
-  if (blockIdx.x == 0) {
-    constexpr int NW = (int)(sizeof(PlanCounters) / sizeof(unsigned long long));
-    static_assert(NW <= PLAN_BLOCK, "one thread per counter word");
-    if (tid < NW) reinterpret_cast<unsigned long long*>(next)[tid] = 0ull;
-  }
+  if (blockIdx.x == 0 && tid == 0) next->status = 0ull;
   if (tid < N_PU_KEYS) s_pu[tid] = 0;
   if (tid < N_JOB_KEYS) s_job[tid] = 0;
-  // PlanMeta = exclusive prefix of the bucket totals: wave 0 loads all 64 job totals at once and
-  // scans them across lanes (a serial loop of dependent loads would cost every block ~70 memory
-  // latencies)
+  // bucket totals and this block's offsets inside the buckets: the column sums of blk, split over
+  // the block's 16 waves (wave w takes rows w, w + 16, ...) so that every thread has only a few
+  // independent loads in flight, then combined through LDS
+  constexpr int NWAVE = PLAN_BLOCK / 64;
+  __shared__ unsigned long long s_ptot[NWAVE][N_KEYS], s_ppre[NWAVE][N_KEYS];
+  {
+    const int lane = tid & 63, w = tid >> 6, b0 = blockIdx.x;
+#pragma unroll
+    for (int kc = 0; kc < N_KEYS; kc += 64) {
+      const int key = kc + lane;
+      if (key < N_KEYS) {
+        unsigned long long tp = 0, pp = 0;
+        for (int b = w; b < n_blocks; b += NWAVE) {
+          const unsigned long long v = blk[(long)b * N_KEYS + key];
+          tp += v;
+          if (b < b0) pp += v;
+        }
+        s_ptot[w][key] = tp;
+        s_ppre[w][key] = pp;
+      }
+    }
+  }
+  __syncthreads();
+  unsigned long long tot = 0, pre = 0;
+  if (tid < N_KEYS) {
+#pragma unroll
+    for (int w = 0; w < NWAVE; w++) {
+      tot += s_ptot[w][tid];
+      pre += s_ppre[w][tid];
+    }
+    if (tid < N_PU_KEYS)
+      g_pu[tid] = pre;
+    else
+      g_job[tid - N_PU_KEYS] = pre;
+  }
+  // PlanMeta = exclusive prefix of the bucket totals: the job buckets are one wave (lanes 6..69
+  // are threads N_PU_KEYS..N_KEYS-1, scanned in two waves' halves through LDS), the PU buckets
+  // are few
+  __shared__ unsigned long long s_tot[N_KEYS];
+  if (tid < N_KEYS) s_tot[tid] = tot;
+  __syncthreads();
   static_assert(N_JOB_KEYS == 64, "one lane per job bucket");
   if (tid < 64) {
-    const unsigned long long v = cnt->job_tot[tid];
+    const unsigned long long v = s_tot[N_PU_KEYS + tid];
     const int items = packed_items(v), elems = packed_elems(v);
     int si = items, se = elems;
 #pragma unroll
@@ -178,16 +214,13 @@ __global__ void __launch_bounds__(PLAN_BLOCK) k_plan_place(const mm_pu_desc* __r
       s_meta.n_elems = se;
     }
     if (tid == 0) {
-      unsigned long long pt[N_PU_KEYS];
-#pragma unroll
-      for (int k = 0; k < N_PU_KEYS; k++) pt[k] = cnt->pu_tot[k];
       int acc = 0, sacc = 0;
 #pragma unroll
       for (int k = 0; k < N_PU_KEYS; k++) {
         s_meta.pu_base[k] = acc;
         s_meta.sb_base[k] = sacc;
-        acc += packed_items(pt[k]);
-        sacc += packed_elems(pt[k]);
+        acc += packed_items(s_tot[k]);
+        sacc += packed_elems(s_tot[k]);
       }
       s_meta.n_pus = acc;
       s_meta.n_sb = sacc;
@@ -223,10 +256,6 @@ __global__ void __launch_bounds__(PLAN_BLOCK) k_plan_place(const mm_pu_desc* __r
         if (p.job[k].valid) lj[k] = atomicAdd(&s_job[p.job[k].key], pack_count(1, p.job[k].n));
     }
   }
-  __syncthreads();
-  if (tid < N_PU_KEYS && s_pu[tid]) g_pu[tid] = atomicAdd(&cnt->pu_cur[tid], s_pu[tid]);
-  if (tid < N_JOB_KEYS && s_job[tid]) g_job[tid] = atomicAdd(&cnt->job_cur[tid], s_job[tid]);
-  __syncthreads();
   if (p.code != MM_OK) return;
   const unsigned long long bp = g_pu[p.key] + lp;
   const int pu_idx = s_meta.pu_base[p.key] + packed_items(bp);
@@ -467,6 +496,42 @@ struct DevBuf {
   }
 };
 
+// Buffers of one device-planned stripe of a picture.
+struct PlanSlot {
+  DevBuf<PuDev> pus;
+  DevBuf<int> pu_off, pu_chunk, job_off, job_chunk;
+  DevBuf<JobDev> jobs;
+  DevBuf<BlockSetup> setup;
+  DevBuf<PlanCounters> cnt;  // ping-pong pair: a stripe reports in cnt[par] and zeroes the other's status
+  int cnt_par = 0;
+  DevBuf<unsigned long long> blk;  // per-planning-block bucket counts (k_plan_count rows)
+  DevBuf<PlanMeta> meta;
+  DevBuf<mm_int4> mc_lum[2];
+  DevBuf<mm_int2> mc_chr[2];
+  PlanCaps caps{};
+  void release() {
+    pus.release();
+    pu_off.release();
+    pu_chunk.release();
+    job_off.release();
+    job_chunk.release();
+    jobs.release();
+    setup.release();
+    cnt.release();
+    blk.release();
+    meta.release();
+    for (int l = 0; l < 2; l++) {
+      mc_lum[l].release();
+      mc_chr[l].release();
+    }
+  }
+};
+
+// Stripes a device-planned picture is cut into (mm_set_stripes)
+#ifndef MM_DEFAULT_STRIPES
+#define MM_DEFAULT_STRIPES 1
+#endif
+
 struct mm_ctx {
   mm_seq_params prm{};
   SeqConst sc{};
@@ -490,13 +555,11 @@ struct mm_ctx {
   DevBuf<M3> d_ged;
   // device-planned prediction (mm_pred_device / mm_pred_run)
   DevBuf<mm_pu_desc> d_pu_in;  // PU list copied in by mm_pred / mm_pred_prepare
-  DevBuf<PlanCounters> d_cnt;  // ping-pong pair: a picture counts in d_cnt[cnt_par] and zeroes the other
-  int cnt_par = 0;
-  PlanCounters* last_cnt = nullptr;  // counters of the last device-planned picture (status word)
-  DevBuf<PlanMeta> d_meta;
-  DevBuf<mm_int4> d_mc_lum[2];
-  DevBuf<mm_int2> d_mc_chr[2];
-  PlanCaps caps{};
+  PlanSlot slot[2];             // device-planned stripes alternate between the two buffer sets
+  hipStream_t aux = nullptr;    // odd stripes run here, overlapping the even stripes' kernels
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  int n_stripes = MM_DEFAULT_STRIPES;
+  std::vector<std::pair<PlanCounters*, int>> last_status;  // status words of the last picture's stripes
   int prep_poc = 0, prep_n = 0;
   bool prepared = false;
   bool status_pending = false;
@@ -622,7 +685,10 @@ int mm_create(const mm_seq_params* p, int device, mm_ctx** out_ctx) {
   c->geo.vec_store = 0;
   if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
       hipEventCreate(&c->ev_stage[0]) != hipSuccess || hipEventCreate(&c->ev_stage[1]) != hipSuccess ||
-      hipEventCreate(&c->ev_stage[2]) != hipSuccess) {
+      hipEventCreate(&c->ev_stage[2]) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess) {
     mm_destroy(c);
     return MM_ERR_HIP;
   }
@@ -687,12 +753,7 @@ int mm_destroy(mm_ctx* c) {
   c->d_reproj.release();
   c->d_pus.release();
   c->d_pu_in.release();
-  for (int l = 0; l < 2; l++) {
-    c->d_mc_lum[l].release();
-    c->d_mc_chr[l].release();
-  }
-  c->d_cnt.release();
-  c->d_meta.release();
+  for (int k = 0; k < 2; k++) c->slot[k].release();
   c->d_ged.release();
   for (auto& kv : c->orgs) (void)hipFree(kv.second.y);
   c->d_me_blocks.release();
@@ -709,6 +770,12 @@ int mm_destroy(mm_ctx* c) {
   c->d_me_chunk.release();
   for (auto& e : c->ev_stage)
     if (e) (void)hipEventDestroy(e);
+  if (c->aux) {
+    (void)hipStreamSynchronize(c->aux);
+    (void)hipStreamDestroy(c->aux);
+  }
+  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   delete c;
@@ -789,40 +856,78 @@ int mm_reproject(mm_ctx* c, const mm_block_desc* blocks, int n, int32_t* out_xy)
 
 static int round_grid(long v) { return (int)((v + 8 * XCD_RUN - 1) / (8 * XCD_RUN) * (8 * XCD_RUN)); }
 
-// Buffers for a PU list of n entries: a PU list predicts each luma sample of the picture at most
+// Buffers for a stripe of n PUs: a PU list predicts each luma sample of the picture at most
 // once, so sub-blocks are bounded by the picture's sub-block count (and by n * 1024, 128x128
 // PUs); a PU has at most 4 jobs and 4 reprojection elements per luma sub-block (2 lists x
 // {luma, chroma}).  k_plan_place refuses a list beyond these capacities (overlapping PUs).
-static int ensure_plan_buffers(mm_ctx* c, int n) {
+static int ensure_slot_buffers(mm_ctx* c, PlanSlot& S, int n) {
   PlanCaps k;
   k.pus = n;
   k.jobs = 4 * n;
   const long area_sb = (long)(c->geo.W / 4) * (c->geo.H / 4);
   k.sb = (int)std::min<long>((long)n * 1024, area_sb);
   k.elems = 4 * k.sb;
-  c->caps = k;
-  HIPCHK(c, c->d_pus.ensure(k.pus));
-  HIPCHK(c, c->d_pu_off.ensure(k.pus));
-  HIPCHK(c, c->d_pu_chunk.ensure(k.sb / 64 + 1));
-  HIPCHK(c, c->d_jobs.ensure(k.jobs));
-  HIPCHK(c, c->d_job_off.ensure(k.jobs));
-  HIPCHK(c, c->d_job_chunk.ensure(k.elems / 64 + 1));
-  HIPCHK(c, c->d_setup.ensure(k.jobs));
-  HIPCHK(c, c->d_reproj.ensure(2 * (size_t)k.elems));
-  if (!c->d_cnt.p) {
-    HIPCHK(c, c->d_cnt.ensure(2));
-    HIPCHK(c, hipMemsetAsync(c->d_cnt.p, 0, 2 * sizeof(PlanCounters), c->stream));  // once per context
+  S.caps = k;
+  HIPCHK(c, S.pus.ensure(k.pus));
+  HIPCHK(c, S.pu_off.ensure(k.pus));
+  HIPCHK(c, S.pu_chunk.ensure(k.sb / 64 + 1));
+  HIPCHK(c, S.jobs.ensure(k.jobs));
+  HIPCHK(c, S.job_off.ensure(k.jobs));
+  HIPCHK(c, S.job_chunk.ensure(k.elems / 64 + 1));
+  HIPCHK(c, S.setup.ensure(k.jobs));
+  if (!S.cnt.p) {
+    HIPCHK(c, S.cnt.ensure(2));
+    HIPCHK(c, hipMemsetAsync(S.cnt.p, 0, 2 * sizeof(PlanCounters), c->stream));  // once per context
+    HIPCHK(c, hipStreamSynchronize(c->stream));
   }
-  HIPCHK(c, c->d_meta.ensure(1));
+  HIPCHK(c, S.meta.ensure(1));
+  HIPCHK(c, S.blk.ensure((size_t)((n + PLAN_BLOCK - 1) / PLAN_BLOCK) * N_KEYS));
   for (int l = 0; l < 2; l++) {
-    HIPCHK(c, c->d_mc_lum[l].ensure(k.sb));
-    HIPCHK(c, c->d_mc_chr[l].ensure(k.sb));
+    HIPCHK(c, S.mc_lum[l].ensure(k.sb));
+    HIPCHK(c, S.mc_chr[l].ensure(k.sb));
   }
   return MM_OK;
 }
 
-// One picture: memset + k_plan_count + k_plan_place + k_setup_dev + k_reproj_dev + k_mc_dev on
-// the context stream, bracketed by ev0/ev1.  Validation errors are deferred to mm_pred_status.
+// One stripe (PUs [base, base + n) of the picture's list) through k_plan_count + k_plan_place +
+// k_setup_dev + k_reproj_dev + k_mc_dev on `st`.  Stage events only in single-stripe timing mode.
+static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables& t, const Geometry& geo,
+                         const mm_pu_desc* d_in, int n, int base, int16_t* dy, ptrdiff_t sdy, int16_t* dcb,
+                         int16_t* dcr, ptrdiff_t sdc) {
+  const PlanCaps& k = S.caps;
+  const int gp = (n + PLAN_BLOCK - 1) / PLAN_BLOCK;
+  const int gs = (k.jobs + 255) / 256;
+  const int gr = round_grid((k.elems + 255) / 256);
+  const int gm = round_grid((k.sb + 255) / 256);
+  PlanCounters* cnt = S.cnt.p + S.cnt_par;
+  PlanCounters* next = S.cnt.p + (S.cnt_par ^ 1);
+  hipLaunchKernelGGL(k_plan_count, dim3(gp), dim3(PLAN_BLOCK), 0, st, d_in, n, base, t, cnt, S.blk.p);
+  hipLaunchKernelGGL(k_plan_place, dim3(gp), dim3(PLAN_BLOCK), 0, st, d_in, n, t, cnt, next, S.blk.p, gp, S.meta.p, k,
+                     S.pus.p, S.pu_off.p, S.pu_chunk.p, S.jobs.p, S.job_off.p, S.job_chunk.p);
+  if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[0], st));
+  hipLaunchKernelGGL(k_setup_dev, dim3(gs), dim3(256), 0, st, c->sc, S.meta.p, S.jobs.p, t, S.setup.p);
+  if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[1], st));
+  McIn mc;
+  for (int l = 0; l < 2; l++) {
+    mc.lum[l] = S.mc_lum[l].p;
+    mc.chr[l] = S.mc_chr[l].p;
+  }
+  hipLaunchKernelGGL(k_reproj_dev, dim3(gr), dim3(256), 0, st, c->sc, S.meta.p, S.jobs.p, S.job_off.p, S.job_chunk.p,
+                     S.setup.p, make_cache(c), mc);
+  if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[2], st));
+  hipLaunchKernelGGL(k_mc_dev, dim3(gm), dim3(256), 0, st, geo, S.meta.p, mc, t, dy, (int)sdy, dcb, dcr, (int)sdc);
+  HIPCHK(c, hipGetLastError());
+  c->last_status.emplace_back(cnt, base);
+  S.cnt_par ^= 1;
+  return MM_OK;
+}
+
+// One picture, bracketed by ev0/ev1 on the context stream.  The PU list (raster CTU order) is cut
+// into n_stripes contiguous stripes; even stripes run on the context stream with slot 0, odd ones
+// on the auxiliary stream with slot 1, so one stripe's latency-bound planning kernels overlap the
+// other's interpolation.  PUs write disjoint samples, so stripes are independent; the auxiliary
+// stream forks from and joins back into the context stream.  Validation errors are deferred to
+// mm_pred_status.
 static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, int n, int16_t* dy, ptrdiff_t sdy,
                               int16_t* dcb, int16_t* dcr, ptrdiff_t sdc) {
   std::vector<std::pair<int, RefDev>> refs;
@@ -832,40 +937,36 @@ static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, in
   std::string err;
   int rc = build_pic_tables(seq_info(c->prm), c->epipoles, cur_poc, refs, &t, &err);
   if (rc) return fail(c, rc, err);
-  RCCHK(ensure_plan_buffers(c, n));
   Geometry geo = c->geo;
   geo.vec_store = ((uintptr_t)dy % 8 == 0) && (sdy % 4 == 0) &&
                   (!geo.chroma || ((uintptr_t)dcb % 4 == 0 && (uintptr_t)dcr % 4 == 0 && sdc % 2 == 0));
-  const PlanCaps& k = c->caps;
-  const int gp = (n + PLAN_BLOCK - 1) / PLAN_BLOCK;
-  const int gs = (k.jobs + 255) / 256;
-  const int gr = round_grid((k.elems + 255) / 256);
-  const int gm = round_grid((k.sb + 255) / 256);
+  const int K = c->stage_timing ? 1 : std::max(1, std::min(c->n_stripes, (n + PLAN_BLOCK - 1) / PLAN_BLOCK));
+  const int per = (n + K - 1) / K;
+  for (int s = 0; s < std::min(K, 2); s++) RCCHK(ensure_slot_buffers(c, c->slot[s], per));
+  c->last_status.clear();
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-  PlanCounters* cnt = c->d_cnt.p + c->cnt_par;
-  PlanCounters* next = c->d_cnt.p + (c->cnt_par ^ 1);
-  hipLaunchKernelGGL(k_plan_count, dim3(gp), dim3(PLAN_BLOCK), 0, c->stream, d_in, n, t, cnt);
-  hipLaunchKernelGGL(k_plan_place, dim3(gp), dim3(PLAN_BLOCK), 0, c->stream, d_in, n, t, cnt, next, c->d_meta.p, k,
-                     c->d_pus.p, c->d_pu_off.p, c->d_pu_chunk.p, c->d_jobs.p, c->d_job_off.p, c->d_job_chunk.p);
-  if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[0], c->stream));
-  hipLaunchKernelGGL(k_setup_dev, dim3(gs), dim3(256), 0, c->stream, c->sc, c->d_meta.p, c->d_jobs.p, t,
-                     c->d_setup.p);
-  if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[1], c->stream));
-  McIn mc;
-  for (int l = 0; l < 2; l++) {
-    mc.lum[l] = c->d_mc_lum[l].p;
-    mc.chr[l] = c->d_mc_chr[l].p;
+  if (K > 1) {
+    HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_fork, 0));
   }
-  hipLaunchKernelGGL(k_reproj_dev, dim3(gr), dim3(256), 0, c->stream, c->sc, c->d_meta.p, c->d_jobs.p,
-                     c->d_job_off.p, c->d_job_chunk.p, c->d_setup.p, make_cache(c), mc);
-  if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[2], c->stream));
-  hipLaunchKernelGGL(k_mc_dev, dim3(gm), dim3(256), 0, c->stream, geo, c->d_meta.p, mc, t, dy, (int)sdy, dcb, dcr,
-                     (int)sdc);
-  HIPCHK(c, hipGetLastError());
+  for (int s = 0; s < K; s++) {
+    const int base = s * per, m = std::min(per, n - base);
+    if (m <= 0) break;
+    RCCHK(launch_stripe(c, c->slot[s & 1], (s & 1) ? c->aux : c->stream, t, geo, d_in + base, m, base, dy, sdy, dcb,
+                        dcr, sdc));
+  }
+  if (K > 1) {
+    HIPCHK(c, hipEventRecord(c->ev_join, c->aux));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
+  }
   HIPCHK(c, hipEventRecord(c->ev1, c->stream));
-  c->last_cnt = cnt;
-  c->cnt_par ^= 1;
   c->status_pending = true;
+  return MM_OK;
+}
+
+int mm_set_stripes(mm_ctx* c, int stripes) {
+  if (!c || stripes < 1 || stripes > 64) return MM_ERR_ARG;
+  c->n_stripes = stripes;
   return MM_OK;
 }
 
@@ -875,8 +976,12 @@ static int read_status(mm_ctx* c, int* first_bad) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (!c->status_pending) return MM_OK;
   c->status_pending = false;
-  unsigned long long w = 0;
-  HIPCHK(c, hipMemcpy(&w, &c->last_cnt->status, sizeof(w), hipMemcpyDeviceToHost));
+  unsigned long long w = 0;  // the stripes' status words combine like the per-PU atomicMax
+  for (const auto& st : c->last_status) {
+    unsigned long long v = 0;
+    HIPCHK(c, hipMemcpy(&v, &st.first->status, sizeof(v), hipMemcpyDeviceToHost));
+    w = std::max(w, v);
+  }
   if (!w) return MM_OK;
   const unsigned long long v = ~w;
   const int code = (int)(v & 0xff), pu = (int)(v >> 8);

@@ -50,6 +50,7 @@ EXPORTED_SYMBOLS = (
     "mm_set_epipole", "mm_upload_ref", "mm_release_ref", "mm_reproject", "mm_pred",
     "mm_pred_device", "mm_pred_status", "mm_pred_prepare", "mm_pred_run", "mm_filter", "mm_last_timing",
     "mm_set_stage_timing", "mm_last_stage_timing", "mm_upload_org", "mm_sad_window", "mm_pred_dmvr", "mm_mvp_convert",
+    "mm_set_stripes",
 )
 
 
@@ -139,6 +140,7 @@ def load_library() -> ctypes.CDLL:
         "mm_pred_dmvr": (c_int, [vp, c_int, vp, c_int, vp, ctypes.c_ssize_t, vp, vp, ctypes.c_ssize_t, vp]),
         "mm_sad_window": (c_int, [vp, c_int, vp, c_int, c_int, c_int, vp]),
         "mm_last_stage_timing": (c_int, [vp, POINTER(c_float)]),
+        "mm_set_stripes": (c_int, [vp, c_int]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -320,6 +322,10 @@ class MMContext:
 
     def set_stage_timing(self, on: bool):
         self._check(self.lib.mm_set_stage_timing(self.h, int(on)))
+
+    def set_stripes(self, stripes: int):
+        """Stripe pipelining of the device-planned path (mm_set_stripes)."""
+        self._check(self.lib.mm_set_stripes(self.h, int(stripes)))
 
     def last_stage_timing_ms(self):
         """(planning, k_setup, k_reproj, k_mc) device milliseconds of the last launch sequence."""
