@@ -35,6 +35,19 @@ from mm360 import workload as W  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
 
+def measured_traffic(args):
+    """HBM bytes per k_mc_dev launch from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes
+    (profiles/r01_traffic.json, tools/traffic_json.py), only when that profile was taken with
+    this very library (sha256) and the C3 workload; else None."""
+    import hashlib
+    path = os.path.join(ROOT, "profiles", "r01_traffic.json")
+    if args.config != "C3" or args.uniform_model is not None or args.coherent_mv or not os.path.exists(path):
+        return None
+    d = json.load(open(path))
+    sha = hashlib.sha256(open(mm360.LIB_PATH, "rb").read()).hexdigest()
+    return d["traffic_bytes_per_launch"] if d.get("lib_sha256") == sha else None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -170,7 +183,7 @@ def main():
                        "pus": int(len(pus)), "luma_area": int(area), "models": [mm360.MODEL_NAMES[m] for m in cfg.models],
                        "parallelism": f"replicas x{world} (one picture per GPU)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": measured_traffic(args),
                          "kernel": "k_mc_dev", "kernel_ms": round(kernel_ms, 4),
                          "algorithmic_bytes": int(alg_bytes)},
             "stages_ms": {"plan": round(float(st[0]), 4), "setup": round(float(st[1]), 4),

@@ -232,6 +232,35 @@ def test_pred_device_resident_list_vs_oracle(cfg_name):
         assert np.array_equal(got, x), describe_mismatch(name, got, x)
 
 
+def test_pred_stripes_do_not_change_results():
+    """mm_set_stripes: the PU list cut into 1..7 stripes over two streams predicts the same picture
+    (== the oracle), and the lowest failing PU is still reported across stripes."""
+    cfg = W.CONFIGS["C2"]
+    params = mm360.seq_params(cfg.width, cfg.height, cfg.models)
+    pus = W.pu_list(cfg, frame=7)
+    refs = {poc: W.ref_planes(cfg.width, cfg.height, poc) for poc in W.REF_POCS}
+    want = Oracle(params, EPI).predict(W.CUR_POC, pus, refs, cfg.width, cfg.height)
+    bad = pus.copy()
+    k_bad = len(pus) - 5  # lands in the last stripe
+    bad[k_bad]["x"] = 2
+    with _ctx(params) as ctx:
+        for poc, (y, cb, cr) in refs.items():
+            ctx.upload_ref(poc, torch.from_numpy(y).cuda(), torch.from_numpy(cb).cuda(), torch.from_numpy(cr).cuda())
+        d_pus = mm360.pus_to_device(pus)
+        for stripes in (1, 2, 3, 7):
+            ctx.set_stripes(stripes)
+            dst = _planes(cfg, -3)
+            ctx.predict_device(W.CUR_POC, d_pus, *dst)
+            assert ctx.status() == (mm360.MM_OK, -1)
+            for x, t, name in zip(want, dst, ("y", "cb", "cr")):
+                got = t.cpu().numpy()
+                assert np.array_equal(got, x), (stripes, describe_mismatch(name, got, x))
+            ctx.predict_device(W.CUR_POC, mm360.pus_to_device(bad), *_planes(cfg))
+            assert ctx.status() == (mm360.MM_ERR_ARG, k_bad), stripes
+        with pytest.raises(mm360.MMError):
+            ctx.set_stripes(0)
+
+
 def test_device_validation_reports_lowest_failing_pu():
     """Device-side CHECKs: a bad PU is skipped and reported (lowest index first); the rest of the
     picture is still predicted exactly."""
