@@ -19,20 +19,24 @@ struct RefDev {
 };
 
 // One reprojection job == one reprojectMotionVectorSubblocks call
-struct JobDev {
+// 64 bytes, 16-byte aligned: written and read as four 16-byte words (k_plan_place, k_reproj*)
+struct alignas(16) JobDev {
   int x, y;    // block position in LUMA units (grid origin)
   int cw, ch;  // block size in component units
-  int comp;    // 0 luma, 1 chroma (4:2:0)
-  int model;
   int mv_hor, mv_ver;
-  int ged_idx;  // index into the GED rotation table (-1 if not GED)
   int n;        // elements = (cw/sbw)*(ch/sbh)
   int rows;     // ch/sbh (Eigen column-major rows)
   int offset;   // first element in the result array
   // device-planned prediction: where k_mc finds this job's results (McIn, one record per luma
   // 4x4 sub-block of the PU, row-major from sb_base)
-  int sb_base, pu_cols, list, slot, alias;  // alias: MPA chroma == luma, fill both records
+  int sb_base, pu_cols;
+  int16_t model;
+  int16_t ged_idx;  // index into the GED rotation table (-1 if not GED)
+  int8_t comp;      // 0 luma, 1 chroma (4:2:0)
+  int8_t list, slot;
+  int8_t alias;     // MPA chroma == luma, fill both records
 };
+static_assert(sizeof(JobDev) == 64, "JobDev is four 16-byte words");
 
 // Per-luma-sub-block inputs of k_mc, written by the reprojection of a device-planned picture so
 // that k_mc reads them with one coalesced load per list instead of chasing PU -> job -> result:
@@ -49,7 +53,7 @@ struct McIn {
   mm_int2* chr[2];
 };
 
-struct PuDev {
+struct alignas(16) PuDev {  // 48 bytes: three 16-byte words
   int x, y, w, h;
   int ref_slot[2];  // -1 = list unused
   int job[2][2];    // [list][comp] -> job index

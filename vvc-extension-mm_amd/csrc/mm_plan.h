@@ -120,8 +120,10 @@ class Planner {
     j.mv_ver = mvv;
     j.ged_idx = -1;
     if (is_ged(model)) {
-      int rc = ged_index(model, cur, ref, &j.ged_idx);
+      int gi = -1;
+      int rc = ged_index(model, cur, ref, &gi);
       if (rc) return rc;
+      j.ged_idx = (int16_t)gi;
     }
     const int sb = comp ? 2 : 4;
     j.rows = ch / sb;
