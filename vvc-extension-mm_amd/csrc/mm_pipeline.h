@@ -186,7 +186,14 @@ MM_HD void reproj_thread_mc(int g, int ji, const SeqConst& sc, const JobDev* job
   // vs tail.  pu_cols = cw / sbw for luma and for 4:2:0 chroma alike.
   const int local = g - job_offsets[ji];
 #if MM_REPROJ_ROWMAJOR
-  const int row = local / j.pu_cols, col = local - row * j.pu_cols;
+  // VVC block widths are powers of two: a shift instead of the ~20-instruction integer division
+  const int pc = j.pu_cols;
+  int row;
+  if ((pc & (pc - 1)) == 0)
+    row = local >> __builtin_ctz((unsigned)pc);
+  else
+    row = local / pc;
+  const int col = local - row * pc;
   const int eig = col * j.rows + row;
 #else
   const int col = local / j.rows, row = local - col * j.rows;
