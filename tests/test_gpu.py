@@ -114,6 +114,37 @@ def test_pred_uniform_per_model(model):
         assert np.array_equal(g, w)
 
 
+@pytest.mark.parametrize("w,h,bd,off,flav,frame", [(264, 136, 10, 1, 1, 1), (1032, 520, 8, 4, 0, 2),
+                                                  (520, 264, 12, 0, 1, 3), (2056, 1032, 10, 3, 1, 4)])
+def test_pred_ragged_size_and_seq_variants(w, h, bd, off, flav, frame):
+    """Picture sizes that are multiples of 8 but not of the CTU or 16 (partial CTUs on the right
+    and bottom, 8-wide / 8-high leaves there), 8/10/12-bit samples, every mm_offset4x4 code
+    (MVReprojection.cpp:10), both GED flavors, and the axis geodesic models GEODESIC_X/Y/Z
+    besides the seven of ALL_MODELS."""
+    models = W.ALL_MODELS + (mm360.GEODESIC_X, mm360.GEODESIC_Y, mm360.GEODESIC_Z)
+    cfg = W.Config("ragged", w, h, models, 1, "ragged")
+    params = mm360.seq_params(w, h, models, bit_depth=bd, mm_offset4x4=off, ged_flavor=flav)
+    pus = W.pu_list(cfg, frame=frame)
+    assert (pus["x"] + pus["w"]).max() == w and (pus["y"] + pus["h"]).max() == h
+    refs = {poc: W.ref_planes(w, h, poc, bit_depth=bd) for poc in W.REF_POCS}
+    if bd == 12:  # spread the 10-bit content over the 12-bit range
+        refs = {poc: tuple(np.clip(a.astype(np.int32) * 4 + 3, 0, 4095).astype(np.int16) for a in planes)
+                for poc, planes in refs.items()}
+    want = Oracle(params, EPI).predict(W.CUR_POC, pus, refs, w, h)
+    with _ctx(params) as ctx:
+        got = _gpu_predict(ctx, params, W.CUR_POC, pus, refs)
+        # the same list through the device planner (mm_pred_device), in 3 stripes
+        ctx.set_stripes(3)
+        dst = _planes(cfg, -7)
+        ctx.predict_device(W.CUR_POC, mm360.pus_to_device(pus), *dst)
+        assert ctx.status() == (mm360.MM_OK, -1)
+        got_dev = [t.cpu().numpy() for t in dst]
+    for name, g, gd, wv in zip("Y Cb Cr".split(), got, got_dev, want):
+        assert np.array_equal(g, wv), f"{name}: {(g != wv).sum()} samples differ"
+        assert np.array_equal(gd, wv), f"{name} (device plan): {(gd != wv).sum()} samples differ"
+    assert int(want[0].max()) <= (1 << bd) - 1 and int(want[0].max()) > (1 << bd) // 2
+
+
 def test_pred_extreme_motion_zeroing():
     cfg = W.CONFIGS["C1"]
     params = mm360.seq_params(cfg.width, cfg.height, W.ALL_MODELS)
