@@ -133,7 +133,7 @@ def test_pred_ragged_size_and_seq_variants(w, h, bd, off, flav, frame):
     want = Oracle(params, EPI).predict(W.CUR_POC, pus, refs, w, h)
     with _ctx(params) as ctx:
         got = _gpu_predict(ctx, params, W.CUR_POC, pus, refs)
-        # the same list through the device planner (mm_pred_device), in 3 stripes
+        # the same list already resident in HBM (mm_pred_device), planned in 3 stripes
         ctx.set_stripes(3)
         dst = _planes(cfg, -7)
         ctx.predict_device(W.CUR_POC, mm360.pus_to_device(pus), *dst)
