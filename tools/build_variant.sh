@@ -10,6 +10,6 @@ rm -rf "$d"; mkdir -p "$d/csrc" "$d/include"
 cp vvc-extension-mm_amd/csrc/* "$d/csrc/"; cp include/mm360.h "$d/include/"
 sed -i 's|"../../include/mm360.h"|"../include/mm360.h"|' "$d"/csrc/*.h "$d"/csrc/*.hip
 if [ -n "$expr" ]; then sed -i "$expr" "$d/csrc/mm_kernels.hip" "$d"/csrc/*.h; fi
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-fast-math -fPIC -shared \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-fast-math -fPIC -shared -mllvm -amdgpu-use-amdgpu-trackers=1 \
   -Wno-unused-function "$@" "$d/csrc/mm_kernels.hip" -o "$d/libmm360.so"
 echo "built $d/libmm360.so"
