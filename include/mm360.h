@@ -15,7 +15,11 @@
  *   mm_pred          <- InterPrediction::xPredInterBlkMM  SRC/InterPrediction.h:151-154,
  *   mm_pred_device      batched over a picture's PU list together with the MM dispatch of
  *                       xPredInterUni (InterPrediction.cpp:455-533) and xWeightedAverage
- *                       (addAvg / copyClip)               SRC/InterPrediction.cpp:1584-1679
+ *                       (addAvg / addWeightedAvg (BCW) / copyClip)
+ *                                                         SRC/InterPrediction.cpp:1584-1679,
+ *                                                         SRC/Buffer.cpp:398-424, 551-658
+ *   mm_pred_list     <- InterPrediction::xPredInterBlkMM 1:1 per list: one reference list of every
+ *                       PU, bi=true (14-bit, rndRes=false) or bi=false (clipped), InterPrediction.cpp:683-856
  *   mm_filter        <- InterpolationFilter::filterHor/filterVer  SRC/InterpolationFilter.h:123-128
  *   mm_pred_dmvr     <- InterPrediction::xProcessDMVRProjected  SRC/InterPrediction.cpp:2442-2634
  *   mm_mvp_convert   <- MVReprojection::motionVectorInDesiredMotionModel  SRC/MVReprojection.cpp:168-217
@@ -85,13 +89,56 @@ typedef struct mm_block_desc {
   int32_t cur_poc, ref_poc;    /* for GEODESIC_CAMPOSE epipole selection */
 } mm_block_desc;
 
-/* One prediction unit (or sub-PU after the host's xSubPuBio / DMVR / SbTMVP split) */
+/* BCW weight index (CU::bcwIdx): g_BcwWeights = {-2, 3, 4, 5, 10} (Rom.cpp:203), BCW_DEFAULT = 2
+ * (CommonDef.h:348-349) is the plain addAvg.  Only bi PUs use it. */
+#define MM_BCW_DEFAULT 2
+
+/* One prediction unit (or sub-PU after the host's xSubPuBio / DMVR / SbTMVP split; the helpers in
+ * host/mm360_vtm.hpp derive these effective blocks).  64 bytes.  The PUs of one call must not
+ * overlap (every luma sample is predicted by at most one PU, as in a decoded picture); the result
+ * of an overlapping list is undefined, and a list whose PUs cover more sub-blocks than the
+ * picture has is rejected with MM_ERR_ARG. */
 typedef struct mm_pu_desc {
   int32_t x, y, w, h;          /* luma area */
   int32_t mv[2][2];            /* [list][hor, ver], 1/16 luma */
   int32_t ref_poc[2];          /* reference POC per list, -1 = list unused */
   int32_t model[2];            /* mm_model_id per list (non-CLASSIC for MM MC) */
+  int32_t bcw_idx;             /* CU::bcwIdx 0..4 (bi PUs; MM_BCW_DEFAULT = addAvg); ignored for uni */
+  int32_t reserved[3];         /* must be zero */
 } mm_pu_desc;
+
+/* ---- Effective blocks (host-side, no GPU) ----------------------------------------------------
+ * The blocks InterPrediction::motionCompensation (SRC/InterPrediction.cpp:1681-1810) hands to
+ * xPredInterBlkMM for one decoded PU: the BDOF pre-check's 16x16 split (xSubPuBio :361-453; the
+ * reprojection block centre moves to the sub-PU), SbTMVP strip merging of identical MotionInfo
+ * (xSubPuMC :283-359), xCheckIdenticalMotion (:248-281, bi -> uni L0) and the DMVR decision
+ * (PU::checkDMVRCondition, UnitTools.cpp:1698-1726).  See csrc/mm_effective.h. */
+#define MM_PU_MERGE 0x001u       /* pu.mergeFlag */
+#define MM_PU_SUBPU 0x002u       /* mergeType == MRG_TYPE_SUBPU_ATMVP: motion per 8x8 in sub_motion */
+#define MM_PU_CIIP 0x004u        /* pu.ciipFlag */
+#define MM_PU_SMVD 0x008u        /* cu.smvdMode */
+#define MM_PU_MMVD 0x010u        /* pu.mmvdMergeFlag || cu.mmvdSkip */
+#define MM_PU_MVREFINE 0x020u    /* pu.mvRefine (DMVR requested) */
+#define MM_PU_WEIGHTED 0x040u    /* explicit weighted prediction applies (WPScalingParam::isWeighted) */
+#define MM_PU_LONGTERM 0x080u    /* a list references a long-term picture */
+#define MM_PU_REF_SCALED 0x100u  /* a reference is scaled (RPR) */
+#define MM_PU_MMVD_ENC2 0x200u   /* encoder: mmvdEncOptMode == 2 && mmvdMergeFlag */
+
+typedef struct mm_tool_flags {  /* SPS / PPS / PH switches of the current picture */
+  int32_t bdof;   /* sps BDOF enabled && !ph_bdof_disabled */
+  int32_t dmvr;   /* sps DMVR enabled && !ph_dmvr_disabled */
+  int32_t bcw;    /* sps BCW enabled */
+  int32_t wp_bi;  /* pps weighted bi-prediction (xCheckIdenticalMotion) */
+} mm_tool_flags;
+
+typedef struct mm_pu_motion {
+  mm_pu_desc pu;        /* the decoded PU: luma area, motion, CU bcwIdx */
+  uint32_t flags;       /* MM_PU_* */
+  int32_t cur_poc;
+  int32_t sub_motion;   /* MM_PU_SUBPU: first of (w/8) x (h/8) raster mm_pu_desc motion records */
+  int32_t reserved;
+} mm_pu_motion;
+
 
 /* One block of an encoder motion search (InterSearch::xMVReprojectionInterpolation call site,
  * EncoderLib/InterSearch.cpp:6189-6273): a window of candidate MVs around `mv` is evaluated. */
@@ -128,8 +175,29 @@ const char* mm_last_error(mm_ctx* ctx);
 int mm_get_version(void);
 
 /* Epipoles in Q24 fixed point (EPIPOLE_PRECISION_FIXED, CommonDef.h:441).  cur/ref POC -1 are
- * the wildcards of EpipoleList::findEpipoleFixed (exact pair, then (cur,-1), then (-1,-1)). */
+ * the wildcards of EpipoleList::findEpipoleFixed (exact pair, then (cur,-1), then (-1,-1)).
+ * mm_set_epipole == EpipoleList::addEpipole(..., makeAvailable = true) on the context's list, as
+ * the decoder adds them (DecLib.cpp:2048, 3141). */
 int mm_set_epipole(mm_ctx* ctx, int cur_poc, int ref_poc, const int32_t q24[3]);
+
+/* EpipoleList (SRC/EpipoleList.{h,cpp}) with its availability semantics.  A new list holds the
+ * global (-1, -1) zero epipole, not available (EpipoleList.h:15-17); lookups only see available
+ * entries.  Standalone lists need no GPU; mm_get_epipole_list returns the context's own list
+ * (owned by the context, which uses it for every GEODESIC_CAMPOSE lookup). */
+typedef struct mm_epipole_list mm_epipole_list;
+mm_epipole_list* mm_epipole_list_create(void);
+void mm_epipole_list_destroy(mm_epipole_list* list);        /* no-op on a context's list */
+mm_epipole_list* mm_get_epipole_list(mm_ctx* ctx);
+/* addEpipole (EpipoleList.cpp:8-11), Q24 in (the caller applies floatingToFixed) */
+int mm_epipole_add(mm_epipole_list* list, int cur_poc, int ref_poc, const int32_t q24[3], int make_available);
+int mm_epipole_make_available(mm_epipole_list* list, int cur_poc);           /* :91-99 */
+int mm_epipole_has(mm_epipole_list* list, int cur_poc, int ref_poc);         /* :82-89, 1 / 0 */
+int mm_epipole_find(mm_epipole_list* list, int cur_poc, int ref_poc, int32_t q24[3]); /* :19-36 */
+/* derivePredictor (EpipoleList.cpp:38-80, incl. the `p0 + p1 / 2` tie rule as written) followed by
+ * the decoder's floatingToFixed (DecLib.cpp:3138): the Q24 predictor the picture header's epipole
+ * delta is added to.  MM_ERR_NOEPIPOLE if the global epipole is not available. */
+int mm_epipole_derive_predictor(mm_epipole_list* list, int cur_poc, int32_t q24[3]);
+int mm_epipole_count(mm_epipole_list* list);                                 /* EpipoleList::count */
 
 /* Reference picture planes (reconstruction, unpadded, picture origin at plane[0]).  `src_is_device`
  * = 1 when the pointers are device memory.  The context keeps its own device copy; padding is
@@ -143,8 +211,9 @@ int mm_release_ref(mm_ctx* ctx, int poc);
 int mm_reproject(mm_ctx* ctx, const mm_block_desc* blocks, int n, int32_t* out_xy);
 
 /* Batched motion compensation of one picture's PU list (host descriptor array).
- * Writes the final prediction (bi: addAvg of both lists' 14-bit predictions; uni: clipped
- * prediction) of every PU into the destination planes (device memory, picture-sized). */
+ * Writes the final prediction (bi: addAvg, or addWeightedAvg when bcw_idx != MM_BCW_DEFAULT, of
+ * both lists' 14-bit predictions; uni: clipped prediction) of every PU into the destination planes
+ * (device memory, picture-sized). */
 int mm_pred(mm_ctx* ctx, int cur_poc, const mm_pu_desc* pus, int n, int16_t* dst_y,
             ptrdiff_t dst_stride_y, int16_t* dst_cb, int16_t* dst_cr, ptrdiff_t dst_stride_c);
 
@@ -169,6 +238,24 @@ int mm_pred_prepare(mm_ctx* ctx, int cur_poc, const mm_pu_desc* pus, int n);
 int mm_pred_run(mm_ctx* ctx, int16_t* dst_y, ptrdiff_t dst_stride_y, int16_t* dst_cb,
                 int16_t* dst_cr, ptrdiff_t dst_stride_c);
 
+/* Effective blocks of n decoded PUs (see MM_PU_*): out_mc receives the PUs for mm_pred (bi, uni,
+ * identical-motion bi as uni L0, 16x16 sub-PUs, merged SbTMVP strips), out_dmvr those for
+ * mm_pred_dmvr, each in motionCompensation's order.  n_mc / n_dmvr receive the counts; a count
+ * beyond cap_* returns MM_ERR_ARG with the required counts.  Host code only: no context, no GPU. */
+int mm_derive_effective_blocks(const mm_tool_flags* tools, const mm_pu_motion* pus, int n, const mm_pu_desc* sub_motion,
+                               mm_pu_desc* out_mc, int cap_mc, int* n_mc, mm_pu_desc* out_dmvr, int cap_dmvr,
+                               int* n_dmvr);
+
+/* xPredInterBlkMM 1:1 per list (InterPrediction.h:151-154): the prediction of reference list
+ * `list` (0/1) of every PU, exactly as InterPrediction::xPredInterBlkMM leaves it in its PelUnitBuf:
+ * hp = 1 -> bi = true, 14-bit intermediate (rndRes = false, InterPrediction.cpp:697), as the
+ * caller's GEO / BCW / CIIP blending consumes it (InterPrediction.cpp:637, 1651-1670); hp = 0 ->
+ * bi = false, rounded and clipped.  Every PU must use `list` (ref_poc[list] >= 0), the other list is
+ * ignored.  dst_y or dst_cb/dst_cr may be NULL to skip that component (per-component calls of the
+ * reference).  Device-planned like mm_pred; host PU list; synchronous status. */
+int mm_pred_list(mm_ctx* ctx, int cur_poc, const mm_pu_desc* pus, int n, int list, int hp, int16_t* dst_y,
+                 ptrdiff_t dst_stride_y, int16_t* dst_cb, int16_t* dst_cr, ptrdiff_t dst_stride_c);
+
 /* MM-DMVR (InterPrediction::xProcessDMVRProjected, InterPrediction.cpp:2442-2634): bi PUs that
  * pass PU::checkDMVRCondition (UnitTools.cpp:1698-1726; equal models, w, h >= 8, w*h >= 128 are
  * checked here, merge mode / POC distances / weights are the caller's decision).  Every
@@ -188,8 +275,10 @@ int mm_mvp_convert(mm_ctx* ctx, const mm_mvp_query* queries, int n, int32_t* mv_
 
 /* Single-block interpolation (InterpolationFilter::filterHor/filterVer on the device), for
  * parity tests of the integer pel pipeline.  comp 0 = luma 8-tap (16 phases), else chroma 4-tap
- * (32 phases).  `src` points at the block origin inside a host buffer that holds at least
- * (taps/2 - 1) samples of margin on every side; dst is host memory (w*h int16). */
+ * (32 phases).  `src` points at the block origin inside a host buffer; along the filtered axis
+ * (columns for filterHor, rows for filterVer) the filter reads (taps/2 - 1) samples before the
+ * block and taps/2 after it (luma 3 before / 4 after, chroma 1 / 2), nothing beyond the block on
+ * the other axis; dst is host memory (w*h int16). */
 int mm_filter(mm_ctx* ctx, int comp, int vertical, const int16_t* src, ptrdiff_t src_stride,
               int16_t* dst, ptrdiff_t dst_stride, int w, int h, int frac, int is_first,
               int is_last);

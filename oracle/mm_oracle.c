@@ -23,6 +23,7 @@
  * Build: gcc -O2 -msse4.1 -ffp-contract=off -fPIC -shared (no -mfma: the reference build has
  * none, CMakeLists.txt:90-93).  File:line citations are into source/Lib/CommonLib.
  */
+#include <limits.h>
 #include <math.h>
 #include <smmintrin.h>
 #include <stdint.h>
@@ -864,15 +865,26 @@ int orc_reproject(void* h, const mm_block_desc* b, int n, int32_t* out) {
 }
 
 /* mm_pred twin.  refs: n_refs pictures given as pocs[i] + planes (unpadded host planes). */
+/* g_BcwWeights (Rom.cpp:203) and getBcwWeight (Rom.cpp:208-213): w1 = g_BcwWeights[idx], w0 = 8 - w1 */
+static const int BCW_WEIGHTS[5] = {-2, 3, 4, 5, 10};
+
 /* One PU: xPredInterUni per list (xPredInterBlkMM per component) + xWeightedAverage
- * (addAvg / copyClip, InterPrediction.cpp:1584-1679) into the destination planes. */
+ * (InterPrediction.cpp:1584-1679): addWeightedAvg when bcwIdx != BCW_DEFAULT (:1596-1600,
+ * Buffer.cpp:398-424), else addAvg (Buffer.cpp:551-582); uni: copyClip.
+ * only_list >= 0: mm_pred_list -- just that list's xPredInterBlkMM(bi = hp) output is written. */
 static int pred_pu(Orc* o, const OPic* pics, int n_refs, const mm_pu_desc* u, int cur_poc, int16_t* pred[2][3],
-                   int16_t* dy, ptrdiff_t sdy, int16_t* dcb, int16_t* dcr, ptrdiff_t sdc) {
+                   int16_t* dy, ptrdiff_t sdy, int16_t* dcb, int16_t* dcr, ptrdiff_t sdc, int only_list, int hp) {
   int rc = 0;
   int bi = u->ref_poc[0] >= 0 && u->ref_poc[1] >= 0;
+  if (only_list >= 0) {
+    if (u->ref_poc[only_list] < 0) return MM_ERR_ARG;
+    bi = hp;
+  } else if (bi && (u->bcw_idx < 0 || u->bcw_idx > 4)) {
+    return MM_ERR_ARG;
+  }
   int ncomp = o->chroma ? 3 : 1;
   for (int l = 0; l < 2 && !rc; l++) {
-    if (u->ref_poc[l] < 0) continue;
+    if (u->ref_poc[l] < 0 || (only_list >= 0 && l != only_list)) continue;
     const OPic* ref = NULL;
     for (int r = 0; r < n_refs; r++)
       if (pics[r].poc == u->ref_poc[l]) ref = &pics[r];
@@ -893,7 +905,13 @@ static int pred_pu(Orc* o, const OPic* pics, int n_refs, const mm_pu_desc* u, in
     for (int y = 0; y < hh; y++)
       for (int x = 0; x < w; x++) {
         int k = y * w + x;
-        if (bi) { /* AreaBuf<Pel>::addAvg */
+        if (only_list >= 0) { /* the PelUnitBuf xPredInterBlkMM wrote */
+          d[y * ds + x] = pred[only_list][c][k];
+        } else if (bi && u->bcw_idx != 2) { /* AreaBuf<Pel>::addWeightedAvg */
+          int w1 = BCW_WEIGHTS[u->bcw_idx], w0 = 8 - w1;
+          int shiftNum = frac_bits(o->bd) + 3, offset = (1 << (shiftNum - 1)) + (8192 << 3);
+          d[y * ds + x] = clip_pel((pred[0][c][k] * w0 + pred[1][c][k] * w1 + offset) >> shiftNum, o->bd);
+        } else if (bi) { /* AreaBuf<Pel>::addAvg */
           int shiftNum = frac_bits(o->bd) + 1, offset = (1 << (shiftNum - 1)) + 2 * 8192;
           d[y * ds + x] = clip_pel((pred[0][c][k] + pred[1][c][k] + offset) >> shiftNum, o->bd);
         } else { /* copyClip */
@@ -928,20 +946,39 @@ static void free_refs(OPic* pics, int n_refs) {
   free(pics);
 }
 
-int orc_pred(void* h, int cur_poc, const mm_pu_desc* pus, int n, int n_refs, const int32_t* pocs,
-             const int16_t* const* ys, const int16_t* const* cbs, const int16_t* const* crs, ptrdiff_t stride_y,
-             ptrdiff_t stride_c, int16_t* dy, ptrdiff_t sdy, int16_t* dcb, int16_t* dcr, ptrdiff_t sdc) {
+static int pred_list_all(void* h, int cur_poc, const mm_pu_desc* pus, int n, int n_refs, const int32_t* pocs,
+                         const int16_t* const* ys, const int16_t* const* cbs, const int16_t* const* crs,
+                         ptrdiff_t stride_y, ptrdiff_t stride_c, int16_t* dy, ptrdiff_t sdy, int16_t* dcb, int16_t* dcr,
+                         ptrdiff_t sdc, int only_list, int hp) {
   Orc* o = (Orc*)h;
   OPic* pics = pad_refs(o, n_refs, pocs, ys, cbs, crs, stride_y, stride_c);
   int rc = 0;
   int16_t* pred[2][3];
   for (int l = 0; l < 2; l++)
     for (int c = 0; c < 3; c++) pred[l][c] = (int16_t*)malloc(sizeof(int16_t) * 128 * 128);
-  for (int i = 0; i < n && !rc; i++) rc = pred_pu(o, pics, n_refs, &pus[i], cur_poc, pred, dy, sdy, dcb, dcr, sdc);
+  for (int i = 0; i < n && !rc; i++)
+    rc = pred_pu(o, pics, n_refs, &pus[i], cur_poc, pred, dy, sdy, dcb, dcr, sdc, only_list, hp);
   for (int l = 0; l < 2; l++)
     for (int c = 0; c < 3; c++) free(pred[l][c]);
   free_refs(pics, n_refs);
   return rc;
+}
+
+int orc_pred(void* h, int cur_poc, const mm_pu_desc* pus, int n, int n_refs, const int32_t* pocs,
+             const int16_t* const* ys, const int16_t* const* cbs, const int16_t* const* crs, ptrdiff_t stride_y,
+             ptrdiff_t stride_c, int16_t* dy, ptrdiff_t sdy, int16_t* dcb, int16_t* dcr, ptrdiff_t sdc) {
+  return pred_list_all(h, cur_poc, pus, n, n_refs, pocs, ys, cbs, crs, stride_y, stride_c, dy, sdy, dcb, dcr, sdc, -1,
+                       0);
+}
+
+/* mm_pred_list twin: xPredInterBlkMM (InterPrediction.cpp:683-856) of list `list` of every PU,
+ * bi = hp (14-bit intermediate) or rounded + clipped. */
+int orc_pred_list(void* h, int cur_poc, const mm_pu_desc* pus, int n, int list, int hp, int n_refs,
+                  const int32_t* pocs, const int16_t* const* ys, const int16_t* const* cbs,
+                  const int16_t* const* crs, ptrdiff_t stride_y, ptrdiff_t stride_c, int16_t* dy, ptrdiff_t sdy,
+                  int16_t* dcb, int16_t* dcr, ptrdiff_t sdc) {
+  return pred_list_all(h, cur_poc, pus, n, n_refs, pocs, ys, cbs, crs, stride_y, stride_c, dy, sdy, dcb, dcr, sdc,
+                       list, hp);
 }
 
 /* ---- MM-DMVR: InterPrediction::xProcessDMVRProjected (InterPrediction.cpp:2442-2634) ---- */
@@ -1008,6 +1045,7 @@ int orc_pred_dmvr(void* h, int cur_poc, const mm_pu_desc* pus, int n, int n_refs
       if (pics[r].poc == u->ref_poc[1]) r1 = &pics[r];
     }
     if (!r0 || !r1) { rc = MM_ERR_NOREF; break; }
+    if (u->bcw_idx != 2) { rc = MM_ERR_ARG; break; } /* checkDMVRCondition: BCW_DEFAULT (UnitTools.cpp:1719) */
     const int dxs = u->w < 16 ? u->w : 16, dys = u->h < 16 ? u->h : 16, model = u->model[0];
     for (int y = u->y; y < u->y + u->h && !rc; y += dys)
       for (int x = u->x; x < u->x + u->w && !rc; x += dxs) {
@@ -1045,7 +1083,7 @@ int orc_pred_dmvr(void* h, int cur_poc, const mm_pu_desc* pus, int n, int n_refs
         sp.x = x; sp.y = y; sp.w = dxs; sp.h = dys;
         sp.mv[0][0] = clip_mv18(u->mv[0][0] + tdx); sp.mv[0][1] = clip_mv18(u->mv[0][1] + tdy);
         sp.mv[1][0] = clip_mv18(u->mv[1][0] - tdx); sp.mv[1][1] = clip_mv18(u->mv[1][1] - tdy);
-        if (!rc) rc = pred_pu(o, pics, n_refs, &sp, cur_poc, pred, dy, sdy, dcb, dcr, sdc);
+        if (!rc) rc = pred_pu(o, pics, n_refs, &sp, cur_poc, pred, dy, sdy, dcb, dcr, sdc, -1, 0);
       }
   }
   free(s0);
@@ -1301,4 +1339,290 @@ int orc_mvp(void* h, const mm_mvp_query* qs, int n, int32_t* out) {
     r[1] = _mm_cvtt_ss2si(_mm_set_ss(ry));
   }
   return 0;
+}
+
+/* ==========================================================================================
+ * EpipoleList (SRC/EpipoleList.{h,cpp}) -- entries kept sorted by (curPOC, refPOC) like the
+ * reference's std::map; Q24 fixed point.
+ * ========================================================================================== */
+typedef struct {
+  int n;
+  int key[512][2];
+  int32_t q[512][3];
+  int avail[512];
+} OEpi;
+
+static int oepi_index(const OEpi* e, int cur, int ref) {
+  for (int i = 0; i < e->n; i++)
+    if (e->key[i][0] == cur && e->key[i][1] == ref) return i;
+  return -1;
+}
+
+/* addEpipole (:8-11): m_epipoleMap[{curPOC, refPOC}] = entry */
+int orc_epi_add(void* h, int cur, int ref, const int32_t* q, int make_available) {
+  OEpi* e = (OEpi*)h;
+  int i = oepi_index(e, cur, ref);
+  if (i < 0) {
+    if (e->n >= 512) return MM_ERR_ARG;
+    i = e->n;
+    while (i > 0 && (e->key[i - 1][0] > cur || (e->key[i - 1][0] == cur && e->key[i - 1][1] > ref))) {
+      memcpy(e->key[i], e->key[i - 1], sizeof(e->key[i]));
+      memcpy(e->q[i], e->q[i - 1], sizeof(e->q[i]));
+      e->avail[i] = e->avail[i - 1];
+      i--;
+    }
+    e->n++;
+    e->key[i][0] = cur;
+    e->key[i][1] = ref;
+  }
+  memcpy(e->q[i], q, 12);
+  e->avail[i] = make_available != 0;
+  return 0;
+}
+
+/* EpipoleList() : addEpipole({0, 0, 0}) -- global, not available (EpipoleList.h:15-17) */
+void* orc_epi_create(void) {
+  OEpi* e = (OEpi*)calloc(1, sizeof(OEpi));
+  const int32_t z[3] = {0, 0, 0};
+  orc_epi_add(e, -1, -1, z, 0);
+  return e;
+}
+void orc_epi_destroy(void* h) { free(h); }
+
+/* findEpipoleFixed (:19-36) */
+int orc_epi_find(void* h, int cur, int ref, int32_t* out) {
+  const OEpi* e = (const OEpi*)h;
+  int i = oepi_index(e, cur, ref);
+  if (i < 0 || !e->avail[i]) i = oepi_index(e, cur, -1);
+  if (i >= 0 && !e->avail[i]) i = -1;
+  if (i < 0) i = oepi_index(e, -1, -1);
+  if (i < 0 || !e->avail[i]) return MM_ERR_NOEPIPOLE;
+  memcpy(out, e->q[i], 12);
+  return 0;
+}
+
+/* hasEpipole (:82-89) */
+int orc_epi_has(void* h, int cur, int ref) {
+  const OEpi* e = (const OEpi*)h;
+  int i = oepi_index(e, cur, ref);
+  return i >= 0 && e->avail[i];
+}
+
+/* makeAvailable (:91-99) */
+void orc_epi_make_available(void* h, int cur) {
+  OEpi* e = (OEpi*)h;
+  for (int i = 0; i < e->n; i++)
+    if (e->key[i][0] == cur) e->avail[i] = 1;
+}
+
+/* FloatingFixedConversion::fixedToFloating / floatingToFixed (Coordinate.cpp:70-92) */
+static float fx2fl(int32_t v) { return (float)(v >> 24) + (float)(v & ((1 << 24) - 1)) / (float)(1 << 24); }
+static int32_t fl2fx(float f) { return (int32_t)roundf(f * (float)(1 << 24)); }
+
+/* derivePredictor (:38-80) + DecLib.cpp:3138 floatingToFixed */
+int orc_epi_predictor(void* h, int cur, int32_t* out) {
+  const OEpi* e = (const OEpi*)h;
+  int g = oepi_index(e, -1, -1);
+  if (g < 0 || !e->avail[g]) return MM_ERR_NOEPIPOLE; /* CHECK(!globalEpipoleEntry.isAvailable) */
+  int minPOCDistances[2] = {INT_MAX, INT_MAX};
+  int32_t predictors[2][3];
+  memcpy(predictors[0], e->q[g], 12);
+  memcpy(predictors[1], e->q[g], 12);
+  for (int i = 0; i < e->n; i++) {
+    if (!e->avail[i]) continue;
+    int distance = abs(cur - e->key[i][0]);
+    if (distance < minPOCDistances[0]) {
+      minPOCDistances[0] = distance;
+      memcpy(predictors[0], e->q[i], 12);
+    } else if (distance < minPOCDistances[1]) {
+      minPOCDistances[1] = distance;
+      memcpy(predictors[1], e->q[i], 12);
+    }
+  }
+  int32_t predictor[3];
+  if (minPOCDistances[0] == minPOCDistances[1]) {
+    for (int k = 0; k < 3; k++) predictor[k] = predictors[0][k] + predictors[1][k] / 2; /* as written (:71) */
+  } else {
+    if (minPOCDistances[0] > minPOCDistances[1]) return MM_ERR_ARG;
+    memcpy(predictor, predictors[0], 12);
+  }
+  for (int k = 0; k < 3; k++) out[k] = fl2fx(fx2fl(predictor[k]));
+  return 0;
+}
+
+int orc_epi_count(void* h) {
+  const OEpi* e = (const OEpi*)h;
+  int g = oepi_index(e, -1, -1);
+  int def = g >= 0 && e->q[g][0] == 0 && e->q[g][1] == 0 && e->q[g][2] == 0;
+  return e->n - def;
+}
+
+/* ==========================================================================================
+ * InterPrediction::motionCompensation (InterPrediction.cpp:1681-1810) for MM PUs: the blocks it
+ * hands to xPredInterBlkMM (via xPredInterUni / xPredInterBi) and the DMVR decision.
+ * ========================================================================================== */
+typedef struct {
+  const mm_tool_flags* tools;
+  mm_pu_desc *mc, *dmvr;
+  int n_mc, n_dmvr, cap_mc, cap_dmvr;
+} OEff;
+
+/* PU::isBiPredFromDifferentDirEqDistPoc (UnitTools.cpp:4466-4487) */
+static int o_bi_dd_eq(const mm_pu_desc* pu, int poc, unsigned flags) {
+  if (pu->ref_poc[0] >= 0 && pu->ref_poc[1] >= 0) {
+    if (flags & MM_PU_LONGTERM) return 0;
+    const int poc0 = pu->ref_poc[0], poc1 = pu->ref_poc[1];
+    if ((poc - poc0) * (poc - poc1) < 0)
+      if (abs(poc - poc0) == abs(poc - poc1)) return 1;
+  }
+  return 0;
+}
+
+/* PU::checkDMVRCondition (UnitTools.cpp:1698-1726) */
+static int o_check_dmvr(const OEff* x, const mm_pu_desc* pu, int poc, unsigned flags, int merge_type_default) {
+  if (!x->tools->dmvr) return 0;
+  return (flags & MM_PU_MERGE) && merge_type_default && !(flags & MM_PU_CIIP) && !(flags & MM_PU_MMVD) &&
+         pu->model[0] == pu->model[1] && o_bi_dd_eq(pu, poc, flags) && pu->h >= 8 && pu->w >= 8 &&
+         pu->h * pu->w >= 128 && pu->bcw_idx == 2 && !(flags & MM_PU_WEIGHTED) && !(flags & MM_PU_REF_SCALED);
+}
+
+static void o_emit(OEff* x, const mm_pu_desc* pu, int to_dmvr) {
+  mm_pu_desc d = *pu;
+  d.reserved[0] = d.reserved[1] = d.reserved[2] = 0;
+  if (to_dmvr) {
+    if (x->n_dmvr < x->cap_dmvr) x->dmvr[x->n_dmvr] = d;
+    x->n_dmvr++;
+  } else {
+    if (x->n_mc < x->cap_mc) x->mc[x->n_mc] = d;
+    x->n_mc++;
+  }
+}
+
+/* MotionInfo::operator== (MotionInfo.h:196-219) */
+static int o_mi_equal(const mm_pu_desc* a, const mm_pu_desc* b) {
+  int interDirA = (a->ref_poc[0] >= 0 ? 1 : 0) + (a->ref_poc[1] >= 0 ? 2 : 0);
+  int interDirB = (b->ref_poc[0] >= 0 ? 1 : 0) + (b->ref_poc[1] >= 0 ? 2 : 0);
+  if (interDirA != interDirB) return 0;
+  if (interDirA != 2) {
+    if (a->ref_poc[0] != b->ref_poc[0] || a->mv[0][0] != b->mv[0][0] || a->mv[0][1] != b->mv[0][1] ||
+        a->model[0] != b->model[0])
+      return 0;
+  }
+  if (interDirA != 1) {
+    if (a->ref_poc[1] != b->ref_poc[1] || a->mv[1][0] != b->mv[1][0] || a->mv[1][1] != b->mv[1][1] ||
+        a->model[1] != b->model[1])
+      return 0;
+  }
+  return 1;
+}
+
+static int o_motion_compensation(OEff* x, const mm_pu_desc* pu, unsigned flags, int poc, int merge_type_default,
+                                 int m_subPuMC, const mm_pu_desc* sub);
+
+/* xSubPuBio (:361-453) */
+static int o_sub_pu_bio(OEff* x, const mm_pu_desc* pu, unsigned flags, int poc) {
+  int fstStep = pu->h < 16 ? pu->h : 16, secStep = pu->w < 16 ? pu->w : 16;
+  for (int fstDim = pu->y; fstDim < pu->y + pu->h; fstDim += fstStep)
+    for (int secDim = pu->x; secDim < pu->x + pu->w; secDim += secStep) {
+      mm_pu_desc subPu = *pu;
+      subPu.x = secDim;
+      subPu.y = fstDim;
+      subPu.w = secStep;
+      subPu.h = fstStep;
+      int rc = o_motion_compensation(x, &subPu, flags, poc, 1, 0, NULL);
+      if (rc) return rc;
+    }
+  return 0;
+}
+
+/* xSubPuMC (:283-359) */
+static int o_sub_pu_mc(OEff* x, const mm_pu_desc* pu, unsigned flags, int poc, const mm_pu_desc* sub) {
+  int numPartLine = (pu->w >> 3) > 1 ? (pu->w >> 3) : 1;
+  int numPartCol = (pu->h >> 3) > 1 ? (pu->h >> 3) : 1;
+  int puHeight = numPartCol == 1 ? pu->h : 8;
+  int puWidth = numPartLine == 1 ? pu->w : 8;
+  int verMC = pu->h > pu->w;
+  int fstStart = !verMC ? pu->y : pu->x, secStart = !verMC ? pu->x : pu->y;
+  int fstEnd = !verMC ? pu->y + pu->h : pu->x + pu->w, secEnd = !verMC ? pu->x + pu->w : pu->y + pu->h;
+  int fstStep = !verMC ? puHeight : puWidth, secStep = !verMC ? puWidth : puHeight;
+  int scaled = (flags & MM_PU_REF_SCALED) != 0;
+#define O_MI(X, Y) (&sub[(((Y) - pu->y) / puHeight) * numPartLine + ((X) - pu->x) / puWidth])
+  for (int fstDim = fstStart; fstDim < fstEnd; fstDim += fstStep)
+    for (int secDim = secStart; secDim < secEnd; secDim += secStep) {
+      int xx = !verMC ? secDim : fstDim, yy = !verMC ? fstDim : secDim;
+      const mm_pu_desc* curMi = O_MI(xx, yy);
+      int length = secStep, later = secDim + secStep;
+      while (later < secEnd) {
+        const mm_pu_desc* laterMi = !verMC ? O_MI(later, fstDim) : O_MI(fstDim, later);
+        if (!scaled && o_mi_equal(laterMi, curMi))
+          length += secStep;
+        else
+          break;
+        later += secStep;
+      }
+      mm_pu_desc subPu = *curMi;
+      subPu.x = xx;
+      subPu.y = yy;
+      subPu.w = !verMC ? length : puWidth;
+      subPu.h = !verMC ? puHeight : length;
+      subPu.bcw_idx = pu->bcw_idx;
+      if (subPu.ref_poc[0] < 0 && subPu.ref_poc[1] < 0) return MM_ERR_ARG;
+      int rc = o_motion_compensation(x, &subPu, flags & ~(unsigned)(MM_PU_MVREFINE | MM_PU_SUBPU), poc, 1, 1, NULL);
+      if (rc) return rc;
+      secDim = later - secStep;
+    }
+#undef O_MI
+  return 0;
+}
+
+static int o_motion_compensation(OEff* x, const mm_pu_desc* pu, unsigned flags, int poc, int merge_type_default,
+                                 int m_subPuMC, const mm_pu_desc* sub) {
+  if (pu->ref_poc[0] >= 0 && pu->ref_poc[1] >= 0 && pu->w + pu->h == 12) return MM_ERR_ARG;
+  int bioApplied = 0;
+  if (x->tools->bdof) {
+    if (m_subPuMC) {
+      bioApplied = 0;
+    } else {
+      if (!(flags & MM_PU_WEIGHTED) && o_bi_dd_eq(pu, poc, flags) && pu->h >= 8 && pu->w >= 8 && pu->h * pu->w >= 128)
+        bioApplied = 1;
+    }
+    if (bioApplied && (flags & MM_PU_CIIP)) bioApplied = 0;
+    if (bioApplied && (flags & MM_PU_SMVD)) bioApplied = 0;
+    if (x->tools->bcw && bioApplied && pu->bcw_idx != 2) bioApplied = 0;
+    if (flags & MM_PU_MMVD_ENC2) bioApplied = 0;
+  }
+  if (flags & MM_PU_REF_SCALED) bioApplied = 0;
+  int dmvrApplied = (flags & MM_PU_MVREFINE) && o_check_dmvr(x, pu, poc, flags, merge_type_default);
+  if ((pu->w > 16 || pu->h > 16) && merge_type_default && (bioApplied && !dmvrApplied))
+    return o_sub_pu_bio(x, pu, flags, poc);
+  if (!merge_type_default) return o_sub_pu_mc(x, pu, flags, poc, sub);
+  /* xCheckIdenticalMotion (:248-281) */
+  if (!x->tools->wp_bi && pu->ref_poc[0] >= 0 && pu->ref_poc[1] >= 0 && pu->ref_poc[0] == pu->ref_poc[1] &&
+      pu->mv[0][0] == pu->mv[1][0] && pu->mv[0][1] == pu->mv[1][1]) {
+    mm_pu_desc u = *pu;
+    u.ref_poc[1] = -1;
+    u.mv[1][0] = u.mv[1][1] = 0;
+    u.model[1] = 0;
+    o_emit(x, &u, 0);
+    return 0;
+  }
+  o_emit(x, pu, dmvrApplied); /* xPredInterBi: DMVR inside when dmvrApplied */
+  return 0;
+}
+
+int orc_effective(const mm_tool_flags* tools, const mm_pu_motion* pus, int n, const mm_pu_desc* sub, mm_pu_desc* out_mc,
+                  int cap_mc, int* n_mc, mm_pu_desc* out_dmvr, int cap_dmvr, int* n_dmvr) {
+  OEff x = {tools, out_mc, out_dmvr, 0, 0, cap_mc, cap_dmvr};
+  for (int i = 0; i < n; i++) {
+    const mm_pu_motion* m = &pus[i];
+    const mm_pu_desc* pu = &m->pu;
+    if (pu->w < 4 || pu->h < 4 || (pu->w & 3) || (pu->h & 3) || (pu->ref_poc[0] < 0 && pu->ref_poc[1] < 0))
+      return MM_ERR_ARG;
+    int rc = o_motion_compensation(&x, pu, m->flags, m->cur_poc, !(m->flags & MM_PU_SUBPU), 0,
+                                   (m->flags & MM_PU_SUBPU) ? sub + m->sub_motion : NULL);
+    if (rc) return rc;
+  }
+  *n_mc = x.n_mc;
+  *n_dmvr = x.n_dmvr;
+  return (x.n_mc > cap_mc || x.n_dmvr > cap_dmvr) ? MM_ERR_ARG : 0;
 }

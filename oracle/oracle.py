@@ -32,6 +32,19 @@ def load():
     lib.orc_pred.argtypes = [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                              ctypes.c_ssize_t, ctypes.c_ssize_t, c_void_p, ctypes.c_ssize_t, c_void_p, c_void_p,
                              ctypes.c_ssize_t]
+    lib.orc_pred_list.argtypes = [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                                  c_void_p, c_void_p, ctypes.c_ssize_t, ctypes.c_ssize_t, c_void_p,
+                                  ctypes.c_ssize_t, c_void_p, c_void_p, ctypes.c_ssize_t]
+    lib.orc_effective.argtypes = [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, POINTER(c_int), c_void_p,
+                                  c_int, POINTER(c_int)]
+    lib.orc_epi_create.restype = c_void_p
+    lib.orc_epi_destroy.argtypes = [c_void_p]
+    lib.orc_epi_add.argtypes = [c_void_p, c_int, c_int, POINTER(c_int32), c_int]
+    lib.orc_epi_find.argtypes = [c_void_p, c_int, c_int, POINTER(c_int32)]
+    lib.orc_epi_has.argtypes = [c_void_p, c_int, c_int]
+    lib.orc_epi_make_available.argtypes = [c_void_p, c_int]
+    lib.orc_epi_predictor.argtypes = [c_void_p, c_int, POINTER(c_int32)]
+    lib.orc_epi_count.argtypes = [c_void_p]
     lib.orc_filter.argtypes = [c_int, c_int, c_int, c_void_p, ctypes.c_ssize_t, c_void_p, ctypes.c_ssize_t, c_int,
                                c_int, c_int, c_int, c_int]
     lib.orc_pred_dmvr.argtypes = [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -95,6 +108,25 @@ class Oracle:
             raise RuntimeError(f"oracle predict failed: {rc}")
         return dy, dcb, dcr
 
+    def predict_list(self, cur_poc, pus, list_, hp, refs, W, H):
+        """xPredInterBlkMM of reference list `list_` of every PU: 14-bit (hp) or clipped planes."""
+        pus = np.ascontiguousarray(pus)
+        pocs = sorted(refs)
+        ys = [np.ascontiguousarray(refs[p][0]) for p in pocs]
+        cbs = [np.ascontiguousarray(refs[p][1]) for p in pocs]
+        crs = [np.ascontiguousarray(refs[p][2]) for p in pocs]
+        dy = np.zeros((H, W), dtype=np.int16)
+        dcb = np.zeros((H // 2, W // 2), dtype=np.int16)
+        dcr = np.zeros((H // 2, W // 2), dtype=np.int16)
+        pa = np.array(pocs, dtype=np.int32)
+        rc = self.lib.orc_pred_list(self.h, cur_poc, c_void_p(pus.ctypes.data), len(pus), int(list_), int(hp),
+                                    len(pocs), c_void_p(pa.ctypes.data), _ptr_array(ys), _ptr_array(cbs),
+                                    _ptr_array(crs), ys[0].shape[1], cbs[0].shape[1], c_void_p(dy.ctypes.data), W,
+                                    c_void_p(dcb.ctypes.data), c_void_p(dcr.ctypes.data), W // 2)
+        if rc:
+            raise RuntimeError(f"oracle predict_list failed: {rc}")
+        return dy, dcb, dcr
+
     def predict_dmvr(self, cur_poc, pus, refs, W, H):
         """MM-DMVR PUs (xProcessDMVRProjected): predicted planes and the per-sub-PU L0 deltas."""
         pus = np.ascontiguousarray(pus)
@@ -151,3 +183,54 @@ class Oracle:
         if rc:
             raise RuntimeError(f"oracle filter failed: {rc}")
         return dst
+
+
+def effective_blocks(tools, pus, sub_motion, pu_dtype, cap=1 << 16):
+    """Oracle restatement of motionCompensation's effective blocks: (mc, dmvr) PU arrays."""
+    lib = load()
+    pus = np.ascontiguousarray(pus)
+    sub = np.ascontiguousarray(sub_motion)
+    mc = np.zeros(cap, dtype=pu_dtype)
+    dm = np.zeros(cap, dtype=pu_dtype)
+    n_mc, n_dm = c_int(0), c_int(0)
+    rc = lib.orc_effective(ctypes.addressof(tools), c_void_p(pus.ctypes.data), len(pus),
+                           c_void_p(sub.ctypes.data) if len(sub) else None, c_void_p(mc.ctypes.data), cap,
+                           ctypes.byref(n_mc), c_void_p(dm.ctypes.data), cap, ctypes.byref(n_dm))
+    if rc:
+        raise RuntimeError(f"oracle effective blocks failed: {rc}")
+    return mc[:n_mc.value], dm[:n_dm.value]
+
+
+class OracleEpipoleList:
+    """Oracle restatement of EpipoleList (SRC/EpipoleList.cpp)."""
+
+    def __init__(self):
+        self.lib = load()
+        self.h = c_void_p(self.lib.orc_epi_create())
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.lib.orc_epi_destroy(self.h)
+            self.h = None
+
+    def add(self, cur, ref, q, make_available=False):
+        self.lib.orc_epi_add(self.h, cur, ref, (c_int32 * 3)(*q), int(make_available))
+
+    def make_available(self, cur):
+        self.lib.orc_epi_make_available(self.h, cur)
+
+    def has(self, cur, ref):
+        return bool(self.lib.orc_epi_has(self.h, cur, ref))
+
+    def find(self, cur, ref):
+        q = (c_int32 * 3)()
+        rc = self.lib.orc_epi_find(self.h, cur, ref, q)
+        return None if rc else tuple(q)
+
+    def derive_predictor(self, cur):
+        q = (c_int32 * 3)()
+        rc = self.lib.orc_epi_predictor(self.h, cur, q)
+        return rc, (tuple(q) if rc == 0 else None)
+
+    def count(self):
+        return int(self.lib.orc_epi_count(self.h))

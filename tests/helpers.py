@@ -16,7 +16,12 @@ def load_blocks(npz):
 
 
 def load_pus(npz):
-    return np.ascontiguousarray(npz["pus"]).view(mm360.PU_DTYPE).reshape(-1)
+    """Fixture PUs: the first 12 int32 words of mm_pu_desc (x, y, w, h, mv, ref_poc, model) per row;
+    bcw_idx = BCW_DEFAULT."""
+    words = np.ascontiguousarray(npz["pus"], dtype=np.int32)
+    out = mm360.new_pus(len(words))
+    out.view(np.int32).reshape(len(words), -1)[:, :12] = words[:, :12]
+    return out
 
 
 def block_offsets(blocks):

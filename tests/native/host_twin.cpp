@@ -22,7 +22,6 @@ struct Twin {
   Geometry geo;
   std::vector<float> px[3], py[3];
   std::vector<uint8_t> vip[3];
-  std::vector<float> sph[3], tan3[3];  // frame-grid sphere points / TAN terms (k_sph_cache)
 };
 
 static void make_twin(const mm_seq_params* p, Twin* t) {
@@ -34,7 +33,8 @@ static void make_twin(const mm_seq_params* p, Twin* t) {
   t->sc.ged_flavor = p->ged_flavor;
   t->geo = Geometry{p->width,        p->height,           p->width >> 1,        p->height >> 1,
                     p->max_cu_width, p->max_cu_height,    p->max_cu_width >> 1, p->max_cu_height >> 1,
-                    p->bit_depth,    p->chroma_format == 1, 0};
+                    p->bit_depth,    p->chroma_format == 1, 0,                     0,
+                    3};
   const int cols = p->width / 4, rows = p->height / 4, n = cols * rows;
   for (int pl = 0; pl < 3; pl++) {
     if (!(p->active_models & (1u << (MPA_FRONT_BACK + pl)))) continue;
@@ -45,20 +45,6 @@ static void make_twin(const mm_seq_params* p, Twin* t) {
     for (int i = 0; i < n; i++)
       mpa_cache_thread(i, t->sc, MPA_FRONT_BACK + pl, cols, rows, t->px[pl].data(), t->py[pl].data(),
                        t->vip[pl].data());
-  }
-  const uint32_t sph_models = (1u << TANGENTIAL) | (1u << THREE_D_TRANSLATIONAL) | (1u << ROTATIONAL) |
-                              (1u << GEODESIC_X) | (1u << GEODESIC_Y) | (1u << GEODESIC_Z) | (1u << GEODESIC_CAMPOSE);
-  if (p->active_models & sph_models) {
-    const bool tan = p->active_models & (1u << TANGENTIAL);
-    for (int k = 0; k < 3; k++) {
-      t->sph[k].resize(n);
-      if (tan) t->tan3[k].resize(n);
-    }
-#pragma omp parallel for schedule(static)
-    for (int i = 0; i < n; i++)
-      sph_cache_thread(i, t->sc, cols, t->sph[0].data(), t->sph[1].data(), t->sph[2].data(),
-                       tan ? t->tan3[0].data() : nullptr, tan ? t->tan3[1].data() : nullptr,
-                       tan ? t->tan3[2].data() : nullptr);
   }
 }
 
@@ -71,22 +57,12 @@ static MpaCache cache_of(const Twin& t) {
   }
   c.cols = t.geo.W / 4;
   c.rows = t.geo.H / 4;
-  if (!t.sph[0].empty()) {
-    c.sx = t.sph[0].data();
-    c.sy = t.sph[1].data();
-    c.sz = t.sph[2].data();
-  }
-  if (!t.tan3[0].empty()) {
-    c.ta = t.tan3[0].data();
-    c.tse = t.tan3[1].data();
-    c.tce = t.tan3[2].data();
-  }
   return c;
 }
 
 static EpipoleMap epi_of(int n, const int32_t* e) {
   EpipoleMap m;
-  for (int i = 0; i < n; i++) m[{e[5 * i], e[5 * i + 1]}] = {e[5 * i + 2], e[5 * i + 3], e[5 * i + 4]};
+  for (int i = 0; i < n; i++) m.add({e[5 * i + 2], e[5 * i + 3], e[5 * i + 4]}, e[5 * i], e[5 * i + 1], true);
   return m;
 }
 
@@ -121,7 +97,7 @@ extern "C" int twin_reproject(const mm_seq_params* p, int n_epi, const int32_t* 
 
 // The device-planned prediction path (mm_devplan.h + mm_pipeline.h bodies), run sequentially.
 static int twin_pred_list(const Twin& t, const mmdev::PicTables& tab, const mm_pu_desc* pus, int n, int16_t* dy,
-                          int sdy, int16_t* dcb, int16_t* dcr, int sdc) {
+                          int sdy, int16_t* dcb, int16_t* dcr, int sdc, int hp = 0, int store = 3) {
   using namespace mmdev;
   std::vector<PuPlan> plans(n);
   PlanCounters cnt{};
@@ -134,8 +110,6 @@ static int twin_pred_list(const Twin& t, const mmdev::PicTables& tab, const mm_p
   }
   PlanMeta m;
   plan_meta(cnt, &m);
-  std::vector<PuDev> dpus(m.n_pus);
-  std::vector<int> pu_off(m.n_pus), pu_chunk(m.n_sb / 64 + 1);
   std::vector<JobDev> jobs(m.n_jobs);
   std::vector<int> job_off(m.n_jobs), job_chunk(m.n_elems / 64 + 1);
   for (int i = 0; i < n; i++) {
@@ -150,20 +124,19 @@ static int twin_pred_list(const Twin& t, const mmdev::PicTables& tab, const mm_p
       joff[k] = m.elem_base[key] + packed_elems(cnt.job_cur[key]);
       cnt.job_cur[key] += pack_count(1, pp.job[k].n);
     }
-    emit_pu(pus[i], pp, m.pu_base[pp.key] + packed_items(bp), m.sb_base[pp.key] + packed_elems(bp), jidx, joff,
-            dpus.data(), pu_off.data(), pu_chunk.data(), jobs.data(), job_off.data(), job_chunk.data());
+    emit_pu(pus[i], pp, m.sb_base[pp.key] + packed_elems(bp), jidx, joff, jobs.data(), job_off.data(),
+            job_chunk.data());
   }
   std::vector<BlockSetup> setups(m.n_jobs);
 #pragma omp parallel for schedule(static)
   for (int i = 0; i < m.n_jobs; i++) setup_thread(i, t.sc, jobs.data(), tab.ged, setups.data());
-  std::vector<mm_int4> lum[2];
-  std::vector<mm_int2> chr[2];
-  McIn mc;
+  std::vector<mm_int2> meta(std::max(m.n_sb, 1), mm_int2{});
+  std::vector<mm_int4> pos[2];
+  McRec mc;
+  mc.meta = meta.data();
   for (int l = 0; l < 2; l++) {
-    lum[l].assign(std::max(m.n_sb, 1), mm_int4{});
-    chr[l].assign(std::max(m.n_sb, 1), mm_int2{});
-    mc.lum[l] = lum[l].data();
-    mc.chr[l] = chr[l].data();
+    pos[l].assign(std::max(m.n_sb, 1), mm_int4{});
+    mc.pos[l] = pos[l].data();
   }
   MpaCache c = cache_of(t);
 #pragma omp parallel for schedule(static, 256)
@@ -171,9 +144,12 @@ static int twin_pred_list(const Twin& t, const mmdev::PicTables& tab, const mm_p
     reproj_thread_mc(g, find_item(job_off.data(), job_chunk.data(), g, m.n_jobs), t.sc, jobs.data(), job_off.data(),
                      setups.data(), c, mc);
   const Taps taps{LUMA_T, CHROMA_T, nullptr};
+  Geometry geo = t.geo;
+  geo.hp = hp;
+  geo.store = store;
 #pragma omp parallel for schedule(static, 256)
   for (int g = 0; g < m.n_sb; g++)
-    mc_thread_rec(g, sb_class(g, m.sb_base), t.geo, taps, mc, tab.ref, dy, sdy, dcb, dcr, sdc);
+    mc_thread_rec(g, sb_class(g, m.sb_base), geo, taps, mc, tab.ref, dy, sdy, dcb, dcr, sdc);
   return 0;
 }
 
@@ -197,6 +173,28 @@ extern "C" int twin_pred(const mm_seq_params* p, int n_epi, const int32_t* epi, 
   int rc = build_pic_tables(seq_info(*p), em, cur_poc, refs, &tab, &err);
   if (rc) return rc;
   return twin_pred_list(t, tab, pus, n, dy, sdy, dcb, dcr, sdc);
+}
+
+// mm_pred_list twin: one list of every PU, 14-bit (hp = 1) or clipped (hp = 0).
+extern "C" int twin_pred_list1(const mm_seq_params* p, int n_epi, const int32_t* epi, int cur_poc,
+                               const mm_pu_desc* pus, int n, int list, int hp, int n_refs, const int32_t* pocs,
+                               const int16_t* const* ys, const int16_t* const* cbs, const int16_t* const* crs,
+                               int stride_y, int stride_c, int16_t* dy, int sdy, int16_t* dcb, int16_t* dcr,
+                               int sdc) {
+  using namespace mmdev;
+  Twin t;
+  make_twin(p, &t);
+  EpipoleMap em = epi_of(n_epi, epi);
+  std::vector<std::pair<int, RefDev>> refs;
+  for (int i = 0; i < n_refs; i++)
+    refs.emplace_back(pocs[i], RefDev{ys[i], cbs ? cbs[i] : nullptr, crs ? crs[i] : nullptr, stride_y, stride_c});
+  std::sort(refs.begin(), refs.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+  PicTables tab;
+  std::string err;
+  int rc = build_pic_tables(seq_info(*p), em, cur_poc, refs, &tab, &err);
+  if (rc) return rc;
+  tab.only_list = list;
+  return twin_pred_list(t, tab, pus, n, dy, sdy, dcb, dcr, sdc, hp, 3);
 }
 
 // Host emulation of the device interior filter's tap-pair regrouping (mm_filter.h PackedTaps):

@@ -21,6 +21,9 @@ def load():
                                    c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int,
                                    c_void_p]
     lib.twin_mvp.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]
+    lib.twin_pred_list1.argtypes = [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
+                                    c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p,
+                                    c_int]
     lib.twin_sad_window.argtypes = [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
                                     c_void_p, c_int, c_void_p, c_int, c_void_p]
     return lib
@@ -62,6 +65,28 @@ def predict(params, cur_poc, pus, refs, W, H, epipoles=()):
                        c_void_p(dcr.ctypes.data), W // 2)
     if rc:
         raise RuntimeError(f"twin predict failed: {rc}")
+    return dy, dcb, dcr
+
+
+def predict_list(params, cur_poc, pus, list_, hp, refs, W, H, epipoles=()):
+    """mm_pred_list twin: list `list_` of every PU, 14-bit (hp) or clipped."""
+    lib = load()
+    pus = np.ascontiguousarray(pus)
+    pocs = sorted(refs)
+    arrs = [[np.ascontiguousarray(refs[p][k]) for p in pocs] for k in range(3)]
+    ptrs = [(c_void_p * len(pocs))(*[a.ctypes.data for a in arrs[k]]) for k in range(3)]
+    dy = np.zeros((H, W), dtype=np.int16)
+    dcb = np.zeros((H // 2, W // 2), dtype=np.int16)
+    dcr = np.zeros((H // 2, W // 2), dtype=np.int16)
+    pa = np.array(pocs, dtype=np.int32)
+    n_epi, ea = _epi(epipoles)
+    rc = lib.twin_pred_list1(ctypes.addressof(params), n_epi, c_void_p(ea.ctypes.data), cur_poc,
+                             c_void_p(pus.ctypes.data), len(pus), int(list_), int(hp), len(pocs),
+                             c_void_p(pa.ctypes.data), ptrs[0], ptrs[1], ptrs[2], arrs[0][0].shape[1],
+                             arrs[1][0].shape[1], c_void_p(dy.ctypes.data), W, c_void_p(dcb.ctypes.data),
+                             c_void_p(dcr.ctypes.data), W // 2)
+    if rc:
+        raise RuntimeError(f"twin predict_list failed: {rc}")
     return dy, dcb, dcr
 
 

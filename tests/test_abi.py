@@ -13,7 +13,7 @@ from helpers import ROOT
 
 def _header_functions():
     text = open(os.path.join(ROOT, "include", "mm360.h")).read()
-    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(mm_\w+)\(", text, re.M)))
+    return sorted(set(re.findall(r"^(?:int|void|const char\*|mm_epipole_list\*)\s+(mm_\w+)\(", text, re.M)))
 
 
 def test_header_and_binding_agree():
@@ -47,7 +47,7 @@ def test_struct_layouts_match_header():
     body = re.search(r"typedef struct mm_seq_params \{(.*?)\}", text, re.S).group(1)
     n_fields = sum(len(re.findall(r"\w+\s*(?:,|;)", l.split("/*")[0])) for l in body.splitlines() if ";" in l)
     assert ctypes.sizeof(mm360.SeqParams) == 4 * n_fields == 36
-    assert mm360.BLOCK_DTYPE.itemsize == 40 and mm360.PU_DTYPE.itemsize == 48
+    assert mm360.BLOCK_DTYPE.itemsize == 40 and mm360.PU_DTYPE.itemsize == 64
 
 
 def test_product_has_no_oracle_dependency():

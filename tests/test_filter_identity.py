@@ -84,3 +84,26 @@ def test_packed_tap_pair_regrouping_matches_scalar_filter():
     lib.twin_packed_taps_selftest.restype = ctypes.c_long
     lib.twin_packed_taps_selftest.argtypes = [ctypes.c_int]
     assert lib.twin_packed_taps_selftest(20000) == 0
+
+
+@pytest.mark.parametrize("bd", [8, 9, 10, 11, 12])
+def test_bcw_default_weighted_avg_equals_add_avg(bd):
+    """The kernels use AreaBuf<Pel>::addWeightedAvg (Buffer.cpp:398-424) for every bi sub-block;
+    with BCW_DEFAULT (w0 = w1 = 4) it must equal AreaBuf<Pel>::addAvg (Buffer.cpp:551-582)
+    exactly, over the whole range of 14-bit intermediates (int16)."""
+    rng = np.random.default_rng(bd)
+    p0 = np.concatenate([rng.integers(-32768, 32768, 400000), np.arange(-32768, 32768)]).astype(np.int64)
+    p1 = np.concatenate([rng.integers(-32768, 32768, 400000), np.arange(32767, -32769, -1)]).astype(np.int64)
+    s = frac_bits(bd)
+    maxv = (1 << bd) - 1
+    avg = np.clip((p0 + p1 + (1 << s) + 2 * 8192) >> (s + 1), 0, maxv)
+    sw = s + 3
+    wavg = np.clip((p0 * 4 + p1 * 4 + (1 << (sw - 1)) + (8192 << 3)) >> sw, 0, maxv)
+    assert np.array_equal(avg, wavg)
+
+
+def test_bcw_weight_nibbles():
+    """bcw_w1 (mm_pipeline.h) packs g_BcwWeights (Rom.cpp:203) as nibbles of w1 + 2."""
+    want = [-2, 3, 4, 5, 10]
+    got = [((0xC7650 >> (4 * i)) & 15) - 2 for i in range(5)]
+    assert got == want

@@ -265,15 +265,13 @@ def test_pred_device_resident_list_vs_oracle(cfg_name):
 
 def test_pred_stripes_do_not_change_results():
     """mm_set_stripes: the PU list cut into 1..7 stripes over two streams predicts the same picture
-    (== the oracle), and the lowest failing PU is still reported across stripes."""
+    (== the oracle), and the lowest failing PU is reported whichever stripe holds it (first, a
+    middle or the last stripe: every stripe reports into the picture's one status word)."""
     cfg = W.CONFIGS["C2"]
     params = mm360.seq_params(cfg.width, cfg.height, cfg.models)
     pus = W.pu_list(cfg, frame=7)
     refs = {poc: W.ref_planes(cfg.width, cfg.height, poc) for poc in W.REF_POCS}
     want = Oracle(params, EPI).predict(W.CUR_POC, pus, refs, cfg.width, cfg.height)
-    bad = pus.copy()
-    k_bad = len(pus) - 5  # lands in the last stripe
-    bad[k_bad]["x"] = 2
     with _ctx(params) as ctx:
         for poc, (y, cb, cr) in refs.items():
             ctx.upload_ref(poc, torch.from_numpy(y).cuda(), torch.from_numpy(cb).cuda(), torch.from_numpy(cr).cuda())
@@ -286,10 +284,76 @@ def test_pred_stripes_do_not_change_results():
             for x, t, name in zip(want, dst, ("y", "cb", "cr")):
                 got = t.cpu().numpy()
                 assert np.array_equal(got, x), (stripes, describe_mismatch(name, got, x))
-            ctx.predict_device(W.CUR_POC, mm360.pus_to_device(bad), *_planes(cfg))
-            assert ctx.status() == (mm360.MM_ERR_ARG, k_bad), stripes
+            for k_bad in (3, len(pus) // 2, len(pus) - 5):  # first / middle / last stripe
+                bad = pus.copy()
+                bad[k_bad]["x"] = 2
+                ctx.predict_device(W.CUR_POC, mm360.pus_to_device(bad), *_planes(cfg))
+                assert ctx.status() == (mm360.MM_ERR_ARG, k_bad), (stripes, k_bad)
+            # a clean picture after a failing one reports OK (the word was reset)
+            ctx.predict_device(W.CUR_POC, d_pus, *_planes(cfg))
+            assert ctx.status() == (mm360.MM_OK, -1), stripes
         with pytest.raises(mm360.MMError):
             ctx.set_stripes(0)
+
+
+def _upload(ctx, refs):
+    for poc, (y, cb, cr) in refs.items():
+        ctx.upload_ref(poc, torch.from_numpy(y).cuda(), torch.from_numpy(cb).cuda(), torch.from_numpy(cr).cuda())
+
+
+def test_pred_bcw_every_index_vs_oracle():
+    """Bi PUs with every BCW index (addWeightedAvg, Buffer.cpp:398-424, chosen at
+    InterPrediction.cpp:1596-1600) at C2 == the oracle; an index outside 0..4 is rejected."""
+    cfg = W.CONFIGS["C2"]
+    params = mm360.seq_params(cfg.width, cfg.height, cfg.models)
+    pus = W.pu_list(cfg, frame=4)
+    pus["bcw_idx"] = np.random.default_rng(4).integers(0, 5, len(pus))
+    bi = (pus["ref_poc"] >= 0).all(axis=1)
+    assert set(pus["bcw_idx"][bi].tolist()) == {0, 1, 2, 3, 4}
+    refs = {poc: W.ref_planes(cfg.width, cfg.height, poc) for poc in W.REF_POCS}
+    want = Oracle(params, EPI).predict(W.CUR_POC, pus, refs, cfg.width, cfg.height)
+    with _ctx(params) as ctx:
+        got = _gpu_predict(ctx, params, W.CUR_POC, pus, refs)
+        bad = pus.copy()
+        k = int(np.nonzero(bi)[0][10])
+        bad[k]["bcw_idx"] = 5
+        dst = _planes(cfg)
+        ctx.predict_device(W.CUR_POC, mm360.pus_to_device(bad), *dst)
+        assert ctx.status() == (mm360.MM_ERR_ARG, k)
+    for name, g, w in zip(("y", "cb", "cr"), got, want):
+        assert np.array_equal(g, w), describe_mismatch(name, g, w)
+
+
+@pytest.mark.parametrize("list_,hp", [(0, 1), (1, 1), (0, 0), (1, 0)])
+def test_pred_list_vs_oracle(list_, hp):
+    """mm_pred_list == xPredInterBlkMM 1:1 per list (InterPrediction.h:151-154): the 14-bit
+    bi=true intermediate (hp) or the clipped prediction of one list, at C2, bit-exact vs the
+    oracle; per-component calls (a NULL plane) leave the other component untouched."""
+    cfg = W.CONFIGS["C2"]
+    params = mm360.seq_params(cfg.width, cfg.height, cfg.models)
+    pus = W.pu_list(cfg, frame=5)
+    pus = pus[pus["ref_poc"][:, list_] >= 0]
+    refs = {poc: W.ref_planes(cfg.width, cfg.height, poc) for poc in W.REF_POCS}
+    want = Oracle(params, EPI).predict_list(W.CUR_POC, pus, list_, hp, refs, cfg.width, cfg.height)
+    with _ctx(params) as ctx:
+        _upload(ctx, refs)
+        dst = _planes(cfg)
+        ctx.predict_list(W.CUR_POC, pus, list_, hp, *dst)
+        for name, t, w in zip(("y", "cb", "cr"), dst, want):
+            got = t.cpu().numpy()
+            assert np.array_equal(got, w), describe_mismatch(name, got, w)
+        luma_only = _planes(cfg, -9)
+        ctx.predict_list(W.CUR_POC, pus, list_, hp, luma_only[0])
+        assert np.array_equal(luma_only[0].cpu().numpy(), want[0])
+        chroma_only = _planes(cfg, -9)
+        ctx.predict_list(W.CUR_POC, pus, list_, hp, None, chroma_only[1], chroma_only[2])
+        assert (chroma_only[0].cpu().numpy() == -9).all()
+        assert np.array_equal(chroma_only[1].cpu().numpy(), want[1])
+        assert np.array_equal(chroma_only[2].cpu().numpy(), want[2])
+        other = W.pu_list(cfg, frame=5)
+        miss = np.nonzero(other["ref_poc"][:, list_] < 0)[0]
+        with pytest.raises(mm360.MMError):  # a PU without the requested list
+            ctx.predict_list(W.CUR_POC, other[: miss[0] + 1], list_, hp, *_planes(cfg))
 
 
 def test_device_validation_reports_lowest_failing_pu():

@@ -62,7 +62,7 @@ def test_sad_window_centre_equals_uni_prediction_sad():
     blocks["sub_shift"] = 0
     sads = Oracle(params, EPI).sad_window(W.CUR_POC, blocks, 0, 16, refs, org)[:, 0]
     full = {poc: W.ref_planes(w, h, poc) for poc in W.REF_POCS}
-    pus = np.zeros(len(blocks), dtype=mm360.PU_DTYPE)
+    pus = mm360.new_pus(len(blocks))
     for i, b in enumerate(blocks):
         pus[i]["x"], pus[i]["y"], pus[i]["w"], pus[i]["h"] = b["x"], b["y"], b["w"], b["h"]
         pus[i]["mv"] = [[b["mv_hor"], b["mv_ver"]], [0, 0]]

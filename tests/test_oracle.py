@@ -140,3 +140,38 @@ def test_mpa_chroma_equals_luma_for_packet_blocks(w, h):
 def helpers_offsets(blocks):
     from helpers import block_offsets
     return block_offsets(blocks)
+
+
+@pytest.mark.parametrize("cfg_name", ["C1", "C2"])
+def test_twin_pred_bcw_matches_oracle(cfg_name):
+    """Every BCW index on bi PUs (addWeightedAvg, Buffer.cpp:398-424): the product's single
+    weighted form (CPU twin) == the oracle's addAvg / addWeightedAvg dispatch."""
+    cfg = W.CONFIGS[cfg_name]
+    params = mm360.seq_params(cfg.width, cfg.height, cfg.models)
+    pus = W.pu_list(cfg, frame=4)
+    pus["bcw_idx"] = np.random.default_rng(4).integers(0, 5, len(pus))
+    refs = {poc: W.ref_planes(cfg.width, cfg.height, poc) for poc in W.REF_POCS}
+    o = Oracle(params, EPI).predict(W.CUR_POC, pus, refs, cfg.width, cfg.height)
+    t = twin.predict(params, W.CUR_POC, pus, refs, cfg.width, cfg.height, EPI)
+    for name, a, b in zip("Y Cb Cr".split(), o, t):
+        assert np.array_equal(a, b), f"{name}: {(a != b).sum()} samples differ"
+    # the weights matter: the same list with BCW_DEFAULT predicts a different picture
+    plain = Oracle(params, EPI).predict(W.CUR_POC, W.pu_list(cfg, frame=4), refs, cfg.width, cfg.height)
+    assert not np.array_equal(plain[0], o[0])
+
+
+@pytest.mark.parametrize("list_,hp", [(0, 1), (1, 1), (0, 0), (1, 0)])
+def test_twin_pred_list_matches_oracle(list_, hp):
+    """mm_pred_list (xPredInterBlkMM 1:1 per list): the 14-bit bi=true intermediate (hp) or the
+    clipped uni prediction of one list of every PU."""
+    cfg = W.CONFIGS["C2"]
+    params = mm360.seq_params(cfg.width, cfg.height, cfg.models)
+    pus = W.pu_list(cfg, frame=5)
+    pus = pus[pus["ref_poc"][:, list_] >= 0]
+    refs = {poc: W.ref_planes(cfg.width, cfg.height, poc) for poc in W.REF_POCS}
+    o = Oracle(params, EPI).predict_list(W.CUR_POC, pus, list_, hp, refs, cfg.width, cfg.height)
+    t = twin.predict_list(params, W.CUR_POC, pus, list_, hp, refs, cfg.width, cfg.height, EPI)
+    for name, a, b in zip("Y Cb Cr".split(), o, t):
+        assert np.array_equal(a, b), f"{name}: {(a != b).sum()} samples differ"
+    if hp:  # 14-bit intermediates leave the 10-bit range
+        assert o[0].min() < 0 or o[0].max() > 1023

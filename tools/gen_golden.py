@@ -38,7 +38,7 @@ def pred_set(name, cfg_name):
     pus = W.pu_list(cfg)
     refs = {poc: W.ref_planes(cfg.width, cfg.height, poc) for poc in W.REF_POCS}
     y, cb, cr = Oracle(params, EPI).predict(W.CUR_POC, pus, refs, cfg.width, cfg.height)
-    np.savez_compressed(os.path.join(OUT, name), pus=pus.view(np.int32).reshape(-1, 12), y=y, cb=cb, cr=cr,
+    np.savez_compressed(os.path.join(OUT, name), pus=pus.view(np.int32).reshape(len(pus), -1)[:, :12], y=y, cb=cb, cr=cr,
                         mode=MODE)
     print(name, len(pus), y.shape)
 

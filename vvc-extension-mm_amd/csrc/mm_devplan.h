@@ -46,6 +46,7 @@ struct PicTables {
   int W, H, chroma;
   uint32_t active;
   int nf_mod4;             // (W/4 * H/4) % 4, frame-cache packet tail (MPA chroma aliasing)
+  int only_list;           // -1: normal prediction; 0/1: mm_pred_list of that list (other list ignored)
 };
 
 // Offsets of everything k_plan_place produced; written by k_plan_place's first thread.
@@ -55,12 +56,11 @@ struct PlanMeta {
   int job_base[N_JOB_KEYS], elem_base[N_JOB_KEYS];
 };
 
-// Device counters, zeroed before every picture.  64-bit words pack (items, elements) so one
-// atomic returns a consistent (index, offset) pair: lo 32 bits = count, hi 32 bits = elements.
+// Host-side bucket counters of the sequential planners (CPU twin).  64-bit words pack
+// (items, elements): lo 32 bits = count, hi 32 bits = elements.
 struct PlanCounters {
   unsigned long long pu_tot[N_PU_KEYS], pu_cur[N_PU_KEYS];
   unsigned long long job_tot[N_JOB_KEYS], job_cur[N_JOB_KEYS];
-  unsigned long long status;  // 0 = ok, else ~((pu_index << 8) | code) of the lowest failing PU
 };
 
 struct JobPlan {
@@ -73,6 +73,7 @@ struct PuPlan {
   int key;      // PU bucket (pu_key)
   int n_sb;     // luma 4x4 sub-blocks
   int slot[2];
+  int bcw;      // BCW weight index (bi), MM_BCW_DEFAULT otherwise
   JobPlan job[4];   // [2 * list + comp]; fixed slots keep the struct in registers
   int alias[2]; // list's chroma job aliases its luma job
 };
@@ -104,14 +105,19 @@ MM_HD void classify_pu(const mm_pu_desc& u, const PicTables& t, PuPlan* p) {
   p->n_sb = 0;
   p->slot[0] = p->slot[1] = -1;
   p->alias[0] = p->alias[1] = 0;
+  p->bcw = MM_BCW_DEFAULT;
   if (u.w < 4 || u.h < 4 || u.w > 128 || u.h > 128 || (u.w & 3) || (u.h & 3) || (u.x & 3) || (u.y & 3) || u.x < 0 ||
       u.y < 0 || u.x > t.W - u.w || u.y > t.H - u.h) {
     p->code = MM_ERR_ARG;
     return;
   }
+  if (t.only_list >= 0 && u.ref_poc[t.only_list] < 0) {  // mm_pred_list: the PU must use the list
+    p->code = MM_ERR_ARG;
+    return;
+  }
   int used = 0;
   for (int l = 0; l < 2; l++) {
-    if (u.ref_poc[l] < 0) continue;
+    if (u.ref_poc[l] < 0 || (t.only_list >= 0 && l != t.only_list)) continue;
     used++;
     const int m = u.model[l];
     if (m <= CLASSIC || m >= NUM_MODELS || !(t.active & (1u << m))) {
@@ -163,6 +169,13 @@ MM_HD void classify_pu(const mm_pu_desc& u, const PicTables& t, PuPlan* p) {
     return;
   }
   p->cls = (p->slot[0] >= 0 && p->slot[1] >= 0) ? 0 : (p->slot[0] >= 0 ? 1 : 2);
+  if (p->cls == 0) {  // CU::bcwIdx, Rom.cpp:203 g_BcwWeights[BCW_NUM]
+    if (u.bcw_idx < 0 || u.bcw_idx > 4) {
+      p->code = MM_ERR_ARG;
+      return;
+    }
+    p->bcw = u.bcw_idx;
+  }
   p->n_sb = (u.w / 4) * (u.h / 4);
   p->key = pu_key(p->cls, p->n_sb);
 }
@@ -205,20 +218,13 @@ MM_HD void write_chunks(int* chunk, int idx, int off, int n) {
   for (int e = (off + 63) & ~63; e < off + n; e += 64) chunk[e >> 6] = idx;
 }
 
-// Emit the PU at its placed position; job_idx/job_elem_off are the placed positions of the valid p.job[k].
-MM_HD void emit_pu(const mm_pu_desc& u, const PuPlan& p, int pu_idx, int sb_off, const int* job_idx,
-                   const int* job_elem_off, PuDev* pus, int* pu_off, int* pu_chunk, JobDev* jobs, int* job_off,
-                   int* job_chunk) {
-  PuDev d;
-  d.x = u.x;
-  d.y = u.y;
-  d.w = u.w;
-  d.h = u.h;
-  d.sb_offset = sb_off;
-  for (int l = 0; l < 2; l++) {
-    d.ref_slot[l] = p.slot[l];
-    d.job[l][0] = d.job[l][1] = -1;
-  }
+// Emit the jobs of the PU placed at luma sub-block offset sb_off; job_idx/job_elem_off are the
+// placed positions of the valid p.job[k].  The PU itself needs no record: its luma job of the
+// first used list writes the per-sub-block meta word k_mc reads (JobDev::meta_hi).
+MM_HD void emit_pu(const mm_pu_desc& u, const PuPlan& p, int sb_off, const int* job_idx, const int* job_elem_off,
+                   JobDev* jobs, int* job_off, int* job_chunk) {
+  const int primary = p.cls == 2 ? 1 : 0;
+  const int meta_hi = (p.slot[0] < 0 ? 0 : p.slot[0]) | ((p.slot[1] < 0 ? 0 : p.slot[1]) << 4) | (p.bcw << 8);
   for (int i = 0; i < 4; i++) {
     const JobPlan& jp = p.job[i];
     if (!jp.valid) continue;
@@ -240,16 +246,11 @@ MM_HD void emit_pu(const mm_pu_desc& u, const PuPlan& p, int pu_idx, int sb_off,
     j.list = jp.list;
     j.slot = p.slot[jp.list];
     j.alias = jp.comp == 0 ? p.alias[jp.list] : 0;
+    j.meta_hi = meta_hi | ((jp.comp == 0 && jp.list == primary) ? MM_META_PRIMARY : 0);
     jobs[job_idx[i]] = j;
     job_off[job_idx[i]] = job_elem_off[i];
     write_chunks(job_chunk, job_idx[i], job_elem_off[i], jp.n);
-    d.job[jp.list][jp.comp] = job_idx[i];
   }
-  for (int l = 0; l < 2; l++)
-    if (p.alias[l]) d.job[l][1] = d.job[l][0];
-  pus[pu_idx] = d;
-  pu_off[pu_idx] = sb_off;
-  write_chunks(pu_chunk, pu_idx, sb_off, p.n_sb);
 }
 
 }  // namespace mmdev

@@ -182,6 +182,8 @@ MM_HD void dmvr_decide_thread(int s, const SubPuDev* sp, const uint32_t* costs, 
   o.ref_poc[0] = u.ref_poc[0];
   o.ref_poc[1] = u.ref_poc[1];
   o.model[0] = o.model[1] = u.model;
+  o.bcw_idx = MM_BCW_DEFAULT;  // PU::checkDMVRCondition requires BCW_DEFAULT (UnitTools.cpp:1698-1726)
+  o.reserved[0] = o.reserved[1] = o.reserved[2] = 0;
   mvd[2 * s] = tdx;
   mvd[2 * s + 1] = tdy;
 }

@@ -27,19 +27,13 @@
 #include <vector>
 
 #include "../../include/mm360.h"
+#include "mm_effective.h"
 #include "mm_pipeline.h"
 #include "mm_plan.h"
 
-// Packet lanes of TAN / 3DT / ROT / GED read their sphere point from a frame-grid cache
-// (k_sph_cache).  Off by default: the 14-28 MB cache costs more in L2 / Infinity-Cache pressure
-// (k_reproj_dev +5 us, k_mc_dev +6 us at C3) than the 4 packet sin/cos per element it saves.
-#ifndef MM_SPH_CACHE
-#define MM_SPH_CACHE 0
-#endif
-
 using namespace mmpipe;
 
-#define MM_VERSION 100
+#define MM_VERSION 200
 
 namespace {
 
@@ -51,13 +45,6 @@ __global__ void k_mpa_cache(SeqConst sc, int plane, int cols, int rows, float* p
   int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= cols * rows) return;
   mpa_cache_thread(t, sc, plane, cols, rows, px, py, vip);
-}
-
-__global__ void k_sph_cache(SeqConst sc, int cols, int n, float* sx, float* sy, float* sz, float* ta, float* tse,
-                            float* tce) {
-  int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n) return;
-  sph_cache_thread(t, sc, cols, sx, sy, sz, ta, tse, tce);
 }
 
 __global__ void k_setup(SeqConst sc, const JobDev* __restrict__ jobs, int n_jobs, const M3* __restrict__ ged,
@@ -109,8 +96,10 @@ __device__ __forceinline__ int xcd_block() {
 constexpr int PLAN_BLOCK = 1024;
 constexpr int N_KEYS = N_PU_KEYS + N_JOB_KEYS;  // one row of `blk`: PU buckets, then job buckets
 
+// status: the picture's validation word (0 = ok, else ~((pu_index << 8) | code) of the lowest
+// failing PU, combined with atomicMax over every stripe of the picture).
 __global__ void __launch_bounds__(PLAN_BLOCK) k_plan_count(const mm_pu_desc* __restrict__ pus, int n, int pu_base,
-                                                    const PicTables t, PlanCounters* __restrict__ cnt,
+                                                    const PicTables t, unsigned long long* __restrict__ status,
                                                     unsigned long long* __restrict__ blk) {
   __shared__ unsigned long long s_cnt[N_KEYS], s_status;
   const int tid = threadIdx.x;
@@ -133,24 +122,24 @@ __global__ void __launch_bounds__(PLAN_BLOCK) k_plan_count(const mm_pu_desc* __r
   }
   __syncthreads();
   if (tid < N_KEYS) blk[(long)blockIdx.x * N_KEYS + tid] = s_cnt[tid];
-  if (tid == 0 && s_status) atomicMax(&cnt->status, s_status);
+  if (tid == 0 && s_status) atomicMax(status, s_status);
 }
 
-// `next` is the other counter set of the ping-pong pair: block 0 zeroes its status word for the
-// next picture, so no memset launch precedes k_plan_count.
+// `next_status` is the other word of the picture ping-pong pair: the first stripe's block 0 zeroes
+// it for the next picture, so no memset launch precedes k_plan_count.
 __global__ void __launch_bounds__(PLAN_BLOCK) k_plan_place(const mm_pu_desc* __restrict__ pus, int n, const PicTables t,
-                                                    PlanCounters* __restrict__ cnt, PlanCounters* __restrict__ next,
+                                                    unsigned long long* __restrict__ status,
+                                                    unsigned long long* __restrict__ next_status,
                                                     const unsigned long long* __restrict__ blk, int n_blocks,
-                                                    PlanMeta* __restrict__ meta,
-                                                    PlanCaps caps, PuDev* __restrict__ d_pus, int* __restrict__ pu_off,
-                                                    int* __restrict__ pu_chunk, JobDev* __restrict__ jobs,
-                                                    int* __restrict__ job_off, int* __restrict__ job_chunk) {
+                                                    PlanMeta* __restrict__ meta, PlanCaps caps,
+                                                    JobDev* __restrict__ jobs, int* __restrict__ job_off,
+                                                    int* __restrict__ job_chunk) {
   __shared__ unsigned long long s_pu[N_PU_KEYS], s_job[N_JOB_KEYS];
   __shared__ unsigned long long g_pu[N_PU_KEYS], g_job[N_JOB_KEYS];
   __shared__ PlanMeta s_meta;
   __shared__ int s_ok;
   const int tid = threadIdx.x;
-  if (blockIdx.x == 0 && tid == 0) next->status = 0ull;
+  if (blockIdx.x == 0 && tid == 0 && next_status) *next_status = 0ull;
   if (tid < N_PU_KEYS) s_pu[tid] = 0;
   if (tid < N_JOB_KEYS) s_job[tid] = 0;
   // bucket totals and this block's offsets inside the buckets: the column sums of blk, split over
@@ -234,7 +223,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK) k_plan_place(const mm_pu_desc* __r
       PlanMeta m = s_meta;
       if (!s_ok) {  // over capacity (overlapping PUs): nothing is predicted, the call fails
         m.n_pus = m.n_sb = m.n_jobs = m.n_elems = 0;
-        atomicMax(&cnt->status, status_word(0, MM_ERR_ARG));
+        atomicMax(status, status_word(0, MM_ERR_ARG));
       }
       *meta = m;
     }
@@ -258,7 +247,6 @@ __global__ void __launch_bounds__(PLAN_BLOCK) k_plan_place(const mm_pu_desc* __r
   }
   if (p.code != MM_OK) return;
   const unsigned long long bp = g_pu[p.key] + lp;
-  const int pu_idx = s_meta.pu_base[p.key] + packed_items(bp);
   const int sb_off = s_meta.sb_base[p.key] + packed_elems(bp);
   int jidx[4], joff[4];
 #pragma unroll
@@ -271,7 +259,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK) k_plan_place(const mm_pu_desc* __r
       joff[k] = s_meta.elem_base[key] + packed_elems(bj);
     }
   }
-  emit_pu(u, p, pu_idx, sb_off, jidx, joff, d_pus, pu_off, pu_chunk, jobs, job_off, job_chunk);
+  emit_pu(u, p, sb_off, jidx, joff, jobs, job_off, job_chunk);
 }
 
 // The 256 setups of a block are contiguous in `out`: each thread builds its BlockSetup in LDS and
@@ -298,7 +286,7 @@ __global__ void __launch_bounds__(256) k_setup_dev(SeqConst sc, const PlanMeta* 
 __global__ void __launch_bounds__(256) k_reproj_dev(SeqConst sc, const PlanMeta* __restrict__ meta,
                                                     const JobDev* __restrict__ jobs, const int* __restrict__ job_offsets,
                                                     const int* __restrict__ chunk_start,
-                                                    const BlockSetup* __restrict__ setups, MpaCache cache, McIn mc) {
+                                                    const BlockSetup* __restrict__ setups, MpaCache cache, McRec mc) {
   const int g = xcd_block() * blockDim.x + threadIdx.x;
   const int n_elems = meta->n_elems;
   if (g - (int)__lane_id() >= n_elems) return;  // whole wave past the end
@@ -310,15 +298,11 @@ __global__ void __launch_bounds__(256) k_reproj_dev(SeqConst sc, const PlanMeta*
 // The tap-pair tables (4 KB) are copied into LDS once per workgroup: every lane indexes them by
 // its own phase, and from __constant__ memory those lookups are ~16 vector loads per wave that
 // compete with the reference-window loads for the texture-address path.
-#ifndef MM_MC_LDS_TAPS
-#define MM_MC_LDS_TAPS 1
-#endif
-__global__ void __launch_bounds__(256) k_mc_dev(Geometry geo, const PlanMeta* __restrict__ meta, McIn mc,
+__global__ void __launch_bounds__(256) k_mc_dev(Geometry geo, const PlanMeta* __restrict__ meta, McRec mc,
                                                 const PicTables t, int16_t* __restrict__ dst_y, int dsy,
                                                 int16_t* __restrict__ dst_cb, int16_t* __restrict__ dst_cr, int dsc) {
   const int g = xcd_block() * blockDim.x + threadIdx.x;
   const int n_sb = meta->n_sb;
-#if MM_MC_LDS_TAPS
   __shared__ PackedTaps s_taps;
   static_assert(sizeof(PackedTaps) % 16 == 0 && sizeof(PackedTaps) / 16 <= 256, "one 16-byte word per thread");
   if (g - (int)threadIdx.x >= n_sb) return;  // whole workgroup past the end
@@ -326,9 +310,6 @@ __global__ void __launch_bounds__(256) k_mc_dev(Geometry geo, const PlanMeta* __
     reinterpret_cast<uint4*>(&s_taps)[threadIdx.x] = reinterpret_cast<const uint4*>(&c_packed_taps)[threadIdx.x];
   __syncthreads();
   const Taps taps{c_luma_taps, c_chroma_taps, &s_taps};
-#else
-  const Taps taps{c_luma_taps, c_chroma_taps, &c_packed_taps};
-#endif
   if (g >= n_sb) return;
   mc_thread_rec(g, sb_class(g, meta->sb_base), geo, taps, mc, t.ref, dst_y, dsy, dst_cb, dst_cr, dsc);
 }
@@ -498,32 +479,23 @@ struct DevBuf {
 
 // Buffers of one device-planned stripe of a picture.
 struct PlanSlot {
-  DevBuf<PuDev> pus;
-  DevBuf<int> pu_off, pu_chunk, job_off, job_chunk;
+  DevBuf<int> job_off, job_chunk;
   DevBuf<JobDev> jobs;
   DevBuf<BlockSetup> setup;
-  DevBuf<PlanCounters> cnt;  // ping-pong pair: a stripe reports in cnt[par] and zeroes the other's status
-  int cnt_par = 0;
   DevBuf<unsigned long long> blk;  // per-planning-block bucket counts (k_plan_count rows)
   DevBuf<PlanMeta> meta;
-  DevBuf<mm_int4> mc_lum[2];
-  DevBuf<mm_int2> mc_chr[2];
+  DevBuf<mm_int2> mc_meta;
+  DevBuf<mm_int4> mc_pos[2];
   PlanCaps caps{};
   void release() {
-    pus.release();
-    pu_off.release();
-    pu_chunk.release();
     job_off.release();
     job_chunk.release();
     jobs.release();
     setup.release();
-    cnt.release();
     blk.release();
     meta.release();
-    for (int l = 0; l < 2; l++) {
-      mc_lum[l].release();
-      mc_chr[l].release();
-    }
+    mc_meta.release();
+    for (int l = 0; l < 2; l++) mc_pos[l].release();
   }
 };
 
@@ -531,6 +503,12 @@ struct PlanSlot {
 #ifndef MM_DEFAULT_STRIPES
 #define MM_DEFAULT_STRIPES 1
 #endif
+
+// C-ABI handle of an EpipoleList: standalone (owned) or a context's own list
+struct mm_epipole_list {
+  mmepi::EpipoleList* l;
+  bool owned;
+};
 
 struct mm_ctx {
   mm_seq_params prm{};
@@ -540,18 +518,16 @@ struct mm_ctx {
   hipStream_t stream = nullptr;
   std::string err;
   std::map<int, RefHost> refs;
-  EpipoleMap epipoles;
+  EpipoleMap epipoles;                            // the context's EpipoleList (mm_epipole.h)
+  mm_epipole_list epi_handle{&epipoles, false};   // its C-ABI handle (mm_get_epipole_list)
   float* mpa_px[3] = {nullptr, nullptr, nullptr};
   float* mpa_py[3] = {nullptr, nullptr, nullptr};
   uint8_t* mpa_vip[3] = {nullptr, nullptr, nullptr};
-  float* sph[3] = {nullptr, nullptr, nullptr};   // frame-grid sphere points (k_sph_cache)
-  float* tan3[3] = {nullptr, nullptr, nullptr};  // TAN alpha / psin(eps) / pcos(eps)
   Plan plan;  // host plan of the parity API mm_reproject
   DevBuf<JobDev> d_jobs;
   DevBuf<int> d_job_off, d_job_chunk, d_pu_off, d_pu_chunk;
   DevBuf<BlockSetup> d_setup;
   DevBuf<int32_t> d_reproj;
-  DevBuf<PuDev> d_pus;
   DevBuf<M3> d_ged;
   // device-planned prediction (mm_pred_device / mm_pred_run)
   DevBuf<mm_pu_desc> d_pu_in;  // PU list copied in by mm_pred / mm_pred_prepare
@@ -559,7 +535,11 @@ struct mm_ctx {
   hipStream_t aux = nullptr;    // odd stripes run here, overlapping the even stripes' kernels
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int n_stripes = MM_DEFAULT_STRIPES;
-  std::vector<std::pair<PlanCounters*, int>> last_status;  // status words of the last picture's stripes
+  // validation status words, one per picture, ping-pong: a picture reports into d_status[pic_par]
+  // and its first stripe zeroes the other word for the next picture
+  DevBuf<unsigned long long> d_status;
+  int pic_par = 0;
+  unsigned long long* last_status = nullptr;  // word of the last device-planned picture
   int prep_poc = 0, prep_n = 0;
   bool prepared = false;
   bool status_pending = false;
@@ -611,16 +591,6 @@ static MpaCache make_cache(mm_ctx* c) {
   }
   mc.cols = c->geo.W / 4;
   mc.rows = c->geo.H / 4;
-#if MM_SPH_CACHE
-  mc.sx = c->sph[0];
-#else
-  mc.sx = nullptr;
-#endif
-  mc.sy = c->sph[1];
-  mc.sz = c->sph[2];
-  mc.ta = c->tan3[0];
-  mc.tse = c->tan3[1];
-  mc.tce = c->tan3[2];
   return mc;
 }
 
@@ -648,6 +618,26 @@ static int run_reproj_kernels(mm_ctx* c) {
 extern "C" {
 
 int mm_get_version(void) { return MM_VERSION; }
+
+int mm_derive_effective_blocks(const mm_tool_flags* tools, const mm_pu_motion* pus, int n, const mm_pu_desc* sub,
+                               mm_pu_desc* out_mc, int cap_mc, int* n_mc, mm_pu_desc* out_dmvr, int cap_dmvr,
+                               int* n_dmvr) {
+  if (!tools || n < 0 || (n > 0 && !pus) || !n_mc || !n_dmvr) return MM_ERR_ARG;
+  std::vector<mm_pu_desc> mc, dmvr;
+  mmeff::Deriver d(*tools, &mc, &dmvr);
+  for (int i = 0; i < n; i++) {
+    const int rc = d.run(pus[i], sub);
+    if (rc) return rc;
+  }
+  *n_mc = (int)mc.size();
+  *n_dmvr = (int)dmvr.size();
+  if ((int)mc.size() > cap_mc || (int)dmvr.size() > cap_dmvr || (!mc.empty() && !out_mc) ||
+      (!dmvr.empty() && !out_dmvr))
+    return MM_ERR_ARG;
+  std::copy(mc.begin(), mc.end(), out_mc);
+  std::copy(dmvr.begin(), dmvr.end(), out_dmvr);
+  return MM_OK;
+}
 
 const char* mm_last_error(mm_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
@@ -683,6 +673,8 @@ int mm_create(const mm_seq_params* p, int device, mm_ctx** out_ctx) {
   c->geo.maxCUhc = p->max_cu_height >> 1;
   c->geo.bd = p->bit_depth;
   c->geo.vec_store = 0;
+  c->geo.hp = 0;
+  c->geo.store = 3;
   if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
       hipEventCreate(&c->ev_stage[0]) != hipSuccess || hipEventCreate(&c->ev_stage[1]) != hipSuccess ||
       hipEventCreate(&c->ev_stage[2]) != hipSuccess ||
@@ -704,23 +696,8 @@ int mm_create(const mm_seq_params* p, int device, mm_ctx** out_ctx) {
     hipLaunchKernelGGL(k_mpa_cache, dim3((n + 255) / 256), dim3(256), 0, c->stream, c->sc, MPA_FRONT_BACK + pl, cols,
                        rows, c->mpa_px[pl], c->mpa_py[pl], c->mpa_vip[pl]);
   }
-  // Sphere points of the frame grid (+ TAN's per-point terms): the grid-only first step of the
-  // TAN / 3DT / ROT / GED array expressions, evaluated once per sequence (GridTerms)
-  const uint32_t sph_models = (1u << TANGENTIAL) | (1u << THREE_D_TRANSLATIONAL) | (1u << ROTATIONAL) |
-                              (1u << GEODESIC_X) | (1u << GEODESIC_Y) | (1u << GEODESIC_Z) | (1u << GEODESIC_CAMPOSE);
-  if (MM_SPH_CACHE && (p->active_models & sph_models)) {
-    const bool tan = p->active_models & (1u << TANGENTIAL);
-    for (int k = 0; k < 3; k++) {
-      if (hipMalloc(&c->sph[k], n * sizeof(float)) != hipSuccess ||
-          (tan && hipMalloc(&c->tan3[k], n * sizeof(float)) != hipSuccess)) {
-        mm_destroy(c);
-        return MM_ERR_HIP;
-      }
-    }
-    hipLaunchKernelGGL(k_sph_cache, dim3((n + 255) / 256), dim3(256), 0, c->stream, c->sc, cols, n, c->sph[0],
-                       c->sph[1], c->sph[2], c->tan3[0], c->tan3[1], c->tan3[2]);
-  }
-  if (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) {
+  if (c->d_status.ensure(2) != hipSuccess || hipMemsetAsync(c->d_status.p, 0, 2 * sizeof(unsigned long long), c->stream) != hipSuccess ||
+      hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) {
     mm_destroy(c);
     return MM_ERR_HIP;
   }
@@ -738,8 +715,6 @@ int mm_destroy(mm_ctx* c) {
     (void)hipFree(kv.second.cr);
   }
   for (int pl = 0; pl < 3; pl++) {
-    if (c->sph[pl]) (void)hipFree(c->sph[pl]);
-    if (c->tan3[pl]) (void)hipFree(c->tan3[pl]);
     if (c->mpa_px[pl]) (void)hipFree(c->mpa_px[pl]);
     if (c->mpa_py[pl]) (void)hipFree(c->mpa_py[pl]);
     if (c->mpa_vip[pl]) (void)hipFree(c->mpa_vip[pl]);
@@ -751,8 +726,8 @@ int mm_destroy(mm_ctx* c) {
   c->d_pu_chunk.release();
   c->d_setup.release();
   c->d_reproj.release();
-  c->d_pus.release();
   c->d_pu_in.release();
+  c->d_status.release();
   for (int k = 0; k < 2; k++) c->slot[k].release();
   c->d_ged.release();
   for (auto& kv : c->orgs) (void)hipFree(kv.second.y);
@@ -795,9 +770,53 @@ int mm_synchronize(mm_ctx* c) {
 
 int mm_set_epipole(mm_ctx* c, int cur, int ref, const int32_t q24[3]) {
   if (!c || !q24) return MM_ERR_ARG;
-  c->epipoles[{cur, ref}] = {q24[0], q24[1], q24[2]};
+  c->epipoles.add({q24[0], q24[1], q24[2]}, cur, ref, true);  // DecLib.cpp:2048, 3141: available
   return MM_OK;
 }
+
+// ---- EpipoleList (mm_epipole.h) ------------------------------------------------------------
+mm_epipole_list* mm_epipole_list_create(void) { return new mm_epipole_list{new mmepi::EpipoleList(), true}; }
+
+void mm_epipole_list_destroy(mm_epipole_list* e) {
+  if (!e || !e->owned) return;  // a context's list lives and dies with the context
+  delete e->l;
+  delete e;
+}
+
+mm_epipole_list* mm_get_epipole_list(mm_ctx* c) { return c ? &c->epi_handle : nullptr; }
+
+int mm_epipole_add(mm_epipole_list* e, int cur, int ref, const int32_t q24[3], int make_available) {
+  if (!e || !q24) return MM_ERR_ARG;
+  e->l->add({q24[0], q24[1], q24[2]}, cur, ref, make_available != 0);
+  return MM_OK;
+}
+
+int mm_epipole_make_available(mm_epipole_list* e, int cur) {
+  if (!e) return MM_ERR_ARG;
+  e->l->make_available(cur);
+  return MM_OK;
+}
+
+int mm_epipole_has(mm_epipole_list* e, int cur, int ref) { return e && e->l->has(cur, ref) ? 1 : 0; }
+
+int mm_epipole_find(mm_epipole_list* e, int cur, int ref, int32_t q24[3]) {
+  if (!e || !q24) return MM_ERR_ARG;
+  mmepi::Q3 q;
+  if (!e->l->find(cur, ref, &q)) return MM_ERR_NOEPIPOLE;
+  for (int i = 0; i < 3; i++) q24[i] = q[i];
+  return MM_OK;
+}
+
+int mm_epipole_derive_predictor(mm_epipole_list* e, int cur, int32_t q24[3]) {
+  if (!e || !q24) return MM_ERR_ARG;
+  mmepi::Q3 q;
+  const int rc = e->l->derive_predictor(cur, &q);
+  if (rc) return rc;
+  for (int i = 0; i < 3; i++) q24[i] = q[i];
+  return MM_OK;
+}
+
+int mm_epipole_count(mm_epipole_list* e) { return e ? e->l->count() : -1; }
 
 int mm_upload_ref(mm_ctx* c, int poc, const int16_t* y, ptrdiff_t sy, const int16_t* cb, const int16_t* cr,
                   ptrdiff_t sc_, int src_dev) {
@@ -868,57 +887,44 @@ static int ensure_slot_buffers(mm_ctx* c, PlanSlot& S, int n) {
   k.sb = (int)std::min<long>((long)n * 1024, area_sb);
   k.elems = 4 * k.sb;
   S.caps = k;
-  HIPCHK(c, S.pus.ensure(k.pus));
-  HIPCHK(c, S.pu_off.ensure(k.pus));
-  HIPCHK(c, S.pu_chunk.ensure(k.sb / 64 + 1));
   HIPCHK(c, S.jobs.ensure(k.jobs));
   HIPCHK(c, S.job_off.ensure(k.jobs));
   HIPCHK(c, S.job_chunk.ensure(k.elems / 64 + 1));
   HIPCHK(c, S.setup.ensure(k.jobs));
-  if (!S.cnt.p) {
-    HIPCHK(c, S.cnt.ensure(2));
-    HIPCHK(c, hipMemsetAsync(S.cnt.p, 0, 2 * sizeof(PlanCounters), c->stream));  // once per context
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-  }
   HIPCHK(c, S.meta.ensure(1));
   HIPCHK(c, S.blk.ensure((size_t)((n + PLAN_BLOCK - 1) / PLAN_BLOCK) * N_KEYS));
-  for (int l = 0; l < 2; l++) {
-    HIPCHK(c, S.mc_lum[l].ensure(k.sb));
-    HIPCHK(c, S.mc_chr[l].ensure(k.sb));
-  }
+  HIPCHK(c, S.mc_meta.ensure(k.sb));
+  for (int l = 0; l < 2; l++) HIPCHK(c, S.mc_pos[l].ensure(k.sb));
   return MM_OK;
 }
 
 // One stripe (PUs [base, base + n) of the picture's list) through k_plan_count + k_plan_place +
 // k_setup_dev + k_reproj_dev + k_mc_dev on `st`.  Stage events only in single-stripe timing mode.
+// status: the picture's status word; next_status (first stripe only): the word to zero for the
+// next picture.
 static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables& t, const Geometry& geo,
-                         const mm_pu_desc* d_in, int n, int base, int16_t* dy, ptrdiff_t sdy, int16_t* dcb,
-                         int16_t* dcr, ptrdiff_t sdc) {
+                         const mm_pu_desc* d_in, int n, int base, unsigned long long* status,
+                         unsigned long long* next_status, int16_t* dy, ptrdiff_t sdy, int16_t* dcb, int16_t* dcr,
+                         ptrdiff_t sdc) {
   const PlanCaps& k = S.caps;
   const int gp = (n + PLAN_BLOCK - 1) / PLAN_BLOCK;
   const int gs = (k.jobs + 255) / 256;
   const int gr = round_grid((k.elems + 255) / 256);
   const int gm = round_grid((k.sb + 255) / 256);
-  PlanCounters* cnt = S.cnt.p + S.cnt_par;
-  PlanCounters* next = S.cnt.p + (S.cnt_par ^ 1);
-  hipLaunchKernelGGL(k_plan_count, dim3(gp), dim3(PLAN_BLOCK), 0, st, d_in, n, base, t, cnt, S.blk.p);
-  hipLaunchKernelGGL(k_plan_place, dim3(gp), dim3(PLAN_BLOCK), 0, st, d_in, n, t, cnt, next, S.blk.p, gp, S.meta.p, k,
-                     S.pus.p, S.pu_off.p, S.pu_chunk.p, S.jobs.p, S.job_off.p, S.job_chunk.p);
+  hipLaunchKernelGGL(k_plan_count, dim3(gp), dim3(PLAN_BLOCK), 0, st, d_in, n, base, t, status, S.blk.p);
+  hipLaunchKernelGGL(k_plan_place, dim3(gp), dim3(PLAN_BLOCK), 0, st, d_in, n, t, status, next_status, S.blk.p, gp,
+                     S.meta.p, k, S.jobs.p, S.job_off.p, S.job_chunk.p);
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[0], st));
   hipLaunchKernelGGL(k_setup_dev, dim3(gs), dim3(256), 0, st, c->sc, S.meta.p, S.jobs.p, t, S.setup.p);
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[1], st));
-  McIn mc;
-  for (int l = 0; l < 2; l++) {
-    mc.lum[l] = S.mc_lum[l].p;
-    mc.chr[l] = S.mc_chr[l].p;
-  }
+  McRec mc;
+  mc.meta = S.mc_meta.p;
+  for (int l = 0; l < 2; l++) mc.pos[l] = S.mc_pos[l].p;
   hipLaunchKernelGGL(k_reproj_dev, dim3(gr), dim3(256), 0, st, c->sc, S.meta.p, S.jobs.p, S.job_off.p, S.job_chunk.p,
                      S.setup.p, make_cache(c), mc);
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[2], st));
   hipLaunchKernelGGL(k_mc_dev, dim3(gm), dim3(256), 0, st, geo, S.meta.p, mc, t, dy, (int)sdy, dcb, dcr, (int)sdc);
   HIPCHK(c, hipGetLastError());
-  c->last_status.emplace_back(cnt, base);
-  S.cnt_par ^= 1;
   return MM_OK;
 }
 
@@ -926,10 +932,12 @@ static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables
 // into n_stripes contiguous stripes; even stripes run on the context stream with slot 0, odd ones
 // on the auxiliary stream with slot 1, so one stripe's latency-bound planning kernels overlap the
 // other's interpolation.  PUs write disjoint samples, so stripes are independent; the auxiliary
-// stream forks from and joins back into the context stream.  Validation errors are deferred to
-// mm_pred_status.
+// stream forks from and joins back into the context stream.  Validation errors of every stripe
+// go to the picture's status word and are reported by mm_pred_status.
+// only_list / hp / store: mm_pred_list (-1 / 0 / 3 for the normal prediction).
 static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, int n, int16_t* dy, ptrdiff_t sdy,
-                              int16_t* dcb, int16_t* dcr, ptrdiff_t sdc) {
+                              int16_t* dcb, int16_t* dcr, ptrdiff_t sdc, int only_list = -1, int hp = 0,
+                              int store = 3) {
   std::vector<std::pair<int, RefDev>> refs;
   for (auto& kv : c->refs)
     refs.emplace_back(kv.first, RefDev{kv.second.y, kv.second.cb, kv.second.cr, kv.second.stride_y, kv.second.stride_c});
@@ -937,13 +945,17 @@ static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, in
   std::string err;
   int rc = build_pic_tables(seq_info(c->prm), c->epipoles, cur_poc, refs, &t, &err);
   if (rc) return fail(c, rc, err);
+  t.only_list = only_list;
   Geometry geo = c->geo;
-  geo.vec_store = ((uintptr_t)dy % 8 == 0) && (sdy % 4 == 0) &&
-                  (!geo.chroma || ((uintptr_t)dcb % 4 == 0 && (uintptr_t)dcr % 4 == 0 && sdc % 2 == 0));
+  geo.hp = hp;
+  geo.store = store;
+  geo.vec_store = (!dy || ((uintptr_t)dy % 8 == 0 && sdy % 4 == 0)) &&
+                  (!geo.chroma || !dcb || ((uintptr_t)dcb % 4 == 0 && (uintptr_t)dcr % 4 == 0 && sdc % 2 == 0));
   const int K = c->stage_timing ? 1 : std::max(1, std::min(c->n_stripes, (n + PLAN_BLOCK - 1) / PLAN_BLOCK));
   const int per = (n + K - 1) / K;
   for (int s = 0; s < std::min(K, 2); s++) RCCHK(ensure_slot_buffers(c, c->slot[s], per));
-  c->last_status.clear();
+  unsigned long long* status = c->d_status.p + c->pic_par;
+  unsigned long long* next_status = c->d_status.p + (c->pic_par ^ 1);
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
   if (K > 1) {
     HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
@@ -952,14 +964,16 @@ static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, in
   for (int s = 0; s < K; s++) {
     const int base = s * per, m = std::min(per, n - base);
     if (m <= 0) break;
-    RCCHK(launch_stripe(c, c->slot[s & 1], (s & 1) ? c->aux : c->stream, t, geo, d_in + base, m, base, dy, sdy, dcb,
-                        dcr, sdc));
+    RCCHK(launch_stripe(c, c->slot[s & 1], (s & 1) ? c->aux : c->stream, t, geo, d_in + base, m, base, status,
+                        s == 0 ? next_status : nullptr, dy, sdy, dcb, dcr, sdc));
   }
   if (K > 1) {
     HIPCHK(c, hipEventRecord(c->ev_join, c->aux));
     HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
   }
   HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+  c->last_status = status;
+  c->pic_par ^= 1;
   c->status_pending = true;
   return MM_OK;
 }
@@ -976,17 +990,14 @@ static int read_status(mm_ctx* c, int* first_bad) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (!c->status_pending) return MM_OK;
   c->status_pending = false;
-  unsigned long long w = 0;  // the stripes' status words combine like the per-PU atomicMax
-  for (const auto& st : c->last_status) {
-    unsigned long long v = 0;
-    HIPCHK(c, hipMemcpy(&v, &st.first->status, sizeof(v), hipMemcpyDeviceToHost));
-    w = std::max(w, v);
-  }
+  unsigned long long w = 0;
+  HIPCHK(c, hipMemcpy(&w, c->last_status, sizeof(w), hipMemcpyDeviceToHost));
   if (!w) return MM_OK;
   const unsigned long long v = ~w;
   const int code = (int)(v & 0xff), pu = (int)(v >> 8);
   if (first_bad) *first_bad = pu;
-  static const char* what[] = {"ok", "PU outside the picture, not 4x4 aligned or using no list, or the list covers more than the picture",
+  static const char* what[] = {"ok", "PU outside the picture, not 4x4 aligned, using no (or not the requested) list, "
+                                     "invalid BCW index, or the list covers more than the picture",
                                "HIP error", "reference POC not uploaded", "no epipole for (curPOC, refPOC)",
                                "invalid, CLASSIC or inactive motion model", "no device"};
   return fail(c, code, "PU " + std::to_string(pu) + ": " + (code >= 0 && code <= 6 ? what[code] : "error"));
@@ -1028,6 +1039,20 @@ int mm_pred(mm_ctx* c, int cur_poc, const mm_pu_desc* pus, int n, int16_t* dy, p
             int16_t* dcr, ptrdiff_t sdc) {
   RCCHK(mm_pred_prepare(c, cur_poc, pus, n));
   RCCHK(mm_pred_run(c, dy, sdy, dcb, dcr, sdc));
+  return read_status(c, nullptr);
+}
+
+int mm_pred_list(mm_ctx* c, int cur_poc, const mm_pu_desc* pus, int n, int list, int hp, int16_t* dy, ptrdiff_t sdy,
+                 int16_t* dcb, int16_t* dcr, ptrdiff_t sdc) {
+  if (!c || n < 0 || (n > 0 && !pus) || (list != 0 && list != 1) || (hp != 0 && hp != 1)) return MM_ERR_ARG;
+  const bool want_c = c->geo.chroma && dcb && dcr;
+  if (!dy && !want_c) return MM_ERR_ARG;
+  if ((dcb == nullptr) != (dcr == nullptr)) return MM_ERR_ARG;
+  if (n == 0) return MM_OK;
+  RCCHK(mm_pred_prepare(c, cur_poc, pus, n));
+  c->prepared = false;  // the buffer now holds this list call's PUs, not a prepared picture
+  RCCHK(launch_device_plan(c, cur_poc, c->d_pu_in.p, n, dy, sdy, dcb, dcr, sdc, list, hp,
+                           (dy ? 1 : 0) | (want_c ? 2 : 0)));
   return read_status(c, nullptr);
 }
 
@@ -1176,18 +1201,22 @@ int mm_filter(mm_ctx* c, int comp, int vertical, const int16_t* src, ptrdiff_t s
   if (frac < 0 || frac >= (comp ? 32 : 16)) return fail(c, MM_ERR_ARG, "invalid fraction");
   if (!vertical && !is_first) return fail(c, MM_ERR_ARG, "filterHor is always isFirst");
   HIPCHK(c, hipSetDevice(c->device));
-  const int NT = comp ? 4 : 8, m = NT / 2;
-  const int ww = w + 2 * m, hh = h + 2 * m;
+  // Window the filter reads (InterpolationFilter.cpp:540-644): (NT/2 - 1) samples before the block
+  // and NT/2 after it along the filtered axis only (mm360.h states this margin to callers).
+  const int NT = comp ? 4 : 8, before = NT / 2 - 1, after = NT / 2;
+  const int mx0 = vertical ? 0 : before, mx1 = vertical ? 0 : after;
+  const int my0 = vertical ? before : 0, my1 = vertical ? after : 0;
+  const int ww = w + mx0 + mx1, hh = h + my0 + my1;
   std::vector<int16_t> win((size_t)ww * hh);
   for (int r = 0; r < hh; r++)
-    for (int q = 0; q < ww; q++) win[(size_t)r * ww + q] = src[(long)(r - m) * src_stride + (q - m)];
+    for (int q = 0; q < ww; q++) win[(size_t)r * ww + q] = src[(long)(r - my0) * src_stride + (q - mx0)];
   int16_t *dsrc = nullptr, *ddst = nullptr;
   HIPCHK(c, hipMalloc(&dsrc, win.size() * 2));
   hipError_t e = hipMalloc(&ddst, (size_t)w * h * 2);
   if (e == hipSuccess) e = hipMemcpy(dsrc, win.data(), win.size() * 2, hipMemcpyHostToDevice);
   if (e == hipSuccess) {
     hipLaunchKernelGGL(k_filter, dim3((w * h + 255) / 256), dim3(256), 0, c->stream, comp, vertical,
-                       dsrc + (size_t)m * ww + m, ww, ddst, w, w, h, frac, is_first, is_last, c->geo.bd);
+                       dsrc + (size_t)my0 * ww + mx0, ww, ddst, w, w, h, frac, is_first, is_last, c->geo.bd);
     e = hipGetLastError();
   }
   std::vector<int16_t> out((size_t)w * h);

@@ -339,19 +339,8 @@ MM_HD void block_setup_f(BlockSetup* b, const SeqConst& s, int model, bool luma,
 // <Model>::modelMotion[Cached] of one element: the moved position as computed (before the NaN
 // fallback, offset removal and rounding).  CLASSIC (TranslationalMotionModel::modelMotion,
 // TranslationalMotionModel.cpp:8-13) adds the MV.
-// Per-grid-point terms of the block's array expressions that depend on the element's grid
-// position only, precomputed once per sequence for the whole frame grid with packet math
-// (k_sph_cache).  Valid for packet lanes only: a tail lane computes them with scalar libm.
-struct GridTerms {
-  int have_p;    // p = EquirectangularProjection::toSphere(grid)   (TAN/3DT/ROT/GED first step)
-  int have_tan;  // TAN: alpha = phi(p), se/ce = psin/pcos(pi/2 - theta(p))  (TangentialMotionModel.cpp:21-29)
-  V3 p;
-  float alpha, se, ce;
-};
-
 MM_HD void model_motion_element(const SeqConst& s, const BlockSetup& b, float gx, float gy, bool packet,
-                                bool mpa_cached, float pers_x, float pers_y, bool pers_vip, float* omx, float* omy,
-                                const GridTerms* gt = nullptr) {
+                                bool mpa_cached, float pers_x, float pers_y, bool pers_vip, float* omx, float* omy) {
   const Math m{packet};
   if (b.model == CLASSIC) {
     *omx = gx + b.mvx;
@@ -366,12 +355,8 @@ MM_HD void model_motion_element(const SeqConst& s, const BlockSetup& b, float gx
   // Every model ends in EquirectangularProjection::fromSphere of a moved sphere point q; the
   // switch computes q and the shared tail projects it (one copy of the acosf/atan2f code).
   const bool mpa = b.model >= MPA_FRONT_BACK && b.model <= MPA_TOP_BOTTOM;
-  const bool tan_cached = gt && gt->have_tan;
   V3 p = {0.0f, 0.0f, 0.0f};  // toSphere(grid) of TAN / 3DT / ROT / GED
-  if (gt && gt->have_p)
-    p = gt->p;
-  else if (!mpa && !tan_cached)
-    p = erp_to_sphere(gx, gy, s, m);
+  if (!mpa) p = erp_to_sphere(gx, gy, s, m);
   V3 q;
   switch (b.model) {
     case MPA_FRONT_BACK:
@@ -399,18 +384,11 @@ MM_HD void model_motion_element(const SeqConst& s, const BlockSetup& b, float gx
         q = {c.z, c.y, -c.x};
     } break;
     case TANGENTIAL: {  // TangentialMotionModel.cpp:8-48
-      float alpha, se, ce;
-      if (tan_cached) {
-        alpha = gt->alpha;
-        se = gt->se;
-        ce = gt->ce;
-      } else {
-        V3 sp = cart_to_sph(p, m, true);
-        float eps = PI_2_F - sp.y;
-        alpha = sp.z;
-        se = m.sin(eps);
-        ce = m.cos(eps);
-      }
+      const V3 sp = cart_to_sph(p, m, true);
+      const float eps = PI_2_F - sp.y;
+      const float alpha = sp.z;
+      const float se = m.sin(eps);
+      const float ce = m.cos(eps);
       float dA = alpha - b.alphaC;
       float cdA = m.cos(dA);
       float cosPsi = b.sE * se + (b.cE * ce) * cdA;
@@ -449,9 +427,9 @@ MM_HD void model_motion_element(const SeqConst& s, const BlockSetup& b, float gx
 
 MM_HD void reproject_element(const SeqConst& s, const BlockSetup& b, float gx, float gy, bool packet,
                              bool mpa_cached, float pers_x, float pers_y, bool pers_vip,
-                             int chroma_shift, int32_t* fx, int32_t* fy, const GridTerms* gt = nullptr) {
+                             int chroma_shift, int32_t* fx, int32_t* fy) {
   float mx, my;
-  model_motion_element(s, b, gx, gy, packet, mpa_cached, pers_x, pers_y, pers_vip, &mx, &my, gt);
+  model_motion_element(s, b, gx, gy, packet, mpa_cached, pers_x, pers_y, pers_vip, &mx, &my);
   // NaN -> unmoved (MVReprojection.cpp:151-154), remove offset, rescale, round to fixed point
   if (isnanf_(mx) || isnanf_(my)) {
     mx = gx;

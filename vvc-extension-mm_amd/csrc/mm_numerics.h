@@ -21,17 +21,9 @@
 #define MM_HD __host__ __device__ __forceinline__
 #define MM_HD_CONST __device__ __constant__
 // Rare paths (huge-argument reductions, double-double fallbacks, scalar libm for Eigen tail
-// lanes).  MM_COLD_NOINLINE=1 keeps them out of line (4-5x smaller kernels), but the calls cost
-// more than the instruction-cache misses they save (measured: k_reproj_dev +10 us at C3), so
-// they are inlined by default.
-#ifndef MM_COLD_NOINLINE
-#define MM_COLD_NOINLINE 0
-#endif
-#if MM_COLD_NOINLINE
-#define MM_HD_COLD __host__ __device__ __attribute__((noinline))
-#else
+// lanes).  Inlined: out-of-line calls measured slower than the instruction-cache misses they save
+// (k_reproj_dev +10 us at C3).
 #define MM_HD_COLD __host__ __device__ __forceinline__
-#endif
 #else
 #define MM_HD inline
 #define MM_HD_CONST static const

@@ -27,9 +27,10 @@ struct alignas(16) JobDev {
   int n;        // elements = (cw/sbw)*(ch/sbh)
   int rows;     // ch/sbh (Eigen column-major rows)
   int offset;   // first element in the result array
-  // device-planned prediction: where k_mc finds this job's results (McIn, one record per luma
+  // device-planned prediction: where k_mc finds this job's results (McRec, one record per luma
   // 4x4 sub-block of the PU, row-major from sb_base)
   int sb_base, pu_cols;
+  int meta_hi;      // McRec meta word .y of the PU (slots, BCW) | MM_META_PRIMARY if this job writes it
   int16_t model;
   int16_t ged_idx;  // index into the GED rotation table (-1 if not GED)
   int8_t comp;      // 0 luma, 1 chroma (4:2:0)
@@ -38,79 +39,37 @@ struct alignas(16) JobDev {
 };
 static_assert(sizeof(JobDev) == 64, "JobDev is four 16-byte words");
 
-// Per-luma-sub-block inputs of k_mc, written by the reprojection of a device-planned picture so
-// that k_mc reads them with one coalesced load per list instead of chasing PU -> job -> result:
-// lum[l][g] = (xPos/xFrac fixed point X, Y, PU id << 5 | reference slot, oy << 16 | ox) and chr[l][g] = the
-// chroma X, Y (1/32 pel) of list l for luma sub-block g.
 struct alignas(16) mm_int4 {
   int x, y, z, w;
 };
 struct alignas(8) mm_int2 {
   int x, y;
 };
-struct McIn {
-  mm_int4* lum[2];
-  mm_int2* chr[2];
+// Per-luma-sub-block inputs of k_mc, written by the reprojection of a device-planned picture in
+// the order k_mc reads them (sub-block g of the class-sorted enumeration):
+//   meta[g]   = (ox | oy << 16, slot0 | slot1 << 4 | bcw << 8): output position of the luma 4x4
+//               sub-block, reference slot per list, BCW index -- written by the PU's primary job;
+//   pos[l][g] = (luma X, luma Y in 1/16 pel, chroma X, Y in 1/32 pel) of list l: the luma job
+//               writes .xy, the chroma job (or the aliasing MPA luma job) .zw.
+// A bi sub-block is 40 bytes, read with one 8-byte and two 16-byte loads.
+struct McRec {
+  mm_int2* meta;
+  mm_int4* pos[2];
 };
+#define MM_META_PRIMARY (1 << 16)
 
-struct alignas(16) PuDev {  // 48 bytes: three 16-byte words
-  int x, y, w, h;
-  int ref_slot[2];  // -1 = list unused
-  int job[2][2];    // [list][comp] -> job index
-  int sb_offset;    // first luma sub-block of this PU in the k_mc enumeration
-};
+// w1 = g_BcwWeights[bcw] (Rom.cpp:203 {-2, 3, 4, 5, 10}) as nibbles of w1 + 2; w0 = 8 - w1
+MM_HD int bcw_w1(int bcw) { return (int)((0xC7650u >> (4 * bcw)) & 15u) - 2; }
 
-// Frame-grid caches, row-major [j][i] over the (W/4) x (H/4) grid x = 4i + off, y = 4j + off:
-//  * MPA perspective coordinates per plane (MotionPlaneAdaptiveMotionModel::fillCache);
-//  * the sphere point of every grid position and TAN's per-point terms (GridTerms), packet math,
-//    used by packet lanes of TAN / 3DT / ROT / GED blocks (null when no such model is active).
+// MVReprojection::fillCache's frame grid, MPA perspective coordinates per plane
+// (MotionPlaneAdaptiveMotionModel::fillCache), row-major [j][i] over the (W/4) x (H/4) grid
+// x = 4i + off, y = 4j + off.
 struct MpaCache {
   const float* px[3];
   const float* py[3];
   const uint8_t* vip[3];
   int cols, rows;  // W/4, H/4
-  const float* sx;
-  const float* sy;
-  const float* sz;
-  const float* ta;   // TAN alpha
-  const float* tse;  // TAN psin(eps)
-  const float* tce;  // TAN pcos(eps)
 };
-
-// k_sph_cache: GridTerms of grid point t (packet math, as every element of an N % 4 == 0 block)
-MM_HD void sph_cache_thread(int t, const SeqConst& sc, int cols, float* sx, float* sy, float* sz, float* ta, float* tse,
-                            float* tce) {
-  const int j = t / cols, i = t - j * cols;
-  const Math m{1};
-  const V3 p = erp_to_sphere(4.0f * (float)i + sc.off, 4.0f * (float)j + sc.off, sc, m);
-  sx[t] = p.x;
-  sy[t] = p.y;
-  sz[t] = p.z;
-  if (ta) {
-    const V3 sp = cart_to_sph(p, m, true);
-    const float eps = PI_2_F - sp.y;
-    ta[t] = sp.z;
-    tse[t] = m.sin(eps);
-    tce[t] = m.cos(eps);
-  }
-}
-
-// Grid terms of element (row, col) of job j when it is a packet lane and the caches hold them.
-MM_HD void load_grid_terms(const MpaCache& cache, const JobDev& j, int row, int col, bool packet, GridTerms* gt) {
-  gt->have_p = gt->have_tan = 0;
-  if (!packet || !cache.sx) return;
-  const int ci = ((j.y >> 2) + row) * cache.cols + (j.x >> 2) + col;
-  if (j.model == TANGENTIAL) {
-    if (!cache.ta) return;
-    gt->have_tan = 1;
-    gt->alpha = cache.ta[ci];
-    gt->se = cache.tse[ci];
-    gt->ce = cache.tce[ci];
-  } else if (j.model >= THREE_D_TRANSLATIONAL && j.model <= GEODESIC_CAMPOSE) {
-    gt->have_p = 1;
-    gt->p = {cache.sx[ci], cache.sy[ci], cache.sz[ci]};
-  }
-}
 
 struct Geometry {
   int W, H, Wc, Hc;
@@ -118,6 +77,8 @@ struct Geometry {
   int bd;
   int chroma;     // 1 = 4:2:0
   int vec_store;  // destination planes allow 8-byte luma / 4-byte chroma row stores
+  int hp;         // mm_pred_list hp: every list keeps the 14-bit intermediate (bi = true)
+  int store;      // components written: bit 0 luma, bit 1 chroma
 };
 
 struct Taps {
@@ -174,18 +135,14 @@ MM_HD void mpa_cache_thread(int t, const SeqConst& sc, int plane, int cols, int 
   vip[t] = v ? 1 : 0;
 }
 
-#ifndef MM_REPROJ_ROWMAJOR
-#define MM_REPROJ_ROWMAJOR 1
-#endif
 // The reprojection of one element of a device-planned job, stored in k_mc's record layout.
 MM_HD void reproj_thread_mc(int g, int ji, const SeqConst& sc, const JobDev* jobs, const int* job_offsets,
-                            const BlockSetup* setups, const MpaCache& cache, const McIn& mc) {
+                            const BlockSetup* setups, const MpaCache& cache, const McRec& mc) {
   const JobDev& j = jobs[ji];
   // Elements are enumerated row-major over the block (the records k_mc reads and the frame-cache
   // entries are then contiguous across lanes); Eigen's column-major index still decides packet
   // vs tail.  pu_cols = cw / sbw for luma and for 4:2:0 chroma alike.
   const int local = g - job_offsets[ji];
-#if MM_REPROJ_ROWMAJOR
   // VVC block widths are powers of two: a shift instead of the ~20-instruction integer division
   const int pc = j.pu_cols;
   int row;
@@ -195,10 +152,6 @@ MM_HD void reproj_thread_mc(int g, int ji, const SeqConst& sc, const JobDev* job
     row = local / pc;
   const int col = local - row * pc;
   const int eig = col * j.rows + row;
-#else
-  const int col = local / j.rows, row = local - col * j.rows;
-  const int eig = local;
-#endif
   const float gx = (float)(j.x + 4 * col) + sc.off;
   const float gy = (float)(j.y + 4 * row) + sc.off;
   const bool mpa_cached = (j.comp == 0) && (j.model >= MPA_FRONT_BACK && j.model <= MPA_TOP_BOTTOM);
@@ -211,26 +164,34 @@ MM_HD void reproj_thread_mc(int g, int ji, const SeqConst& sc, const JobDev* job
     py = cache.py[pl][ci];
     vip = cache.vip[pl][ci] != 0;
   }
-  const bool packet = packet_lane(eig, j.n);
-  GridTerms gt;
-  load_grid_terms(cache, j, row, col, packet, &gt);
   int32_t fx, fy;
-  reproject_element(sc, setups[ji], gx, gy, packet, mpa_cached, px, py, vip, j.comp ? 1 : 0, &fx, &fy, &gt);
+  reproject_element(sc, setups[ji], gx, gy, packet_lane(eig, j.n), mpa_cached, px, py, vip, j.comp ? 1 : 0, &fx, &fy);
   // chroma 2x2 sub-block (row, col) belongs to luma 4x4 sub-block (row, col) of the same PU
   const int sb = j.sb_base + row * j.pu_cols + col;
-  mm_int2 xy;
-  xy.x = fx;
-  xy.y = fy;
+  mm_int4* rec = &mc.pos[j.list][sb];
   if (j.comp == 0) {
-    mm_int4 r;
-    r.x = fx;
-    r.y = fy;
-    r.z = (j.sb_base << 5) | j.slot;  // reference slot (< 32) and the PU's id (its first sub-block)
-    r.w = ((j.y + 4 * row) << 16) | (j.x + 4 * col);
-    mc.lum[j.list][sb] = r;
-    if (j.alias) mc.chr[j.list][sb] = xy;
+    if (j.alias) {
+      mm_int4 r;
+      r.x = r.z = fx;
+      r.y = r.w = fy;
+      *rec = r;
+    } else {
+      mm_int2 xy;
+      xy.x = fx;
+      xy.y = fy;
+      reinterpret_cast<mm_int2*>(rec)[0] = xy;
+    }
+    if (j.meta_hi & MM_META_PRIMARY) {
+      mm_int2 m;
+      m.x = ((j.y + 4 * row) << 16) | (j.x + 4 * col);
+      m.y = j.meta_hi & 0xffff;
+      mc.meta[sb] = m;
+    }
   } else {
-    mc.chr[j.list][sb] = xy;
+    mm_int2 xy;
+    xy.x = fx;
+    xy.y = fy;
+    reinterpret_cast<mm_int2*>(rec)[1] = xy;
   }
 }
 
@@ -291,82 +252,97 @@ MM_HD void store_row(int16_t* d, const int16_t* v, int vec) {
   for (int c = 0; c < N; c++) d[c] = v[c];
 }
 
-// One luma 4x4 sub-block and its two 4:2:0 chroma 2x2 sub-blocks from the McIn records (device-
-// planned pictures); cls = 0 bi, 1 uni L0, 2 uni L1 (sb_class of g's PU bucket).
-MM_HD void mc_thread_rec(int g, int cls, const Geometry& geo, const Taps& taps, const McIn& mc, const RefDev* refs,
+// AreaBuf<Pel>::addWeightedAvg (Buffer.cpp:398-424): clip((p0 w0 + p1 w1 + offset) >> shiftNum),
+// shiftNum = IF_INTERNAL_FRAC_BITS + 3, offset = (1 << (shiftNum - 1)) + (IF_INTERNAL_OFFS << 3).
+// With BCW_DEFAULT (w0 = w1 = 4) numerator and shift are exactly 4x those of AreaBuf<Pel>::addAvg
+// (Buffer.cpp:551-582), so this one form is xWeightedAverage's bi output for every bcwIdx
+// (InterPrediction.cpp:1596-1600); tests/test_filter_identity.py checks the identity.
+MM_HD int16_t weighted_avg(int p0, int p1, int w0, int w1, int bd) {
+  const int shiftNum = if_internal_frac_bits(bd) + 3;
+  const int offset = (1 << (shiftNum - 1)) + (IF_INTERNAL_OFFS << 3);
+  return clip_pel((p0 * w0 + p1 * w1 + offset) >> shiftNum, (1 << bd) - 1);
+}
+
+// One luma 4x4 sub-block and its two 4:2:0 chroma 2x2 sub-blocks from the McRec records (device-
+// planned pictures): for each used list, xPredInterBlkMM's per-sub-block dispatch
+// (InterPrediction.cpp:776-828), then xWeightedAverage (addAvg / addWeightedAvg for bi, the
+// rndRes uni prediction otherwise, InterPrediction.cpp:1584-1679).  cls = 0 bi, 1 uni L0, 2 uni
+// L1 (sb_class of g's PU bucket).  geo.hp (mm_pred_list): the 14-bit intermediate of the one list.
+MM_HD void mc_thread_rec(int g, int cls, const Geometry& geo, const Taps& taps, const McRec& mc, const RefDev* refs,
                          int16_t* dst_y, int dsy, int16_t* dst_cb, int16_t* dst_cr, int dsc) {
   const bool bi = cls == 0;
+  const bool hp = bi || geo.hp;  // keep the 14-bit intermediate (rndRes = !bi)
   const int uni_list = cls == 2 ? 1 : 0;
   const bool used[2] = {bi || uni_list == 0, bi || uni_list == 1};
-  mm_int4 L[2];
-  mm_int2 C[2];
+  const mm_int2 meta = mc.meta[g];
+  mm_int4 P[2];
 #pragma unroll
-  for (int l = 0; l < 2; l++) {
-    if (!used[l]) continue;
-    L[l] = mc.lum[l][g];
-    if (geo.chroma) C[l] = mc.chr[l][g];
-  }
-  const int pos = used[0] ? L[0].w : L[1].w;
-  const int ox = pos & 0xffff, oy = pos >> 16;
-  int16_t pl[2][16];
+  for (int l = 0; l < 2; l++)
+    if (used[l]) P[l] = mc.pos[l][g];
+  const int ox = meta.x & 0xffff, oy = meta.x >> 16;
+  const int slot[2] = {meta.y & 15, (meta.y >> 4) & 15};
+  const int w1 = bcw_w1((meta.y >> 8) & 7), w0 = 8 - w1;
+  if (geo.store & 1) {
+    int16_t pl[2][16];
 #pragma unroll
-  for (int l = 0; l < 2; l++) {
-    if (!used[l]) continue;
-    const int32_t fx = L[l].x, fy = L[l].y;
-    const int xPos = fx >> 4, yPos = fy >> 4, xFrac = fx & 15, yFrac = fy & 15;
-    const RefDev r = refs[L[l].z & 31];
-    if (sb_out_of_range(xPos, yPos, geo.W, geo.H, geo.maxCUw, geo.maxCUh, 4, 4)) {
-      for (int i = 0; i < 16; i++) pl[l][i] = 0;
-    } else if (window_interior<8, 4, 4>(xPos, yPos, geo.W, geo.H)) {
+    for (int l = 0; l < 2; l++) {
+      if (!used[l]) continue;
+      const int32_t fx = P[l].x, fy = P[l].y;
+      const int xPos = fx >> 4, yPos = fy >> 4, xFrac = fx & 15, yFrac = fy & 15;
+      const RefDev r = refs[slot[l]];
+      if (sb_out_of_range(xPos, yPos, geo.W, geo.H, geo.maxCUw, geo.maxCUh, 4, 4)) {
+        for (int i = 0; i < 16; i++) pl[l][i] = 0;
+      } else if (window_interior<8, 4, 4>(xPos, yPos, geo.W, geo.H)) {
 #if defined(__HIP_DEVICE_COMPILE__)
-      predict_subblock_interior<8, 4, 4>(r.y, r.stride_y, xPos, yPos, taps.packed->lh[xFrac][(xPos - 3) & 1],
-                                         taps.packed->lv[yFrac], bi, geo.bd, pl[l]);
+        predict_subblock_interior<8, 4, 4>(r.y, r.stride_y, xPos, yPos, taps.packed->lh[xFrac][(xPos - 3) & 1],
+                                           taps.packed->lv[yFrac], hp, geo.bd, pl[l]);
 #else
-      predict_subblock_interior<8, 4, 4>(r.y, r.stride_y, xPos, yPos, taps.luma[xFrac], taps.luma[yFrac], bi, geo.bd,
-                                         pl[l]);
+        predict_subblock_interior<8, 4, 4>(r.y, r.stride_y, xPos, yPos, taps.luma[xFrac], taps.luma[yFrac], hp,
+                                           geo.bd, pl[l]);
 #endif
-    } else {
-      predict_subblock<8, 4, 4>(r.y, r.stride_y, geo.W, geo.H, xPos, yPos, taps.luma[xFrac], taps.luma[yFrac], bi,
-                                geo.bd, pl[l]);
+      } else {
+        predict_subblock<8, 4, 4>(r.y, r.stride_y, geo.W, geo.H, xPos, yPos, taps.luma[xFrac], taps.luma[yFrac], hp,
+                                  geo.bd, pl[l]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      int16_t o[4];
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        const int i = r * 4 + c;
+        o[c] = bi ? weighted_avg(pl[0][i], pl[1][i], w0, w1, geo.bd) : pl[uni_list][i];
+      }
+      store_row<4>(dst_y + (long)(oy + r) * dsy + ox, o, geo.vec_store);
     }
   }
-#pragma unroll
-  for (int r = 0; r < 4; r++) {
-    int16_t o[4];
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-      const int i = r * 4 + c;
-      o[c] = bi ? add_avg(pl[0][i], pl[1][i], geo.bd) : (uni_list == 0 ? pl[0][i] : pl[1][i]);
-    }
-    store_row<4>(dst_y + (long)(oy + r) * dsy + ox, o, geo.vec_store);
-  }
-  if (!geo.chroma) return;
+  if (!geo.chroma || !(geo.store & 2)) return;
   int16_t pcb[2][4], pcr[2][4];
 #pragma unroll
   for (int l = 0; l < 2; l++) {
     if (!used[l]) continue;
-    const int32_t fx = C[l].x, fy = C[l].y;
+    const int32_t fx = P[l].z, fy = P[l].w;
     const int xPos = fx >> 5, yPos = fy >> 5, xFrac = fx & 31, yFrac = fy & 31;
-    const RefDev r = refs[L[l].z & 31];
+    const RefDev r = refs[slot[l]];
     if (sb_out_of_range(xPos, yPos, geo.Wc, geo.Hc, geo.maxCUwc, geo.maxCUhc, 2, 2)) {
       for (int i = 0; i < 4; i++) pcb[l][i] = pcr[l][i] = 0;
     } else if (window_interior<4, 2, 2>(xPos, yPos, geo.Wc, geo.Hc)) {
 #if defined(__HIP_DEVICE_COMPILE__)
       const uint32_t* ht = taps.packed->ch[xFrac][(xPos - 1) & 1];
       const uint32_t* vt = taps.packed->cv[yFrac];
-      predict_subblock_interior<4, 2, 2>(r.cb, r.stride_c, xPos, yPos, ht, vt, bi, geo.bd, pcb[l]);
-      predict_subblock_interior<4, 2, 2>(r.cr, r.stride_c, xPos, yPos, ht, vt, bi, geo.bd, pcr[l]);
+      predict_subblock_interior<4, 2, 2>(r.cb, r.stride_c, xPos, yPos, ht, vt, hp, geo.bd, pcb[l]);
+      predict_subblock_interior<4, 2, 2>(r.cr, r.stride_c, xPos, yPos, ht, vt, hp, geo.bd, pcr[l]);
 #else
-      predict_subblock_interior<4, 2, 2>(r.cb, r.stride_c, xPos, yPos, taps.chroma[xFrac], taps.chroma[yFrac], bi,
+      predict_subblock_interior<4, 2, 2>(r.cb, r.stride_c, xPos, yPos, taps.chroma[xFrac], taps.chroma[yFrac], hp,
                                          geo.bd, pcb[l]);
-      predict_subblock_interior<4, 2, 2>(r.cr, r.stride_c, xPos, yPos, taps.chroma[xFrac], taps.chroma[yFrac], bi,
+      predict_subblock_interior<4, 2, 2>(r.cr, r.stride_c, xPos, yPos, taps.chroma[xFrac], taps.chroma[yFrac], hp,
                                          geo.bd, pcr[l]);
 #endif
     } else {
       predict_subblock<4, 2, 2>(r.cb, r.stride_c, geo.Wc, geo.Hc, xPos, yPos, taps.chroma[xFrac], taps.chroma[yFrac],
-                                bi, geo.bd, pcb[l]);
+                                hp, geo.bd, pcb[l]);
       predict_subblock<4, 2, 2>(r.cr, r.stride_c, geo.Wc, geo.Hc, xPos, yPos, taps.chroma[xFrac], taps.chroma[yFrac],
-                                bi, geo.bd, pcr[l]);
+                                hp, geo.bd, pcr[l]);
     }
   }
   const int cx = ox >> 1, cy = oy >> 1;
@@ -376,113 +352,11 @@ MM_HD void mc_thread_rec(int g, int cls, const Geometry& geo, const Taps& taps, 
 #pragma unroll
     for (int c = 0; c < 2; c++) {
       const int i = r * 2 + c;
-      ob[c] = bi ? add_avg(pcb[0][i], pcb[1][i], geo.bd) : (uni_list == 0 ? pcb[0][i] : pcb[1][i]);
-      orr[c] = bi ? add_avg(pcr[0][i], pcr[1][i], geo.bd) : (uni_list == 0 ? pcr[0][i] : pcr[1][i]);
+      ob[c] = bi ? weighted_avg(pcb[0][i], pcb[1][i], w0, w1, geo.bd) : pcb[uni_list][i];
+      orr[c] = bi ? weighted_avg(pcr[0][i], pcr[1][i], w0, w1, geo.bd) : pcr[uni_list][i];
     }
     store_row<2>(dst_cb + (long)(cy + r) * dsc + cx, ob, geo.vec_store);
     store_row<2>(dst_cr + (long)(cy + r) * dsc + cx, orr, geo.vec_store);
-  }
-}
-
-// One luma 4x4 sub-block (and its two 4:2:0 chroma 2x2 sub-blocks) of one PU: both lists,
-// xPredInterBlkMM's per-sub-block dispatch (InterPrediction.cpp:776-828), then addAvg (bi) or the
-// rndRes uni prediction (xWeightedAverage, InterPrediction.cpp:1584-1679).
-// pi = the PU holding luma sub-block g (find_item / wave_find_item)
-MM_HD void mc_thread(int g, int pi, const Geometry& geo, const Taps& taps, const PuDev* pus, const JobDev* jobs,
-                     const int32_t* reproj, const RefDev* refs, int16_t* dst_y, int dsy, int16_t* dst_cb,
-                     int16_t* dst_cr, int dsc) {
-  const PuDev pu = pus[pi];
-  // lanes walk the PU row-major (horizontally adjacent sub-blocks in adjacent lanes share the
-  // reference cache lines of each window row); reprojection results are Eigen column-major
-  const int lin = g - pu.sb_offset;
-  const int rows = pu.h >> 2, cols = pu.w >> 2;
-  const int row = lin / cols, col = lin - row * cols;
-  const int local = col * rows + row;
-  const bool bi = pu.ref_slot[0] >= 0 && pu.ref_slot[1] >= 0;
-  const int uni_list = pu.ref_slot[0] >= 0 ? 0 : 1;
-
-  // ---- luma 4x4 ----
-  int16_t pl[2][16];
-#pragma unroll
-  for (int l = 0; l < 2; l++) {
-    if (pu.ref_slot[l] < 0) continue;
-    const JobDev& j = jobs[pu.job[l][0]];
-    const int32_t fx = reproj[2 * (j.offset + local)], fy = reproj[2 * (j.offset + local) + 1];
-    const int xPos = fx >> 4, yPos = fy >> 4, xFrac = fx & 15, yFrac = fy & 15;
-    const RefDev r = refs[pu.ref_slot[l]];
-    if (sb_out_of_range(xPos, yPos, geo.W, geo.H, geo.maxCUw, geo.maxCUh, 4, 4)) {
-      for (int i = 0; i < 16; i++) pl[l][i] = 0;
-    } else if (window_interior<8, 4, 4>(xPos, yPos, geo.W, geo.H)) {
-#if defined(__HIP_DEVICE_COMPILE__)
-      predict_subblock_interior<8, 4, 4>(r.y, r.stride_y, xPos, yPos, taps.packed->lh[xFrac][(xPos - 3) & 1],
-                                         taps.packed->lv[yFrac], bi, geo.bd, pl[l]);
-#else
-      predict_subblock_interior<8, 4, 4>(r.y, r.stride_y, xPos, yPos, taps.luma[xFrac], taps.luma[yFrac], bi, geo.bd,
-                                         pl[l]);
-#endif
-    } else {
-      predict_subblock<8, 4, 4>(r.y, r.stride_y, geo.W, geo.H, xPos, yPos, taps.luma[xFrac],
-                                taps.luma[yFrac], bi, geo.bd, pl[l]);
-    }
-  }
-  {
-    const int ox = pu.x + 4 * col, oy = pu.y + 4 * row;
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      int16_t o[4];
-#pragma unroll
-      for (int c = 0; c < 4; c++) {
-        const int i = r * 4 + c;
-        o[c] = bi ? add_avg(pl[0][i], pl[1][i], geo.bd) : (uni_list == 0 ? pl[0][i] : pl[1][i]);
-      }
-      store_row<4>(dst_y + (long)(oy + r) * dsy + ox, o, geo.vec_store);
-    }
-  }
-  if (!geo.chroma) return;
-  // ---- chroma 2x2 (Cb and Cr share one reprojection) ----
-  int16_t pcb[2][4], pcr[2][4];
-#pragma unroll
-  for (int l = 0; l < 2; l++) {
-    if (pu.ref_slot[l] < 0) continue;
-    const JobDev& j = jobs[pu.job[l][1]];
-    const int32_t fx = reproj[2 * (j.offset + local)], fy = reproj[2 * (j.offset + local) + 1];
-    const int xPos = fx >> 5, yPos = fy >> 5, xFrac = fx & 31, yFrac = fy & 31;
-    const RefDev r = refs[pu.ref_slot[l]];
-    if (sb_out_of_range(xPos, yPos, geo.Wc, geo.Hc, geo.maxCUwc, geo.maxCUhc, 2, 2)) {
-      for (int i = 0; i < 4; i++) pcb[l][i] = pcr[l][i] = 0;
-    } else if (window_interior<4, 2, 2>(xPos, yPos, geo.Wc, geo.Hc)) {
-#if defined(__HIP_DEVICE_COMPILE__)
-      const uint32_t* ht = taps.packed->ch[xFrac][(xPos - 1) & 1];
-      const uint32_t* vt = taps.packed->cv[yFrac];
-      predict_subblock_interior<4, 2, 2>(r.cb, r.stride_c, xPos, yPos, ht, vt, bi, geo.bd, pcb[l]);
-      predict_subblock_interior<4, 2, 2>(r.cr, r.stride_c, xPos, yPos, ht, vt, bi, geo.bd, pcr[l]);
-#else
-      predict_subblock_interior<4, 2, 2>(r.cb, r.stride_c, xPos, yPos, taps.chroma[xFrac], taps.chroma[yFrac], bi,
-                                         geo.bd, pcb[l]);
-      predict_subblock_interior<4, 2, 2>(r.cr, r.stride_c, xPos, yPos, taps.chroma[xFrac], taps.chroma[yFrac], bi,
-                                         geo.bd, pcr[l]);
-#endif
-    } else {
-      predict_subblock<4, 2, 2>(r.cb, r.stride_c, geo.Wc, geo.Hc, xPos, yPos, taps.chroma[xFrac],
-                                taps.chroma[yFrac], bi, geo.bd, pcb[l]);
-      predict_subblock<4, 2, 2>(r.cr, r.stride_c, geo.Wc, geo.Hc, xPos, yPos, taps.chroma[xFrac],
-                                taps.chroma[yFrac], bi, geo.bd, pcr[l]);
-    }
-  }
-  {
-    const int ox = (pu.x >> 1) + 2 * col, oy = (pu.y >> 1) + 2 * row;
-#pragma unroll
-    for (int r = 0; r < 2; r++) {
-      int16_t ob[2], orr[2];
-#pragma unroll
-      for (int c = 0; c < 2; c++) {
-        const int i = r * 2 + c;
-        ob[c] = bi ? add_avg(pcb[0][i], pcb[1][i], geo.bd) : (uni_list == 0 ? pcb[0][i] : pcb[1][i]);
-        orr[c] = bi ? add_avg(pcr[0][i], pcr[1][i], geo.bd) : (uni_list == 0 ? pcr[0][i] : pcr[1][i]);
-      }
-      store_row<2>(dst_cb + (long)(oy + r) * dsc + ox, ob, geo.vec_store);
-      store_row<2>(dst_cr + (long)(oy + r) * dsc + ox, orr, geo.vec_store);
-    }
   }
 }
 

@@ -20,6 +20,7 @@
 #include "mm_devplan.h"
 #include "mm_me.h"
 #include "mm_dmvr.h"
+#include "mm_epipole.h"
 #include "mm_mvp.h"
 #include "mm_pipeline.h"
 
@@ -29,15 +30,13 @@ using namespace mmpipe;
 struct Plan {
   std::vector<JobDev> jobs;
   std::vector<int> job_off, job_chunk;
-  std::vector<PuDev> pus;
-  std::vector<int> pu_off, pu_chunk;
   std::vector<int> ref_pocs;  // slot -> POC
   std::vector<M3> ged;
   int n_elems = 0, n_sb = 0;
   std::string err;
 };
 
-using EpipoleMap = std::map<std::pair<int, int>, std::array<int32_t, 3>>;
+using EpipoleMap = mmepi::EpipoleList;
 
 struct SeqInfo {
   mm_seq_params prm;
@@ -48,14 +47,9 @@ inline SeqInfo seq_info(const mm_seq_params& p) { return {p, p.width, p.height, 
 
 inline bool is_ged(int m) { return m >= GEODESIC_X && m <= GEODESIC_CAMPOSE; }
 
-// EpipoleList::findEpipoleFixed lookup order (EpipoleList.cpp:19-36)
+// EpipoleList::findEpipoleFixed lookup order (EpipoleList.cpp:19-36), available entries only
 inline bool find_epipole(const EpipoleMap& epi, int cur, int ref, std::array<int32_t, 3>* out) {
-  auto it = epi.find({cur, ref});
-  if (it == epi.end()) it = epi.find({cur, -1});
-  if (it == epi.end()) it = epi.find({-1, -1});
-  if (it == epi.end()) return false;
-  *out = it->second;
-  return true;
+  return epi.find(cur, ref, out);
 }
 
 inline void build_chunks(const std::vector<int>& off, int total, std::vector<int>* chunk) {
@@ -166,17 +160,9 @@ class Planner {
       return (j.comp * 64 + j.model) * 2 + (j.n < 4 ? 1 : 0);
     };
     std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return key(a) < key(b); });
-    std::vector<int> inv(n);
     std::vector<JobDev> sorted(n);
-    for (int i = 0; i < n; i++) {
-      sorted[i] = plan_->jobs[order[i]];
-      inv[order[i]] = i;
-    }
+    for (int i = 0; i < n; i++) sorted[i] = plan_->jobs[order[i]];
     plan_->jobs.swap(sorted);
-    for (auto& d : plan_->pus)
-      for (int l = 0; l < 2; l++)
-        for (int c = 0; c < 2; c++)
-          if (d.job[l][c] >= 0) d.job[l][c] = inv[d.job[l][c]];
     plan_->job_off.resize(n);
     int acc = 0;
     for (int i = 0; i < n; i++) {
@@ -214,6 +200,7 @@ inline int build_pic_tables(const SeqInfo& s, const EpipoleMap& epi, int cur_poc
   t->chroma = s.chroma ? 1 : 0;
   t->active = s.prm.active_models;
   t->nf_mod4 = (int)(((long)(s.W / 4) * (s.H / 4)) % 4);
+  t->only_list = -1;
   const V3 fixed[3] = {{1.0f, 0.0f, 0.0f}, {0.0f, 1.0f, 0.0f}, {0.0f, 0.0f, 1.0f}};
   for (int i = 0; i < 3; i++) t->ged[i] = ged_rotation(fixed[i]);
   for (int k = 0; k < t->n_slots; k++) {
@@ -324,8 +311,9 @@ inline int plan_dmvr(const SeqInfo& s, const mmdev::PicTables& t, const mm_pu_de
     if (u.w < 8 || u.h < 8 || u.w * u.h < 128 || u.w > 128 || u.h > 128 || (u.w & 3) || (u.h & 3) ||
         (u.w > 16 && (u.w & 15)) || (u.h > 16 && (u.h & 15)) || (u.x & 3) ||
         (u.y & 3) || u.x < 0 || u.y < 0 || u.x > s.W - u.w || u.y > s.H - u.h || u.ref_poc[0] < 0 || u.ref_poc[1] < 0 ||
-        u.model[0] != u.model[1]) {
-      *err = "DMVR PU " + std::to_string(i) + ": needs bi prediction, equal models and w, h >= 8, w*h >= 128";
+        u.model[0] != u.model[1] || u.bcw_idx != MM_BCW_DEFAULT) {
+      *err = "DMVR PU " + std::to_string(i) +
+             ": needs bi prediction, equal models, BCW_DEFAULT and w, h >= 8, w*h >= 128 (PU::checkDMVRCondition)";
       return MM_ERR_ARG;
     }
     const int m = u.model[0];

@@ -5,7 +5,11 @@
 //   mm360::MVReprojectionGPU   MVReprojection::init / isInitialized / subblockSize /
 //                              reprojectMotionVectorSubblocks      (SRC/MVReprojection.h:32-58)
 //   mm360::InterPredictionMM   xPredInterBlkMM + xWeightedAverage for a whole picture's PU list
-//                              (SRC/InterPrediction.h:151-154, InterPrediction.cpp:1584-1679)
+//                              (SRC/InterPrediction.h:151-154, InterPrediction.cpp:1584-1679),
+//                              per-list 14-bit predictions (xPredInterBlkMM bi = true), and the
+//                              effective blocks of decoded PUs (motionCompensation's splits,
+//                              SRC/InterPrediction.cpp:1681-1810)
+//   mm360::EpipoleList         EpipoleList (SRC/EpipoleList.{h,cpp}) incl. derivePredictor
 //
 // Status codes become exceptions, like the reference's CHECK -> Exception (SRC/TypeDef.h:1120-1135).
 // NaN reprojections (zero motion) and out-of-range sub-blocks (zero samples) are results, as in
@@ -29,7 +33,7 @@ class Exception : public std::runtime_error {
   int code_;
 };
 
-inline void check(mm_ctx* ctx, int rc, const char* call) {
+inline void check(mm_ctx* ctx, int rc, const char* call) {  // ctx may be null (host-only calls)
   if (rc != MM_OK)
     throw Exception(rc, std::string(call) + " failed (" + std::to_string(rc) + "): " +
                             (ctx ? mm_last_error(ctx) : "no context"));
@@ -70,6 +74,37 @@ class Context {
  private:
   mm_ctx* ctx_ = nullptr;
   mm_seq_params params_{};
+};
+
+// ---------------------------------------------------------------------------------------------
+// EpipoleList (SRC/EpipoleList.h): a standalone list, or a view of a context's own list.
+class EpipoleList {
+ public:
+  EpipoleList() : l_(mm_epipole_list_create()), owned_(true) {}
+  explicit EpipoleList(Context& ctx) : l_(mm_get_epipole_list(ctx.get())), owned_(false) {}
+  ~EpipoleList() {
+    if (owned_) mm_epipole_list_destroy(l_);
+  }
+  EpipoleList(const EpipoleList&) = delete;
+  EpipoleList& operator=(const EpipoleList&) = delete;
+
+  void addEpipole(const int32_t q24[3], int curPOC = -1, int refPOC = -1, bool makeAvailable = false) {
+    check(nullptr, mm_epipole_add(l_, curPOC, refPOC, q24, makeAvailable ? 1 : 0), "mm_epipole_add");
+  }
+  void makeAvailable(int curPOC) { mm_epipole_make_available(l_, curPOC); }
+  bool hasEpipole(int curPOC, int refPOC) const { return mm_epipole_has(l_, curPOC, refPOC) != 0; }
+  void findEpipoleFixed(int curPOC, int refPOC, int32_t q24[3]) const {
+    check(nullptr, mm_epipole_find(l_, curPOC, refPOC, q24), "EpipoleList::findEpipole");
+  }
+  // derivePredictor + floatingToFixed, as DecLib does before adding the picture header's delta
+  void derivePredictorFixed(int curPOC, int32_t q24[3]) const {
+    check(nullptr, mm_epipole_derive_predictor(l_, curPOC, q24), "EpipoleList::derivePredictor");
+  }
+  int count() const { return mm_epipole_count(l_); }
+
+ private:
+  mm_epipole_list* l_;
+  bool owned_;
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -128,10 +163,16 @@ class InterPredictionMM {
  public:
   explicit InterPredictionMM(Context* ctx) : ctx_(ctx) {}
 
-  void clear() { pus_.clear(); }
-  // One PU: luma area, per list (mv in 1/16 luma, reference POC or -1, motion model)
-  void addPU(int x, int y, int w, int h, const int mv[2][2], const int refPOC[2], const int model[2]) {
+  void clear() {
+    pus_.clear();
+    dmvr_.clear();
+  }
+  // One effective block: luma area, per list (mv in 1/16 luma, reference POC or -1, motion
+  // model), the CU's BCW index
+  void addPU(int x, int y, int w, int h, const int mv[2][2], const int refPOC[2], const int model[2],
+             int bcwIdx = MM_BCW_DEFAULT) {
     mm_pu_desc d{};
+    d.bcw_idx = bcwIdx;
     d.x = x;
     d.y = y;
     d.w = w;
@@ -144,8 +185,21 @@ class InterPredictionMM {
     }
     pus_.push_back(d);
   }
+  // One decoded PU as motionCompensation sees it: its effective blocks (16x16 BDOF-size
+  // sub-PUs, merged SbTMVP strips, identical-motion uni L0) join the list, DMVR PUs the DMVR list
+  void addDecodedPU(const mm_tool_flags& tools, const mm_pu_motion& pu, const mm_pu_desc* subMotion = nullptr) {
+    const int cap = (pu.pu.w / 4) * (pu.pu.h / 4) + 1;
+    std::vector<mm_pu_desc> mc(cap), dm(cap);
+    int n_mc = 0, n_dm = 0;
+    check(ctx_->get(),
+          mm_derive_effective_blocks(&tools, &pu, 1, subMotion, mc.data(), cap, &n_mc, dm.data(), cap, &n_dm),
+          "mm_derive_effective_blocks");
+    pus_.insert(pus_.end(), mc.begin(), mc.begin() + n_mc);
+    dmvr_.insert(dmvr_.end(), dm.begin(), dm.begin() + n_dm);
+  }
   size_t size() const { return pus_.size(); }
   const std::vector<mm_pu_desc>& pus() const { return pus_; }
+  const std::vector<mm_pu_desc>& dmvrPUs() const { return dmvr_; }
 
   // Synchronous: host PU list -> predicted device planes (bi: addAvg, uni: clipped).
   void predictPicture(int curPOC, int16_t* dstY, ptrdiff_t strideY, int16_t* dstCb, int16_t* dstCr,
@@ -153,6 +207,24 @@ class InterPredictionMM {
     check(ctx_->get(),
           mm_pred(ctx_->get(), curPOC, pus_.data(), (int)pus_.size(), dstY, strideY, dstCb, dstCr, strideC),
           "mm_pred");
+  }
+  // DMVR PUs collected by addDecodedPU (xProcessDMVRProjected), synchronous
+  void predictDmvr(int curPOC, int16_t* dstY, ptrdiff_t strideY, int16_t* dstCb, int16_t* dstCr, ptrdiff_t strideC) {
+    if (dmvr_.empty()) return;
+    check(ctx_->get(),
+          mm_pred_dmvr(ctx_->get(), curPOC, dmvr_.data(), (int)dmvr_.size(), dstY, strideY, dstCb, dstCr, strideC,
+                       nullptr),
+          "mm_pred_dmvr");
+  }
+  // xPredInterBlkMM of one list of every collected PU: bi = true keeps the 14-bit intermediate
+  // (GEO / CIIP / weighted-prediction blending happens in the caller), dstY or dstCb/dstCr may be
+  // null for a per-component call.
+  void predictList(int curPOC, int list, bool bi, int16_t* dstY, ptrdiff_t strideY, int16_t* dstCb, int16_t* dstCr,
+                   ptrdiff_t strideC) {
+    check(ctx_->get(),
+          mm_pred_list(ctx_->get(), curPOC, pus_.data(), (int)pus_.size(), list, bi ? 1 : 0, dstY, strideY, dstCb,
+                       dstCr, strideC),
+          "mm_pred_list");
   }
   // Asynchronous on the context stream: PU list already in device memory (e.g. written by a GPU
   // parser); errors surface at Context::synchronize().
@@ -164,7 +236,7 @@ class InterPredictionMM {
 
  private:
   Context* ctx_;
-  std::vector<mm_pu_desc> pus_;
+  std::vector<mm_pu_desc> pus_, dmvr_;
 };
 
 }  // namespace mm360

@@ -6,8 +6,9 @@ Mirrors the reference's C++ call surface for this path:
     EpipoleList::addEpipole                       -> MMContext.set_epipole   (mm_set_epipole)
     Picture reconstruction planes                 -> MMContext.upload_ref    (mm_upload_ref)
     MVReprojection::reprojectMotionVectorSubblocks-> MMContext.reproject_motion_vector_subblocks
-    InterPrediction::xPredInterBlkMM (+ addAvg)   -> MMContext.predict       (mm_pred)
+    InterPrediction::xPredInterBlkMM (+ addAvg / addWeightedAvg) -> MMContext.predict (mm_pred)
       same, PU list resident in HBM               -> MMContext.predict_device (mm_pred_device)
+    InterPrediction::xPredInterBlkMM, one list    -> MMContext.predict_list  (mm_pred_list)
     InterpolationFilter::filterHor / filterVer    -> MMContext.filter_hor / filter_ver
 
 Everything runs through the HIP C-ABI library ``lib/libmm360.so`` (include/mm360.h).  There is
@@ -50,8 +51,12 @@ EXPORTED_SYMBOLS = (
     "mm_set_epipole", "mm_upload_ref", "mm_release_ref", "mm_reproject", "mm_pred",
     "mm_pred_device", "mm_pred_status", "mm_pred_prepare", "mm_pred_run", "mm_filter", "mm_last_timing",
     "mm_set_stage_timing", "mm_last_stage_timing", "mm_upload_org", "mm_sad_window", "mm_pred_dmvr", "mm_mvp_convert",
-    "mm_set_stripes",
+    "mm_set_stripes", "mm_pred_list", "mm_derive_effective_blocks", "mm_epipole_list_create",
+    "mm_epipole_list_destroy", "mm_get_epipole_list", "mm_epipole_add", "mm_epipole_make_available", "mm_epipole_has",
+    "mm_epipole_find", "mm_epipole_derive_predictor", "mm_epipole_count",
 )
+
+BCW_DEFAULT = 2  # CommonDef.h:348-349; g_BcwWeights = {-2, 3, 4, 5, 10} (Rom.cpp:203)
 
 
 class MMError(RuntimeError):
@@ -75,15 +80,35 @@ BLOCK_DTYPE = np.dtype([("x", "<i4"), ("y", "<i4"), ("w", "<i4"), ("h", "<i4"), 
                         ("mv_ver", "<i4"), ("model", "<i4"), ("comp", "<i4"), ("cur_poc", "<i4"),
                         ("ref_poc", "<i4")])
 PU_DTYPE = np.dtype([("x", "<i4"), ("y", "<i4"), ("w", "<i4"), ("h", "<i4"), ("mv", "<i4", (2, 2)),
-                     ("ref_poc", "<i4", (2,)), ("model", "<i4", (2,))])
+                     ("ref_poc", "<i4", (2,)), ("model", "<i4", (2,)), ("bcw_idx", "<i4"),
+                     ("reserved", "<i4", (3,))])
 ME_BLOCK_DTYPE = np.dtype([("x", "<i4"), ("y", "<i4"), ("w", "<i4"), ("h", "<i4"), ("mv_hor", "<i4"),
                            ("mv_ver", "<i4"), ("model", "<i4"), ("ref_poc", "<i4"), ("sub_shift", "<i4")])
 MVP_QUERY_DTYPE = np.dtype([(n, "<i4") for n in (
     "pos_x", "pos_y", "mv_hor", "mv_ver", "model_orig", "model_desired", "shift_hor", "shift_ver", "cur_poc_orig",
     "ref_poc_orig", "cur_poc_desired", "ref_poc_desired", "cand_x", "cand_y", "cand_w", "cand_h", "cur_x", "cur_y",
     "cur_w", "cur_h")])
-assert BLOCK_DTYPE.itemsize == 40 and PU_DTYPE.itemsize == 48 and ME_BLOCK_DTYPE.itemsize == 36
+assert BLOCK_DTYPE.itemsize == 40 and PU_DTYPE.itemsize == 64 and ME_BLOCK_DTYPE.itemsize == 36
 assert MVP_QUERY_DTYPE.itemsize == 80
+# mm_pu_motion: a decoded PU for the effective-block derivation (mm_derive_effective_blocks)
+PU_MOTION_DTYPE = np.dtype([("pu", PU_DTYPE), ("flags", "<u4"), ("cur_poc", "<i4"), ("sub_motion", "<i4"),
+                            ("reserved", "<i4")])
+assert PU_MOTION_DTYPE.itemsize == 80
+# MM_PU_* flags (include/mm360.h)
+PU_MERGE, PU_SUBPU, PU_CIIP, PU_SMVD, PU_MMVD, PU_MVREFINE = 0x1, 0x2, 0x4, 0x8, 0x10, 0x20
+PU_WEIGHTED, PU_LONGTERM, PU_REF_SCALED, PU_MMVD_ENC2 = 0x40, 0x80, 0x100, 0x200
+
+
+class ToolFlags(ctypes.Structure):
+    """mm_tool_flags: SPS / PPS / PH switches of the current picture."""
+    _fields_ = [("bdof", c_int32), ("dmvr", c_int32), ("bcw", c_int32), ("wp_bi", c_int32)]
+
+
+def new_pus(n: int) -> np.ndarray:
+    """n zeroed mm_pu_desc records with bcw_idx = BCW_DEFAULT (plain addAvg for bi PUs)."""
+    out = np.zeros(n, dtype=PU_DTYPE)
+    out["bcw_idx"] = BCW_DEFAULT
+    return out
 
 
 def active_mask(models: Sequence[int]) -> int:
@@ -141,6 +166,19 @@ def load_library() -> ctypes.CDLL:
         "mm_sad_window": (c_int, [vp, c_int, vp, c_int, c_int, c_int, vp]),
         "mm_last_stage_timing": (c_int, [vp, POINTER(c_float)]),
         "mm_set_stripes": (c_int, [vp, c_int]),
+        "mm_pred_list": (c_int, [vp, c_int, vp, c_int, c_int, c_int, vp, ctypes.c_ssize_t, vp, vp,
+                                 ctypes.c_ssize_t]),
+        "mm_derive_effective_blocks": (c_int, [POINTER(ToolFlags), vp, c_int, vp, vp, c_int, POINTER(c_int), vp,
+                                               c_int, POINTER(c_int)]),
+        "mm_epipole_list_create": (vp, []),
+        "mm_epipole_list_destroy": (None, [vp]),
+        "mm_get_epipole_list": (vp, [vp]),
+        "mm_epipole_add": (c_int, [vp, c_int, c_int, POINTER(c_int32), c_int]),
+        "mm_epipole_make_available": (c_int, [vp, c_int]),
+        "mm_epipole_has": (c_int, [vp, c_int, c_int]),
+        "mm_epipole_find": (c_int, [vp, c_int, c_int, POINTER(c_int32)]),
+        "mm_epipole_derive_predictor": (c_int, [vp, c_int, POINTER(c_int32)]),
+        "mm_epipole_count": (c_int, [vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -148,6 +186,71 @@ def load_library() -> ctypes.CDLL:
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+def derive_effective_blocks(tools: ToolFlags, pus: np.ndarray, sub_motion: Optional[np.ndarray] = None):
+    """InterPrediction::motionCompensation's effective blocks of decoded PUs (PU_MOTION_DTYPE):
+    (PUs for mm_pred, PUs for mm_pred_dmvr), both PU_DTYPE.  Host code, no GPU."""
+    lib = load_library()
+    pus = np.ascontiguousarray(pus, dtype=PU_MOTION_DTYPE)
+    sub = np.ascontiguousarray(sub_motion if sub_motion is not None else new_pus(0), dtype=PU_DTYPE)
+    cap = int(((pus["pu"]["w"] // 4).astype(np.int64) * (pus["pu"]["h"] // 4)).sum()) + 1  # <= one per 4x4
+    mc, dm = new_pus(cap), new_pus(cap)
+    n_mc, n_dmvr = c_int(0), c_int(0)
+    rc = lib.mm_derive_effective_blocks(byref(tools), c_void_p(pus.ctypes.data), len(pus),
+                                        c_void_p(sub.ctypes.data) if len(sub) else None, c_void_p(mc.ctypes.data),
+                                        cap, byref(n_mc), c_void_p(dm.ctypes.data), cap, byref(n_dmvr))
+    if rc != MM_OK:
+        raise MMError(rc, "mm_derive_effective_blocks: invalid PU")
+    return mc[:n_mc.value], dm[:n_dmvr.value]
+
+
+class EpipoleList:
+    """EpipoleList (SRC/EpipoleList.{h,cpp}) through the C-ABI: Q24 epipoles keyed by
+    (curPOC, refPOC) with -1 wildcards and availability.  Standalone (no GPU) or a context's own
+    list (MMContext.epipole_list())."""
+
+    def __init__(self, handle=None, owner=None):
+        self.lib = load_library()
+        self._owned = handle is None
+        self.h = c_void_p(self.lib.mm_epipole_list_create()) if handle is None else c_void_p(handle)
+        self._owner = owner  # keeps the context alive
+
+    def __del__(self):
+        try:
+            if self._owned and self.h:
+                self.lib.mm_epipole_list_destroy(self.h)
+        except Exception:
+            pass
+
+    def add(self, cur_poc: int, ref_poc: int, q24: Sequence[int], make_available: bool = False):
+        rc = self.lib.mm_epipole_add(self.h, cur_poc, ref_poc, (c_int32 * 3)(*[int(v) for v in q24]),
+                                     int(make_available))
+        if rc:
+            raise MMError(rc, "mm_epipole_add")
+
+    def make_available(self, cur_poc: int):
+        self.lib.mm_epipole_make_available(self.h, cur_poc)
+
+    def has(self, cur_poc: int, ref_poc: int) -> bool:
+        return bool(self.lib.mm_epipole_has(self.h, cur_poc, ref_poc))
+
+    def find(self, cur_poc: int, ref_poc: int):
+        q = (c_int32 * 3)()
+        rc = self.lib.mm_epipole_find(self.h, cur_poc, ref_poc, q)
+        if rc:
+            raise MMError(rc, f"no epipole for ({cur_poc}, {ref_poc})")
+        return tuple(int(v) for v in q)
+
+    def derive_predictor(self, cur_poc: int):
+        q = (c_int32 * 3)()
+        rc = self.lib.mm_epipole_derive_predictor(self.h, cur_poc, q)
+        if rc:
+            raise MMError(rc, "derivePredictor")
+        return tuple(int(v) for v in q)
+
+    def count(self) -> int:
+        return int(self.lib.mm_epipole_count(self.h))
 
 
 def _ptr(a) -> int:
@@ -162,7 +265,7 @@ def _is_device(a) -> bool:
 
 
 def pus_to_device(pus: np.ndarray, device: int = 0):
-    """Copy a PU_DTYPE array into device memory (int32 CUDA tensor of 12 words per PU)."""
+    """Copy a PU_DTYPE array into device memory (int32 CUDA tensor of 16 words per PU)."""
     import torch
     pus = np.ascontiguousarray(pus, dtype=PU_DTYPE)
     words = pus.view(np.int32).reshape(len(pus), PU_DTYPE.itemsize // 4)
@@ -217,6 +320,10 @@ class MMContext:
         self._check(self.lib.mm_synchronize(self.h))
 
     # -- EpipoleList -------------------------------------------------------------------------
+    def epipole_list(self) -> "EpipoleList":
+        """The context's own EpipoleList (used for every GEODESIC_CAMPOSE lookup)."""
+        return EpipoleList(self.lib.mm_get_epipole_list(self.h), owner=self)
+
     def set_epipole(self, cur_poc: int, ref_poc: int, q24: Sequence[int]):
         arr = (c_int32 * 3)(*[int(v) for v in q24])
         self._check(self.lib.mm_set_epipole(self.h, cur_poc, ref_poc, arr))
@@ -266,6 +373,19 @@ class MMContext:
                                      c_void_p(_ptr(dst_cb)) if dst_cb is not None else None,
                                      c_void_p(_ptr(dst_cr)) if dst_cr is not None else None,
                                      dst_cb.stride(0) if dst_cb is not None else 0))
+
+    def predict_list(self, cur_poc: int, pus: np.ndarray, list_: int, hp: bool, dst_y=None, dst_cb=None,
+                     dst_cr=None):
+        """xPredInterBlkMM of one reference list of every PU (mm_pred_list): hp=True gives the
+        14-bit bi=true intermediate, hp=False the rounded and clipped prediction.  A plane left
+        None is not predicted."""
+        pus = np.ascontiguousarray(pus, dtype=PU_DTYPE)
+        self._check(self.lib.mm_pred_list(self.h, cur_poc, c_void_p(pus.ctypes.data), len(pus), int(list_), int(hp),
+                                          c_void_p(_ptr(dst_y)) if dst_y is not None else None,
+                                          dst_y.stride(0) if dst_y is not None else 0,
+                                          c_void_p(_ptr(dst_cb)) if dst_cb is not None else None,
+                                          c_void_p(_ptr(dst_cr)) if dst_cr is not None else None,
+                                          dst_cb.stride(0) if dst_cb is not None else 0))
 
     def mvp_convert(self, queries: np.ndarray) -> np.ndarray:
         """Batched MVReprojection::motionVectorInDesiredMotionModel: int32 [n, 2] MVs."""

@@ -21,8 +21,8 @@ from typing import List, Sequence, Tuple
 
 import numpy as np
 
-from . import (GEODESIC_CAMPOSE, MPA_FRONT_BACK, MPA_LEFT_RIGHT, MPA_TOP_BOTTOM, PU_DTYPE,
-               ROTATIONAL, TANGENTIAL, THREE_D_TRANSLATIONAL)
+from . import (GEODESIC_CAMPOSE, MPA_FRONT_BACK, MPA_LEFT_RIGHT, MPA_TOP_BOTTOM, ROTATIONAL,
+               TANGENTIAL, THREE_D_TRANSLATIONAL, new_pus)
 
 MPA3 = (MPA_FRONT_BACK, MPA_LEFT_RIGHT, MPA_TOP_BOTTOM)
 ALL_MODELS = MPA3 + (TANGENTIAL, THREE_D_TRANSLATIONAL, ROTATIONAL, GEODESIC_CAMPOSE)
@@ -140,7 +140,7 @@ def pu_list(cfg: Config, frame: int = 0, uniform: bool = False, uniform_model: i
                     rows.append((xx, yy, sw, sh, mvs, refs, (m0, m1)))
         else:
             rows.append((x, y, w, h, mvs, refs, (m0, m1)))
-    out = np.zeros(len(rows), dtype=PU_DTYPE)
+    out = new_pus(len(rows))
     for i, (x, y, w, h, mvs, refs, ms) in enumerate(rows):
         out[i]["x"], out[i]["y"], out[i]["w"], out[i]["h"] = x, y, w, h
         out[i]["mv"] = np.array(mvs, dtype=np.int32)
@@ -241,7 +241,7 @@ def dmvr_pu_list(cfg: Config, frame: int = 0, ctu: int = 128) -> np.ndarray:
         mv1 = [-mv0[0] + int(rng.integers(-8, 9)), -mv0[1] + int(rng.integers(-8, 9))]
         rows.append((x, y, w, h, [mv0, mv1], (REF_POCS[0], REF_POCS[1]), (m, m)))
     from . import PU_DTYPE
-    out = np.zeros(len(rows), dtype=PU_DTYPE)
+    out = new_pus(len(rows))
     for i, (x, y, w, h, mvs, refs, ms) in enumerate(rows):
         out[i]["x"], out[i]["y"], out[i]["w"], out[i]["h"] = x, y, w, h
         out[i]["mv"] = np.array(mvs, dtype=np.int32)
