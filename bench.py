@@ -1,25 +1,35 @@
-"""Benchmark: MC+reprojection Mpixels/s on 6144x3072 ERP (BASELINE.json metric, config C3).
+"""Benchmark: MC+reprojection Mpixels/s on 6144x3072 ERP (BASELINE.json metric).
 
 One step = one pass of the MM motion-compensation path over one picture's PU list: device-side
 planning (PU classification + validation, job bucketing), the per-block setup, the per-sub-block
 reprojection of every (PU, list, component) and the 8-tap / 4-tap interpolation + bi-averaging
 of every predicted sample, for a synthetic 6144x3072 10-bit 4:2:0 ERP picture whose PU list uses
 all five motion models (MPA x3, TAN, 3DT, ROT, GED_CAMPOSE).  Inputs (reference planes, the PU
-descriptor list) are resident in HBM before the timed region; nothing is planned on the host.
+descriptor lists) are resident in HBM before the timed region; nothing is planned on the host.
+
+Configurations (BASELINE.json configs):
+  C3 (default at 1 GPU)  `--pictures` distinct pictures (PU lists of frames 0..P-1), each with its
+        own pair of reference pictures (2P resident references, 453 MB at P = 4 -- more than the
+        256 MB Infinity Cache), predicted in rotation: step s predicts picture s % P.  After
+        timing, every picture's output is compared with the CPU oracle (`bit_exact`).
+  C4 (default at N > 1 GPUs)  one C3 picture per step, CTU-row sharded: rank r predicts the PUs
+        of its stripe (mm360.parallel) straight into its segment of the stripe-major packed
+        picture, then ONE in-place RCCL all-gather (Y + Cb + Cr together) rebuilds the picture on
+        every rank; picture t's all-gather overlaps picture t+1's prediction (two picture
+        buffers).  value = pictures' luma area / max-over-ranks time ("strong" scaling: the
+        picture is fixed); `mc_only` is the same loop without the all-gather.
+  C5  encoder ME candidate evaluation (Mcandidates/s).
 
 roofline: the dominant kernel is k_mc (interpolation + averaging); its algorithmic bytes (SURVEY
 8(d): 6 B uni / 9 B bi per luma pixel) over its per-launch device time, measured with HIP events
 on the context stream (mm_last_stage_timing).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
-
-Multi-GPU (torch.distributed.run, one rank per GPU): every rank predicts its own picture (PU
-list of frame = rank) from its own resident references -- independent pictures, no data-path
-collective ("scaling": "weak"); value = pictures' luma area of all ranks / max-over-ranks time.
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3|C4|C5]
 """
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -30,171 +40,294 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import mm360  # noqa: E402
+from mm360 import parallel as P  # noqa: E402
 from mm360 import workload as W  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "MC+reprojection Mpixels/s on 6144x3072 ERP; bit-exact vs the CPU oracle restatement (parity unpinned)"
+POC_STRIDE = 32  # picture f: refs (32 f, 32 f + 16), current POC 32 f + 8
+RED_DEVICE = ["cuda"]  # where the timing reductions run: "cpu" under the gloo rehearsal backend
 
 
-def measured_traffic(args):
+def measured_traffic(args, config):
     """HBM bytes per k_mc_dev launch from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes
-    (profiles/r01_traffic.json, tools/traffic_json.py), only when that profile was taken with
-    this very library (sha256) and the C3 workload; else None."""
+    (profiles/r02_traffic.json, tools/traffic_json.py), only when that profile was taken with
+    this very library (sha256) and the same workload; else None."""
     import hashlib
-    path = os.path.join(ROOT, "profiles", "r01_traffic.json")
-    if args.config != "C3" or args.uniform_model is not None or args.coherent_mv or not os.path.exists(path):
+    path = os.path.join(ROOT, "profiles", "r02_traffic.json")
+    if config != "C3" or args.uniform_model is not None or args.coherent_mv or not os.path.exists(path):
         return None
     d = json.load(open(path))
     sha = hashlib.sha256(open(mm360.LIB_PATH, "rb").read()).hexdigest()
-    return d["traffic_bytes_per_launch"] if d.get("lib_sha256") == sha else None
+    ok = d.get("lib_sha256") == sha and d.get("pictures") == args.pictures
+    return d["traffic_bytes_per_launch"] if ok else None
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="C3")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="length of the CPU baseline sample")
-    ap.add_argument("--kernel-steps", type=int, default=10, help="extra steps timed per launch with HIP events")
-    ap.add_argument("--lib", default=None, help="alternative build of libmm360.so (A/B experiments)")
-    ap.add_argument("--stripes", type=int, default=None, help="mm_set_stripes (default: the library's)")
-    ap.add_argument("--coherent-mv", action="store_true",
-                    help="experiment: one MV for every PU and list (spatially coherent motion)")
-    ap.add_argument("--uniform-model", type=int, default=None,
-                    help="per-model workload: all PUs 16x16 with this MotionModelID (SURVEY 8(d))")
-    args = ap.parse_args()
+def host_info(threads):
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    libc = " ".join(platform.libc_ver())
+    return {"cpu_model": model, "nproc": os.cpu_count(), "threads_available": threads, "glibc": libc}
 
-    if args.lib:
-        mm360.LIB_PATH = os.path.abspath(args.lib)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl")
-    torch.cuda.set_device(local)
 
-    cfg = W.CONFIGS[args.config]
-    params = mm360.seq_params(cfg.width, cfg.height, cfg.models)
-    if args.config == "C5":
-        return bench_me(args, cfg, params, rank, world, local, dist)
-    if args.uniform_model is not None:
-        pus = W.pu_list(cfg, frame=rank, uniform=True, uniform_model=args.uniform_model)
-    else:
-        pus = W.pu_list(cfg, frame=rank)
-    if args.coherent_mv:
-        pus["mv"][:, 0, :] = (85, -43)
-        pus["mv"][:, 1, :] = (-37, 91)
-    area = W.luma_area(pus)
-    alg_bytes = W.algorithmic_bytes(pus)
+def cpu_threads():
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))  # the GPU box's CPU share is 16 threads per GPU
 
+
+def picture_set(cfg, n, frame0=0, uniform_model=None, coherent=False):
+    """n pictures: (cur_poc, PU list, {poc: planes}) with disjoint reference pairs."""
+    out = []
+    for f in range(n):
+        base = POC_STRIDE * (frame0 + f)
+        if uniform_model is not None:
+            pus = W.pu_list(cfg, frame=frame0 + f, uniform=True, uniform_model=uniform_model)
+        else:
+            pus = W.pu_list(cfg, frame=frame0 + f)
+        if coherent:
+            pus["mv"][:, 0, :] = (85, -43)
+            pus["mv"][:, 1, :] = (-37, 91)
+        pus["ref_poc"] = np.where(pus["ref_poc"] >= 0, pus["ref_poc"] + base, -1)
+        refs = {base + p: W.ref_planes(cfg.width, cfg.height, base + p) for p in W.REF_POCS}
+        out.append((base + W.CUR_POC, pus, refs))
+    return out
+
+
+def new_ctx(params, local, pictures):
     ctx = mm360.MMContext(params, device=local)
     ctx.set_stream(torch.cuda.current_stream().cuda_stream)
-    if args.stripes:
-        ctx.set_stripes(args.stripes)
-    ctx.set_epipole(W.CUR_POC, -1, W.GED_EPIPOLE_Q24)
-    for poc in W.REF_POCS:
-        y, cb, cr = W.ref_planes(cfg.width, cfg.height, poc)
-        ctx.upload_ref(poc, torch.from_numpy(y).cuda(), torch.from_numpy(cb).cuda(), torch.from_numpy(cr).cuda())
+    for cur, _, refs in pictures:
+        ctx.set_epipole(cur, -1, W.GED_EPIPOLE_Q24)
+        for poc, (y, cb, cr) in refs.items():
+            ctx.upload_ref(poc, torch.from_numpy(y).cuda(), torch.from_numpy(cb).cuda(), torch.from_numpy(cr).cuda())
+    return ctx
+
+
+def planes(cfg):
     dy = torch.zeros((cfg.height, cfg.width), dtype=torch.int16, device="cuda")
     dcb = torch.zeros((cfg.height // 2, cfg.width // 2), dtype=torch.int16, device="cuda")
-    dcr = torch.zeros_like(dcb)
-    ctx.prepare(W.CUR_POC, pus)  # PU descriptors -> HBM (outside the timed region)
+    return dy, dcb, torch.zeros_like(dcb)
 
-    for _ in range(args.warmup):
-        ctx.run(dy, dcb, dcr)
+
+def timed(steps, warmup, body, dist):
+    for s in range(warmup):
+        body(s)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        ctx.run(dy, dcb, dcr)
+    for s in range(steps):
+        body(s)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=RED_DEVICE[0])
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-        at = torch.tensor([area], dtype=torch.float64, device="cuda")
+    return elapsed
+
+
+def cpu_baseline_and_check(args, cfg, params, pictures, gpu_out):
+    """The oracle on the host cores of this box: (a) one thread, as VTM's serial decoder, over a
+    bounded sample (~cpu_seconds) of the bench pictures; (b) PU-parallel on all available threads
+    (std::thread-style pthreads in the oracle) over the same pictures.  References are padded
+    once per picture outside the timing (reported separately).  The all-thread outputs are
+    compared with the GPU outputs of every bench picture: bit_exact."""
+    from oracle.oracle import Oracle
+    orc = Oracle(params, [(cur, -1, W.GED_EPIPOLE_Q24) for cur, _, _ in pictures])
+    t = time.perf_counter()
+    padded = [orc.padded_refs(refs) for _, _, refs in pictures]
+    pad_s = (time.perf_counter() - t) / len(pictures)
+    threads = cpu_threads()
+    # (b) all threads, every picture once -> bit-exact check
+    mismatches = 0
+    t_all, area_all = 0.0, 0
+    for (cur, pus, _), pr, got in zip(pictures, padded, gpu_out):
+        t = time.perf_counter()
+        want = orc.predict_padded(pr, cur, pus, cfg.width, cfg.height, threads)
+        t_all += time.perf_counter() - t
+        area_all += W.luma_area(pus)
+        mismatches += sum(int((g != w).sum()) for g, w in zip(got, want))
+    # (a) one thread, bounded sample
+    t_one, area_one, n_one = 0.0, 0, 0
+    while t_one < args.cpu_seconds:
+        cur, pus, _ = pictures[n_one % len(pictures)]
+        t = time.perf_counter()
+        orc.predict_padded(padded[n_one % len(pictures)], cur, pus, cfg.width, cfg.height, 1)
+        t_one += time.perf_counter() - t
+        area_one += W.luma_area(pus)
+        n_one += 1
+    info = host_info(threads)
+    cpu = {"value": round(area_one / t_one / 1e6, 3), "unit": "Mpixels/s", "cores": 1, "kind": "port",
+           "sample": f"{n_one} full {cfg.width}x{cfg.height} pictures of the bench workload through the oracle "
+                     f"(oracle/mm_oracle.c: array-at-a-time restatement, glibc libm + SSE packets, gcc -O2), "
+                     f"one host thread, {t_one:.1f} s; reference padding (extendPicBorder) {pad_s * 1e3:.0f} ms per "
+                     f"picture done once outside the timing",
+           "all_cores": {"value": round(area_all / t_all / 1e6, 3), "unit": "Mpixels/s", "threads": threads,
+                         "sample": f"{len(pictures)} pictures, PU-parallel pthreads, {t_all:.2f} s"},
+           "padding_ms_per_picture": round(pad_s * 1e3, 1)}
+    cpu.update(info)
+    return cpu, mismatches == 0, mismatches
+
+
+def bench_pictures(args, cfg, params, rank, world, local, dist):
+    """C3 (and C2 / uniform-model variants): rotating pictures, one per step."""
+    pictures = picture_set(cfg, args.pictures, frame0=rank * args.pictures, uniform_model=args.uniform_model,
+                           coherent=args.coherent_mv)
+    ctx = new_ctx(params, local, pictures)
+    if args.stripes:
+        ctx.set_stripes(args.stripes)
+    d_pus = [mm360.pus_to_device(p) for _, p, _ in pictures]
+    outs = [planes(cfg) for _ in pictures]
+    area = [W.luma_area(p) for _, p, _ in pictures]
+    alg = [W.algorithmic_bytes(p) for _, p, _ in pictures]
+    P_ = len(pictures)
+
+    def step(s):
+        f = s % P_
+        ctx.predict_device(pictures[f][0], d_pus[f], *outs[f])
+
+    elapsed = timed(args.steps, args.warmup, step, dist)
+    ctx.synchronize()  # raises if the device planner rejected a PU
+    steps_area = sum(area[s % P_] for s in range(args.steps))
+    total_area = float(steps_area)
+    if dist:
+        at = torch.tensor([total_area], dtype=torch.float64, device=RED_DEVICE[0])
         dist.all_reduce(at, op=dist.ReduceOp.SUM)
         total_area = float(at.item())
-    else:
-        total_area = float(area)
-
-    ctx.synchronize()  # raises if the device planner rejected a PU
     # per-launch device time of each stage (HIP events between the launches on the context stream)
     ctx.set_stage_timing(True)
     stages = []
-    for _ in range(args.kernel_steps):
-        ctx.run(dy, dcb, dcr)
+    for s in range(args.kernel_steps):
+        step(s)
         stages.append(ctx.last_stage_timing_ms())
     ctx.set_stage_timing(False)
     st = np.mean(np.array(stages), axis=0)
     kernel_ms = float(st[3])
-    pipeline_ms = float(st.sum())
+    alg_step = float(np.mean([alg[s % P_] for s in range(args.kernel_steps)]))
+    achieved = alg_step / (kernel_ms * 1e-3) / 1e9
+    got = [tuple(t.cpu().numpy() for t in o) for o in outs]
 
-    ms_per_step = elapsed / args.steps * 1e3
-    value = total_area * args.steps / elapsed / 1e6
-    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
-
-    cpu = None
+    cpu, bit_exact, mism = None, None, None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        # bounded sample of the same workload, ~10 s on one host thread: the PU lists of
-        # consecutive synthetic pictures (frames 0, 1, ...) of this configuration
-        from oracle.oracle import Oracle
-        refs = {poc: W.ref_planes(cfg.width, cfg.height, poc) for poc in W.REF_POCS}
-        orc = Oracle(params, [(W.CUR_POC, -1, W.GED_EPIPOLE_Q24)])
-        done_area, cpu_s, frames = 0, 0.0, 0
-        while cpu_s < args.cpu_seconds:
-            fp = pus if frames == 0 else W.pu_list(cfg, frame=frames)
-            t = time.perf_counter()
-            orc.predict(W.CUR_POC, fp, refs, cfg.width, cfg.height)
-            cpu_s += time.perf_counter() - t
-            done_area += W.luma_area(fp)
-            frames += 1
-        cpu = {"value": round(done_area / cpu_s / 1e6, 3), "unit": "Mpixels/s", "cores": 1, "kind": "port",
-               "sample": f"{frames} full {cfg.width}x{cfg.height} pictures (seeded PU lists of frames 0..{frames - 1}) "
-                         f"through the oracle (oracle/mm_oracle.c, array-at-a-time restatement, glibc libm + SSE "
-                         f"packets), single thread, {cpu_s:.1f} s incl. reference padding"}
-
+        cpu, bit_exact, mism = cpu_baseline_and_check(args, cfg, params, pictures, got)
     if rank == 0:
         line = {
-            "metric": "MC+reprojection Mpixels/s on 6144x3072 ERP; bit-exact vs VTM CPU",
-            "value": round(value, 2),
-            "unit": "Mpixels/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f32+int16",
+            "metric": METRIC, "value": round(total_area / elapsed / 1e6, 2), "unit": "Mpixels/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32+int16",
             "data": "synthetic (seeded ERP planes + PU lists, SURVEY 8(d))",
             "config": {"workload": f"{args.config}: {cfg.description}" + (
                            f" [uniform 16x16 PUs, model {mm360.MODEL_NAMES[args.uniform_model]}]"
-                           if args.uniform_model is not None else ""), "width": cfg.width, "height": cfg.height,
-                       "pus": int(len(pus)), "luma_area": int(area), "models": [mm360.MODEL_NAMES[m] for m in cfg.models],
-                       "parallelism": f"replicas x{world} (one picture per GPU)"},
+                           if args.uniform_model is not None else ""),
+                       "width": cfg.width, "height": cfg.height, "pictures": P_,
+                       "pus_per_picture": int(np.mean([len(p) for _, p, _ in pictures])),
+                       "luma_area": int(area[0]), "resident_refs": 2 * P_,
+                       "models": [mm360.MODEL_NAMES[m] for m in cfg.models],
+                       "parallelism": "1 GPU" if world == 1 else f"replicas x{world} (own pictures per GPU)"},
+            "bit_exact": bit_exact, "mismatching_samples": mism,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": measured_traffic(args),
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": measured_traffic(args, args.config),
                          "kernel": "k_mc_dev", "kernel_ms": round(kernel_ms, 4),
-                         "algorithmic_bytes": int(alg_bytes)},
+                         "algorithmic_bytes": int(alg_step)},
             "stages_ms": {"plan": round(float(st[0]), 4), "setup": round(float(st[1]), 4),
                           "reproj": round(float(st[2]), 4), "mc": round(float(st[3]), 4),
-                          "pipeline": round(pipeline_ms, 4)},
+                          "pipeline": round(float(st.sum()), 4)},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     ctx.close()
-    if dist:
-        dist.destroy_process_group()
+
+
+def bench_c4(args, cfg, params, rank, world, local, dist):
+    """C4: one C3 picture per step, CTU-row sharded over the ranks, one packed all-gather."""
+    (cur, pus, refs), = picture_set(cfg, 1)
+    ctx = new_ctx(params, local, [(cur, pus, refs)])
+    mine = P.shard_pus(pus, cfg.height, world, rank)
+    ctx.prepare(cur, mine)
+    lay = P.StripeLayout(cfg.width, cfg.height, world)
+    bufs = [torch.zeros(lay.total, dtype=torch.int16, device="cuda") for _ in range(2)]
+    ptrs = [lay.dst_pointers(b.data_ptr(), rank) for b in bufs]
+    area = W.luma_area(pus)
+    pending = [None, None]  # the all-gather still reading/writing each picture buffer
+
+    def mc_only(s):
+        ctx.run_raw(*ptrs[s % 2])
+
+    def with_allgather(s):
+        b = s % 2
+        if pending[b] is not None:  # picture s - 2's all-gather must finish before s overwrites
+            pending[b].wait()       # the buffer (a stream wait, not a host wait)
+        ctx.run_raw(*ptrs[b])
+        if args.dist_backend == "nccl":
+            pending[b] = P.allgather_packed(bufs[b], lay, async_op=True)
+        else:  # gloo rehearsal: host staging, synchronous
+            host = bufs[b].cpu()
+            P.allgather_packed(host, lay)
+            bufs[b].copy_(host)
+
+    t_mc = timed(args.steps, args.warmup, mc_only, dist)
+    t_e2e = timed(args.steps, args.warmup, with_allgather, dist) if world > 1 else t_mc
+    for w in pending:
+        if w is not None:
+            w.wait()
+    torch.cuda.synchronize()
+    ctx.synchronize()
+    # stage timing of this rank's stripe
+    ctx.set_stage_timing(True)
+    stages = []
+    for s in range(args.kernel_steps):
+        mc_only(s)
+        stages.append(ctx.last_stage_timing_ms())
+    ctx.set_stage_timing(False)
+    st = np.mean(np.array(stages), axis=0)
+    kernel_ms = float(st[3])
+    achieved = W.algorithmic_bytes(mine) / (kernel_ms * 1e-3) / 1e9
+    # the last gathered picture (steps - 1) on this rank vs the oracle's full picture
+    bit_exact = None
+    if rank == 0 and not args.no_cpu_baseline:
+        from oracle.oracle import Oracle
+        orc = Oracle(params, [(cur, -1, W.GED_EPIPOLE_Q24)])
+        want = orc.predict_padded(orc.padded_refs(refs), cur, pus, cfg.width, cfg.height, cpu_threads())
+        got = lay.unpack(bufs[(args.steps - 1) % 2].cpu().numpy())
+        bit_exact = all(np.array_equal(g, w) for g, w in zip(got, want))
+    if rank == 0:
+        ag_bytes = (world - 1) * lay.seg * 2
+        print(json.dumps({
+            "metric": METRIC, "value": round(area * args.steps / t_e2e / 1e6, 2), "unit": "Mpixels/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(t_e2e / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "f32+int16", "data": "synthetic (seeded ERP planes + PU list, SURVEY 8(d))",
+            "config": {"workload": f"C4: {cfg.description}, CTU-row sharded across {world} GPU(s) with one packed "
+                                   f"RCCL all-gather per picture", "width": cfg.width, "height": cfg.height,
+                       "pus": int(len(pus)), "pus_rank0": int(len(mine)), "luma_area": int(area),
+                       "stripe_ctu_rows": lay.rows // 128, "allgather_bytes_in_per_rank": int(ag_bytes),
+                       "parallelism": f"ctu-row stripes x{world}"},
+            "mc_only": {"value": round(area * args.steps / t_mc / 1e6, 2), "ms_per_step": round(t_mc / args.steps * 1e3, 4),
+                        "note": "same loop without the all-gather (references pre-replicated)"},
+            "bit_exact": bit_exact,
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "k_mc_dev (rank 0 stripe)",
+                         "kernel_ms": round(kernel_ms, 4), "algorithmic_bytes": int(W.algorithmic_bytes(mine))},
+            "stages_ms": {"plan": round(float(st[0]), 4), "setup": round(float(st[1]), 4),
+                          "reproj": round(float(st[2]), 4), "mc": round(float(st[3]), 4),
+                          "pipeline": round(float(st.sum()), 4)},
+            "cpu_baseline": None,
+        }), flush=True)
+    ctx.close()
 
 
 def bench_me(args, cfg, params, rank, world, local, dist):
@@ -213,31 +346,19 @@ def bench_me(args, cfg, params, rank, world, local, dist):
         ctx.upload_ref(poc, torch.from_numpy(y).cuda(), torch.from_numpy(cb).cuda(), torch.from_numpy(cr).cuda())
     ctx.upload_org(W.CUR_POC, torch.from_numpy(W.org_plane(cfg.width, cfg.height)).cuda())
     sads = torch.zeros((len(blocks), C), dtype=torch.int32, device="cuda")
-    for _ in range(args.warmup):
-        ctx.sad_window(W.CUR_POC, blocks, W.ME_RANGE, 16, out=sads)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
     kms = []
-    for _ in range(args.steps):
+
+    def step(s):
         ctx.sad_window(W.CUR_POC, blocks, W.ME_RANGE, 16, out=sads)
         kms.append(ctx.last_timing_ms())
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+
+    elapsed = timed(args.steps, args.warmup, step, dist)
     total = float(n_cand)
     if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-        at = torch.tensor([total], dtype=torch.float64, device="cuda")
+        at = torch.tensor([total], dtype=torch.float64, device=RED_DEVICE[0])
         dist.all_reduce(at, op=dist.ReduceOp.SUM)
         total = float(at.item())
-    kernel_ms = float(np.mean(kms))
+    kernel_ms = float(np.mean(kms[args.warmup:]))
     alg_bytes = cand_px * 4  # read ref 2 B + read org 2 B per candidate pixel
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
     cpu = None
@@ -254,11 +375,11 @@ def bench_me(args, cfg, params, rank, world, local, dist):
         cpu = {"value": round(len(sample) * C / cpu_s / 1e6, 4), "unit": "Mcandidates/s", "cores": 1, "kind": "port",
                "sample": f"{len(sample)} blocks x {C} candidates of the same workload through the oracle "
                          f"(oracle/mm_oracle.c), single thread, {cpu_s:.2f} s"}
+        cpu.update(host_info(cpu_threads()))
     if rank == 0:
         print(json.dumps({
             "metric": "MM encoder ME candidate evaluations/s (reprojection + 8-tap + SAD) on 2048x1024 ERP",
-            "value": round(total * args.steps / elapsed / 1e6, 3),
-            "unit": "Mcandidates/s",
+            "value": round(total * args.steps / elapsed / 1e6, 3), "unit": "Mcandidates/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32+int16",
@@ -274,6 +395,54 @@ def bench_me(args, cfg, params, rank, world, local, dist):
             "cpu_baseline": cpu,
         }), flush=True)
     ctx.close()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default=None, help="C3 (default at 1 GPU), C4 (default at N > 1), C2, C5")
+    ap.add_argument("--pictures", type=int, default=4, help="C3: distinct pictures (each with its own references)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="length of the one-thread CPU baseline sample")
+    ap.add_argument("--kernel-steps", type=int, default=8, help="extra steps timed per launch with HIP events")
+    ap.add_argument("--lib", default=None, help="alternative build of libmm360.so (A/B experiments)")
+    ap.add_argument("--stripes", type=int, default=None, help="mm_set_stripes (default: the library's)")
+    ap.add_argument("--coherent-mv", action="store_true",
+                    help="experiment: one MV for every PU and list (spatially coherent motion)")
+    ap.add_argument("--uniform-model", type=int, default=None,
+                    help="per-model workload: all PUs 16x16 with this MotionModelID (SURVEY 8(d))")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (RCCL over xGMI, default) or gloo (rehearsal of N ranks on one GPU: the "
+                         "all-gather then stages through host memory)")
+    args = ap.parse_args()
+
+    if args.lib:
+        mm360.LIB_PATH = os.path.abspath(args.lib)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dist_backend != "nccl":  # gloo rehearsal: ranks may share the box's GPU(s)
+        local %= max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(args.dist_backend)
+            RED_DEVICE[0] = "cpu"
+    args.config = args.config or ("C3" if world == 1 else "C4")
+    cfg = W.CONFIGS["C3" if args.config == "C4" else args.config]
+    params = mm360.seq_params(cfg.width, cfg.height, cfg.models)
+    if args.config == "C5":
+        bench_me(args, cfg, params, rank, world, local, dist)
+    elif args.config == "C4":
+        bench_c4(args, cfg, params, rank, world, local, dist)
+    else:
+        bench_pictures(args, cfg, params, rank, world, local, dist)
     if dist:
         dist.destroy_process_group()
 

@@ -1626,3 +1626,81 @@ int orc_effective(const mm_tool_flags* tools, const mm_pu_motion* pus, int n, co
   *n_dmvr = x.n_dmvr;
   return (x.n_mc > cap_mc || x.n_dmvr > cap_dmvr) ? MM_ERR_ARG : 0;
 }
+
+/* ==========================================================================================
+ * CPU baseline helpers (bench.py cpu_baseline leg): reference pictures padded once, then the
+ * picture's PUs predicted on n_threads host threads (PU-parallel: PUs write disjoint samples;
+ * the Orc state is read-only during prediction).  The per-PU arithmetic is pred_pu's.
+ * ========================================================================================== */
+#include <pthread.h>
+
+typedef struct {
+  int n;
+  OPic* pics;
+} ORefs;
+
+void* orc_refs_create(void* h, int n_refs, const int32_t* pocs, const int16_t* const* ys, const int16_t* const* cbs,
+                      const int16_t* const* crs, ptrdiff_t stride_y, ptrdiff_t stride_c) {
+  ORefs* r = (ORefs*)calloc(1, sizeof(ORefs));
+  r->n = n_refs;
+  r->pics = pad_refs((Orc*)h, n_refs, pocs, ys, cbs, crs, stride_y, stride_c);
+  return r;
+}
+
+void orc_refs_destroy(void* p) {
+  ORefs* r = (ORefs*)p;
+  if (!r) return;
+  free_refs(r->pics, r->n);
+  free(r);
+}
+
+typedef struct {
+  Orc* o;
+  const ORefs* refs;
+  int cur_poc;
+  const mm_pu_desc* pus;
+  int begin, end;
+  int16_t *dy, *dcb, *dcr;
+  ptrdiff_t sdy, sdc;
+  int rc;
+} OJob;
+
+static void* pred_range(void* arg) {
+  OJob* j = (OJob*)arg;
+  int16_t* pred[2][3];
+  for (int l = 0; l < 2; l++)
+    for (int c = 0; c < 3; c++) pred[l][c] = (int16_t*)malloc(sizeof(int16_t) * 128 * 128);
+  j->rc = 0;
+  for (int i = j->begin; i < j->end && !j->rc; i++)
+    j->rc = pred_pu(j->o, j->refs->pics, j->refs->n, &j->pus[i], j->cur_poc, pred, j->dy, j->sdy, j->dcb, j->dcr, j->sdc,
+                    -1, 0);
+  for (int l = 0; l < 2; l++)
+    for (int c = 0; c < 3; c++) free(pred[l][c]);
+  return NULL;
+}
+
+int orc_pred_padded(void* h, void* refs, int cur_poc, const mm_pu_desc* pus, int n, int16_t* dy, ptrdiff_t sdy,
+                    int16_t* dcb, int16_t* dcr, ptrdiff_t sdc, int n_threads) {
+  if (n_threads < 1) n_threads = 1;
+  if (n_threads > 256) n_threads = 256;
+  OJob jobs[256];
+  pthread_t th[256];
+  for (int t = 0; t < n_threads; t++) {
+    /* interleaved chunks of 64 PUs would balance better; contiguous ranges keep it simple and the
+       PU list is raster-ordered with a uniform mix of models */
+    OJob jb = {(Orc*)h, (const ORefs*)refs, cur_poc, pus, (int)((long)n * t / n_threads),
+               (int)((long)n * (t + 1) / n_threads), dy, dcb, dcr, sdy, sdc, 0};
+    jobs[t] = jb;
+  }
+  if (n_threads == 1) {
+    pred_range(&jobs[0]);
+    return jobs[0].rc;
+  }
+  for (int t = 0; t < n_threads; t++) pthread_create(&th[t], NULL, pred_range, &jobs[t]);
+  int rc = 0;
+  for (int t = 0; t < n_threads; t++) {
+    pthread_join(th[t], NULL);
+    if (jobs[t].rc && !rc) rc = jobs[t].rc;
+  }
+  return rc;
+}

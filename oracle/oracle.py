@@ -45,6 +45,12 @@ def load():
     lib.orc_epi_make_available.argtypes = [c_void_p, c_int]
     lib.orc_epi_predictor.argtypes = [c_void_p, c_int, POINTER(c_int32)]
     lib.orc_epi_count.argtypes = [c_void_p]
+    lib.orc_refs_create.restype = c_void_p
+    lib.orc_refs_create.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_ssize_t,
+                                    ctypes.c_ssize_t]
+    lib.orc_refs_destroy.argtypes = [c_void_p]
+    lib.orc_pred_padded.argtypes = [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, ctypes.c_ssize_t, c_void_p,
+                                    c_void_p, ctypes.c_ssize_t, c_int]
     lib.orc_filter.argtypes = [c_int, c_int, c_int, c_void_p, ctypes.c_ssize_t, c_void_p, ctypes.c_ssize_t, c_int,
                                c_int, c_int, c_int, c_int]
     lib.orc_pred_dmvr.argtypes = [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
@@ -58,6 +64,16 @@ def load():
 
 def _ptr_array(arrs):
     return (c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+
+
+class _PaddedRefs:
+    def __init__(self, lib, h):
+        self.lib, self.h = lib, c_void_p(h)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.lib.orc_refs_destroy(self.h)
+            self.h = None
 
 
 class Oracle:
@@ -106,6 +122,30 @@ class Oracle:
                                c_void_p(dcb.ctypes.data), c_void_p(dcr.ctypes.data), W // 2)
         if rc:
             raise RuntimeError(f"oracle predict failed: {rc}")
+        return dy, dcb, dcr
+
+    def padded_refs(self, refs):
+        """Pad the reference pictures once (Picture::extendPicBorder layout) for predict_padded."""
+        pocs = sorted(refs)
+        ys = [np.ascontiguousarray(refs[p][0]) for p in pocs]
+        cbs = [np.ascontiguousarray(refs[p][1]) for p in pocs]
+        crs = [np.ascontiguousarray(refs[p][2]) for p in pocs]
+        pa = np.array(pocs, dtype=np.int32)
+        h = self.lib.orc_refs_create(self.h, len(pocs), c_void_p(pa.ctypes.data), _ptr_array(ys), _ptr_array(cbs),
+                                     _ptr_array(crs), ys[0].shape[1], cbs[0].shape[1])
+        return _PaddedRefs(self.lib, h)
+
+    def predict_padded(self, prefs, cur_poc, pus, W, H, threads=1):
+        """predict() on pre-padded references, PU-parallel on `threads` host threads."""
+        pus = np.ascontiguousarray(pus)
+        dy = np.zeros((H, W), dtype=np.int16)
+        dcb = np.zeros((H // 2, W // 2), dtype=np.int16)
+        dcr = np.zeros((H // 2, W // 2), dtype=np.int16)
+        rc = self.lib.orc_pred_padded(self.h, prefs.h, cur_poc, c_void_p(pus.ctypes.data), len(pus),
+                                      c_void_p(dy.ctypes.data), W, c_void_p(dcb.ctypes.data),
+                                      c_void_p(dcr.ctypes.data), W // 2, int(threads))
+        if rc:
+            raise RuntimeError(f"oracle predict_padded failed: {rc}")
         return dy, dcb, dcr
 
     def predict_list(self, cur_poc, pus, list_, hp, refs, W, H):

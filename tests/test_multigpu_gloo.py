@@ -1,7 +1,9 @@
-"""CTU-row sharding + stripe all-gather on CPU with the gloo backend, world size 2.
+"""CTU-row sharding + the one packed stripe all-gather on CPU with the
+gloo backend, world sizes 2 and 3 (unequal stripes).
 
-Each rank predicts its stripe's PUs with the CPU twin of the device pipeline, all-gathers the
-stripes, and must end with exactly the unsharded full-picture prediction."""
+Each rank predicts its stripe's PUs with the CPU twin of the device pipeline, packs its stripe
+into its segment of the stripe-major picture (mm360.parallel.StripeLayout), runs the single
+in-place all-gather, and must end with exactly the unsharded full-picture prediction."""
 import os
 import socket
 
@@ -39,13 +41,41 @@ def _worker(rank, world, port, cfg_name, out_dir):
     mine = P.shard_pus(pus, cfg.height, world, rank)
     refs = {poc: W.ref_planes(cfg.width, cfg.height, poc) for poc in W.REF_POCS}
     epi = [(W.CUR_POC, -1, W.GED_EPIPOLE_Q24)]
-    y, cb, cr = twin.predict(params, W.CUR_POC, mine, refs, cfg.width, cfg.height, epi)
-    planes = [torch.from_numpy(y.copy()), torch.from_numpy(cb.copy()), torch.from_numpy(cr.copy())]
-    P.allgather_stripes(planes, cfg.height, world)
-    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), y=planes[0].numpy(), cb=planes[1].numpy(),
-             cr=planes[2].numpy(), n=len(mine))
+    planes = twin.predict(params, W.CUR_POC, mine, refs, cfg.width, cfg.height, epi)
+    layout = P.StripeLayout(cfg.width, cfg.height, world)
+    buf = np.full(layout.total, -5, dtype=np.int16)
+    layout.pack(planes, rank, buf)
+    t = torch.from_numpy(buf)
+    P.allgather_packed(t, layout)
+    y, cb, cr = layout.unpack(t.numpy())
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), y=y, cb=cb, cr=cr, n=len(mine))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def test_stripe_layout_pointers_and_unpack():
+    """The destination pointers of every rank land each stripe row in its own segment, and
+    pack/unpack invert each other (C3 at 1, 2, 3, 4, 8 ranks)."""
+    cfg = W.CONFIGS["C3"]
+    rng = np.random.default_rng(3)
+    planes = [rng.integers(-512, 1024, size=(cfg.height, cfg.width)).astype(np.int16),
+              rng.integers(-512, 1024, size=(cfg.height // 2, cfg.width // 2)).astype(np.int16),
+              rng.integers(-512, 1024, size=(cfg.height // 2, cfg.width // 2)).astype(np.int16)]
+    for world in (1, 2, 3, 4, 8):
+        lay = P.StripeLayout(cfg.width, cfg.height, world)
+        buf = np.zeros(lay.total, dtype=np.int16)
+        for r in range(world):
+            lay.pack(planes, r, buf)
+            y0, y1 = P.stripe_rows(cfg.height, world, r)
+            py, sy, pcb, pcr, sc = lay.dst_pointers(0, r)
+            # picture sample (y, x) of the stripe -> element (py + 2 (y sy + x)) / 2 of the buffer
+            for (y, x) in ((y0, 0), (y1 - 1, cfg.width - 1)):
+                assert buf[(py + 2 * (y * sy + x)) // 2] == planes[0][y, x]
+            for (y, x) in ((y0 // 2, 0), (y1 // 2 - 1, cfg.width // 2 - 1)):
+                assert buf[(pcb + 2 * (y * sc + x)) // 2] == planes[1][y, x]
+                assert buf[(pcr + 2 * (y * sc + x)) // 2] == planes[2][y, x]
+        for a, b in zip(lay.unpack(buf), planes):
+            assert np.array_equal(a, b)
 
 
 def test_stripes_partition_pus():
@@ -60,9 +90,8 @@ def test_stripes_partition_pus():
         assert all(rows[i][1] == rows[i + 1][0] for i in range(world - 1))
 
 
-@pytest.mark.parametrize("cfg_name", ["C1", "C2"])
-def test_gloo_world2_sharded_equals_full(tmp_path, cfg_name):
-    world = 2
+@pytest.mark.parametrize("cfg_name,world", [("C1", 2), ("C2", 2), ("C2", 3)])
+def test_gloo_sharded_equals_full(tmp_path, cfg_name, world):
     port = _free_port()
     mp.spawn(_worker, args=(world, port, cfg_name, str(tmp_path)), nprocs=world, join=True)
     import twin

@@ -20,7 +20,10 @@ for step in "$@"; do
     tests) run gpu_tests 900 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
-    prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
+    bench_c4) run bench_c4 600 python bench.py --config C4 ;;
+    c4_gloo2) run c4_gloo2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --dist-backend gloo --steps 6 --warmup 2 ;;
+    ubench) run ubench 300 bash -c "tools/ubench/load_check && tools/ubench/valu_rate2" ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 12 --warmup 4 --no-cpu-baseline ;;
     pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 ;;
     pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 ;;
     pmc_valu) run pmc_valu 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES -d gpurun_out/pmc_valu -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 ;;

@@ -111,11 +111,14 @@ MM_HD void classify_pu(const mm_pu_desc& u, const PicTables& t, PuPlan* p) {
     p->code = MM_ERR_ARG;
     return;
   }
-  if (t.only_list >= 0 && u.ref_poc[t.only_list] < 0) {  // mm_pred_list: the PU must use the list
+  // mm_pred_list: the PU must use the list (selects, not an index: a runtime index into `u` would
+  // demote the descriptor from registers to LDS)
+  if ((t.only_list == 0 && u.ref_poc[0] < 0) || (t.only_list == 1 && u.ref_poc[1] < 0)) {
     p->code = MM_ERR_ARG;
     return;
   }
   int used = 0;
+#pragma unroll
   for (int l = 0; l < 2; l++) {
     if (u.ref_poc[l] < 0 || (t.only_list >= 0 && l != t.only_list)) continue;
     used++;
@@ -142,6 +145,7 @@ MM_HD void classify_pu(const mm_pu_desc& u, const PicTables& t, PuPlan* p) {
     } else if (m >= GEODESIC_X && m <= GEODESIC_Z) {
       ged = m - GEODESIC_X;
     }
+#pragma unroll
     for (int comp = 0; comp < 2; comp++) {
       if (comp == 1 && !t.chroma) continue;
       if (comp == 1 && mpa_chroma_aliases(t, m, u.w, u.h)) {

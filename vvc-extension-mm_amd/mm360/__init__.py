@@ -435,6 +435,19 @@ class MMContext:
                                          c_void_p(_ptr(dst_cr)) if dst_cr is not None else None,
                                          dst_cb.stride(0) if dst_cb is not None else 0))
 
+    def run_raw(self, ptr_y: int, stride_y: int, ptr_cb: int, ptr_cr: int, stride_c: int):
+        """mm_pred_run into raw device addresses (e.g. a rank's segment of a packed picture,
+        parallel.StripeLayout.dst_pointers)."""
+        self._check(self.lib.mm_pred_run(self.h, c_void_p(ptr_y), stride_y, c_void_p(ptr_cb), c_void_p(ptr_cr),
+                                         stride_c))
+
+    def predict_device_raw(self, cur_poc: int, d_pus, ptr_y: int, stride_y: int, ptr_cb: int, ptr_cr: int,
+                           stride_c: int):
+        """mm_pred_device into raw device addresses."""
+        n = d_pus.numel() * d_pus.element_size() // PU_DTYPE.itemsize
+        self._check(self.lib.mm_pred_device(self.h, cur_poc, c_void_p(_ptr(d_pus)), n, c_void_p(ptr_y), stride_y,
+                                            c_void_p(ptr_cb), c_void_p(ptr_cr), stride_c))
+
     def last_timing_ms(self) -> float:
         ms = c_float()
         self._check(self.lib.mm_last_timing(self.h, byref(ms)))

@@ -1,14 +1,18 @@
-"""Multi-GPU partitioning of the MM motion-compensation path (SURVEY.md section 8(e)).
+"""Multi-GPU partitioning of the MM motion-compensation path (SURVEY.md section 8(e), config C4).
 
 Given the reference pictures, PUs are independent: MC reads only the references plus the PU's
 own descriptor.  A picture therefore shards by contiguous CTU-row stripes (PU -> rank owning
 the CTU row of its top-left sample); the references stay replicated on every GPU because MM
-motion can fetch anywhere in the picture (it wraps across the ERP seam).  After MC, one
-all-gather of the predicted stripes (RCCL over xGMI with the "nccl" backend; gloo on CPU)
-gives every rank the whole picture again, as a decoder needs for the next reference.
+motion can fetch anywhere in the picture (it wraps across the ERP seam, Projection.cpp:235, and is
+bounded only by the +-maxCU zeroing rule, InterPrediction.cpp:780).  After MC, ONE all-gather of
+the predicted stripes (RCCL over xGMI with the "nccl" backend; gloo on CPU) gives every rank the
+whole picture again, as a decoder needs for the next reference.
 
-The bench's default multi-GPU mode does not use this: every rank predicts its own picture
-(independent pictures, no data-path collective, weak scaling).
+The all-gather moves the picture in a stripe-major packed layout (StripeLayout): rank r's segment
+holds its luma rows, then its Cb rows, then its Cr rows, so one in-place all_gather_into_tensor of
+equal segments carries Y + Cb + Cr together and no staging copy exists -- each rank's kernels
+write their stripe straight into their own segment (the destination pointers are offset so that
+picture row y0 of the stripe lands at the segment start).
 """
 from __future__ import annotations
 
@@ -36,24 +40,63 @@ def max_stripe_rows(height: int, world: int, ctu: int = 128) -> int:
     return max(b - a for a, b in (stripe_rows(height, world, r, ctu) for r in range(world)))
 
 
-def allgather_stripes(planes: List, height: int, world: int, group=None, ctu: int = 128) -> None:
-    """In place: every rank contributes its stripe of each plane (torch tensors [H_c, W_c]) and
-    receives all the others.  Chroma planes (half height) use the halved stripe bounds."""
+class StripeLayout:
+    """Stripe-major packed 4:2:0 picture (int16 samples): segment r = Y rows of stripe r
+    (rows x W), then its Cb rows ((rows / 2) x W/2), then its Cr rows; every segment is sized for
+    the largest stripe so that the all-gather exchanges equal chunks."""
+
+    def __init__(self, width: int, height: int, world: int, ctu: int = 128):
+        self.W, self.H, self.world, self.ctu = width, height, world, ctu
+        self.rows = max_stripe_rows(height, world, ctu)
+        self.luma = self.rows * width
+        self.chroma = (self.rows // 2) * (width // 2)
+        self.seg = self.luma + 2 * self.chroma  # int16 elements per segment
+        self.total = self.seg * world
+
+    def dst_pointers(self, base_ptr: int, rank: int):
+        """(ptr_y, stride_y, ptr_cb, ptr_cr, stride_c) for rank's kernels writing into a packed
+        buffer at device address base_ptr: picture row y of the stripe maps to segment row
+        y - y0.  Only rows inside the stripe are ever written."""
+        y0, _ = stripe_rows(self.H, self.world, rank, self.ctu)
+        seg = base_ptr + 2 * rank * self.seg
+        py = seg - 2 * y0 * self.W
+        pcb = seg + 2 * self.luma - 2 * (y0 // 2) * (self.W // 2)
+        pcr = pcb + 2 * self.chroma
+        return py, self.W, pcb, pcr, self.W // 2
+
+    def pack(self, planes, rank: int, out: np.ndarray) -> None:
+        """Host helper: copy rank's stripe of full planes (Y, Cb, Cr) into its segment of `out`."""
+        y0, y1 = stripe_rows(self.H, self.world, rank, self.ctu)
+        s = out[rank * self.seg:(rank + 1) * self.seg]
+        s[: (y1 - y0) * self.W] = planes[0][y0:y1].reshape(-1)
+        c0, c1, wc = y0 // 2, y1 // 2, self.W // 2
+        s[self.luma:self.luma + (c1 - c0) * wc] = planes[1][c0:c1].reshape(-1)
+        s[self.luma + self.chroma:self.luma + self.chroma + (c1 - c0) * wc] = planes[2][c0:c1].reshape(-1)
+
+    def unpack(self, buf: np.ndarray):
+        """Full (Y, Cb, Cr) planes from a packed picture (host int16 array of `total` elements)."""
+        W, wc = self.W, self.W // 2
+        y = np.zeros((self.H, W), dtype=np.int16)
+        cb = np.zeros((self.H // 2, wc), dtype=np.int16)
+        cr = np.zeros_like(cb)
+        for r in range(self.world):
+            y0, y1 = stripe_rows(self.H, self.world, r, self.ctu)
+            s = buf[r * self.seg:(r + 1) * self.seg]
+            y[y0:y1] = s[: (y1 - y0) * W].reshape(y1 - y0, W)
+            c0, c1 = y0 // 2, y1 // 2
+            cb[c0:c1] = s[self.luma:self.luma + (c1 - c0) * wc].reshape(c1 - c0, wc)
+            cr[c0:c1] = s[self.luma + self.chroma:self.luma + self.chroma + (c1 - c0) * wc].reshape(c1 - c0, wc)
+        return y, cb, cr
+
+
+def allgather_packed(buf, layout: StripeLayout, group=None, async_op: bool = False):
+    """In place: the one collective of a sharded picture.  `buf` (torch int16, layout.total
+    elements) holds this rank's segment; afterwards every rank holds every segment.  int16 travels
+    bit-exactly as bytes (RCCL and gloo have no int16 type)."""
     import torch
     import torch.distributed as dist
 
     rank = dist.get_rank(group)
-    smax = max_stripe_rows(height, world, ctu)
-    for p in planes:
-        scale = height // p.shape[0]  # 1 luma, 2 chroma 4:2:0
-        y0, y1 = stripe_rows(height, world, rank, ctu)
-        rows = smax // scale
-        send = torch.zeros((rows, p.shape[1]), dtype=p.dtype, device=p.device)
-        send[: (y1 - y0) // scale] = p[y0 // scale: y1 // scale]
-        # int16 samples travel bit-exactly as uint8 (NCCL/RCCL and gloo have no int16 type)
-        send_b = send.view(torch.uint8)
-        recv = [torch.empty_like(send_b) for _ in range(world)]
-        dist.all_gather(recv, send_b, group=group)
-        for r in range(world):
-            a, b = stripe_rows(height, world, r, ctu)
-            p[a // scale: b // scale] = recv[r].view(p.dtype)[: (b - a) // scale]
+    b8 = buf.view(-1).view(torch.uint8)
+    seg = b8.numel() // layout.world
+    return dist.all_gather_into_tensor(b8, b8[rank * seg:(rank + 1) * seg], group=group, async_op=async_op)
