@@ -115,6 +115,9 @@ static float orc_rsqrtps1(float x) {
   return u2f(((uint32_t)(126 - half) << 23) | MM_RSQRTPS_MANT[e & 1][(ax >> 13) & 1023]);
 }
 static __m128 orc_psqrt(__m128 _x) {
+#if MM_PSQRT_EXACT
+  return _mm_sqrt_ps(_x);
+#endif
   float in[4], r[4];
   _mm_storeu_ps(in, _x);
   for (int i = 0; i < 4; i++) r[i] = orc_rsqrtps1(in[i]);
@@ -320,8 +323,29 @@ static void mpa_to_projection_arr(const Orc* o, int plane, const float* px, cons
   a3_free(q); a3_free(s);
 }
 
+/* Numerics modes (same switches as the product's mm_numerics.h): MM_ROUND_MODE,
+ * MM_PROD3_MODE, MM_TAN_CENTRE_MODE, MM_PSQRT_EXACT; 0 = the believed Eigen 3.3.7 behaviour. */
+#ifndef MM_ROUND_MODE
+#define MM_ROUND_MODE 0
+#endif
+#ifndef MM_PROD3_MODE
+#define MM_PROD3_MODE 0
+#endif
+#ifndef MM_TAN_CENTRE_MODE
+#define MM_TAN_CENTRE_MODE 0
+#endif
+#ifndef MM_PSQRT_EXACT
+#define MM_PSQRT_EXACT 0
+#endif
+
 /* Eigen lazy coefficient-based 3x3 product coefficient: p0 + (p1 + p2) */
-static float dot3(float a0, float b0, float a1, float b1, float a2, float b2) { return a0 * b0 + (a1 * b1 + a2 * b2); }
+static float dot3(float a0, float b0, float a1, float b1, float a2, float b2) {
+#if MM_PROD3_MODE
+  return (a0 * b0 + a1 * b1) + a2 * b2;
+#else
+  return a0 * b0 + (a1 * b1 + a2 * b2);
+#endif
+}
 static void matmul3(const float* A, const float* B, float* C) {
   float T[9];
   for (int i = 0; i < 3; i++)
@@ -458,7 +482,11 @@ static void tan_model(const Orc* o, const float* gx, const float* gy, int n, flo
   const float epsC = (float)(M_PI_2 - (double)tc);
   const float alphaC = pc;
   /* unqualified sin/cos on a float -> double ::sin/::cos, result promoted to float in the array expr */
+#if MM_TAN_CENTRE_MODE
+  const float sE = sinf(epsC), cE = cosf(epsC);
+#else
   const float sE = (float)sin((double)epsC), cE = (float)cos((double)epsC);
+#endif
   A3 c = a3_new(n);
   erp_to_sphere_arr(o, gx, gy, c, n);
   float *R = fa(n), *th = fa(n), *ph = fa(n);
@@ -624,7 +652,13 @@ static int reproject(Orc* o, int px_, int py_, int w, int h, int mvh, int mvv, i
     x = x - o->off;
     y = y - o->off;
     if (chroma) { x = x / scale; y = y / scale; }
+#if MM_ROUND_MODE
+    const int packet = n >= 4 && i < n - n % 4; /* pround = _mm_round_ps(x, 0): ties to even */
+    float rx = packet ? rintf(x * (float)(1 << shift)) : roundf(x * (float)(1 << shift));
+    float ry = packet ? rintf(y * (float)(1 << shift)) : roundf(y * (float)(1 << shift));
+#else
     float rx = roundf(x * (float)(1 << shift)), ry = roundf(y * (float)(1 << shift));
+#endif
     out[2 * i] = _mm_cvtt_ss2si(_mm_set_ss(rx));
     out[2 * i + 1] = _mm_cvtt_ss2si(_mm_set_ss(ry));
   }

@@ -20,10 +20,12 @@ def build():
     subprocess.check_call(["make", "-s", "-C", HERE])
 
 
-def load():
-    if not os.path.exists(LIB):
-        build()
-    lib = ctypes.CDLL(LIB)
+def load(variant=None):
+    """The oracle library; variant = a numerics-mode build ("round", "prod3", "tanc", "psqrt")."""
+    path = LIB if variant is None else os.path.join(HERE, "_build", f"libmmoracle_{variant}.so")
+    if not os.path.exists(path):
+        subprocess.check_call(["make", "-s", "-C", HERE] + ([] if variant is None else ["variants"]))
+    lib = ctypes.CDLL(path)
     lib.orc_create.restype = c_void_p
     lib.orc_create.argtypes = [c_void_p]
     lib.orc_destroy.argtypes = [c_void_p]
@@ -79,8 +81,8 @@ class _PaddedRefs:
 class Oracle:
     """CPU restatement of MVReprojection / xPredInterBlkMM for one sequence."""
 
-    def __init__(self, params, epipoles=()):
-        self.lib = load()
+    def __init__(self, params, epipoles=(), variant=None):
+        self.lib = load(variant)
         self.params = params
         self.h = self.lib.orc_create(ctypes.byref(params))
         for (cur, ref, q) in epipoles:

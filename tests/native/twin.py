@@ -10,10 +10,19 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "_build", "libhosttwin.so")
 
 
+_VARIANT = [None]  # numerics-mode build in use (None = default; "round", "prod3", "tanc", "psqrt")
+
+
+def use_variant(name):
+    """Route the following calls to a numerics-mode build (make -C tests/native variants)."""
+    _VARIANT[0] = name
+
+
 def load():
-    if not os.path.exists(LIB):
-        subprocess.check_call(["make", "-s", "-C", HERE])
-    lib = ctypes.CDLL(LIB)
+    path = LIB if _VARIANT[0] is None else os.path.join(HERE, "_build", f"libhosttwin_{_VARIANT[0]}.so")
+    if not os.path.exists(path):
+        subprocess.check_call(["make", "-s", "-C", HERE] + ([] if _VARIANT[0] is None else ["variants"]))
+    lib = ctypes.CDLL(path)
     lib.twin_reproject.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]
     lib.twin_pred.argtypes = [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p,
                               c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int]

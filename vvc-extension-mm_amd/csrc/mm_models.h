@@ -163,7 +163,11 @@ struct M3 {
   float m[9];
 };
 MM_HD float dot3_(float a0, float b0, float a1, float b1, float a2, float b2) {
+#if MM_PROD3_MODE
+  return (a0 * b0 + a1 * b1) + a2 * b2;
+#else
   return a0 * b0 + (a1 * b1 + a2 * b2);
+#endif
 }
 MM_HD M3 mat_mul(const M3& A, const M3& B) {
   M3 C;
@@ -287,8 +291,13 @@ MM_HD void block_setup_f(BlockSetup* b, const SeqConst& s, int model, bool luma,
       V3 sp = cart_to_sph(c3, sc, false);
       float epsC = (float)(PI_2_D - (double)sp.y);
       b->alphaC = sp.z;
+#if MM_TAN_CENTRE_MODE
+      b->sE = g_sinf(epsC);
+      b->cE = g_cosf(epsC);
+#else
       b->sE = sinf_via_double(epsC);   // unqualified sin(float) -> double ::sin
       b->cE = cosf_via_double(epsC);
+#endif
     } break;
     case THREE_D_TRANSLATIONAL: {  // ThreeDTranslationalMotionModel.cpp:7-24
       if (zero) { b->identity = 1; break; }
@@ -442,7 +451,12 @@ MM_HD void reproject_element(const SeqConst& s, const BlockSetup& b, float gx, f
     my = my / 2.0f;
   }
   const float scale = (float)(1 << (4 + chroma_shift));
+#if MM_ROUND_MODE
+  float rx = packet ? roundeven_(mx * scale) : roundf_(mx * scale);
+  float ry = packet ? roundeven_(my * scale) : roundf_(my * scale);
+#else
   float rx = roundf_(mx * scale), ry = roundf_(my * scale);
+#endif
   // cast<int>: x86 cvttss2si semantics for out-of-range values
   *fx = (fabsf_(rx) < 2147483648.0f) ? (int32_t)rx : (int32_t)0x80000000u;
   *fy = (fabsf_(ry) < 2147483648.0f) ? (int32_t)ry : (int32_t)0x80000000u;

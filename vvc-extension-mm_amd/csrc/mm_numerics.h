@@ -48,6 +48,27 @@ MM_HD bool isnanf_(float x) { return (asu(x) & 0x7fffffffu) > 0x7f800000u; }
 MM_HD float sqrtf_(float x) { return __builtin_sqrtf(x); }   // IEEE correctly rounded
 MM_HD double fma_(double a, double b, double c) { return __builtin_fma(a, b, c); }
 
+// ------------------------------------------------------------------------------------------
+// Numerics modes: every belief about Eigen 3.3.7 that cannot be verified
+// offline is a compile-time switch, defaulting to the belief.  tools/numerics_sensitivity.py
+// builds the CPU twin in each alternative mode and counts what changes at C3.
+//   MM_ROUND_MODE      0: std::round (ties away) for every element (A6 belief: cast<int> is not
+//                         packet-enabled, so the whole rounding expression is scalar)
+//                      1: packet elements use SSE4.1 pround (ties to even), tail elements std::round
+//   MM_PROD3_MODE      0: 3x3 product coefficient p0 + (p1 + p2) (A7 belief)   1: (p0 + p1) + p2
+//   MM_TAN_CENTRE_MODE 0: TAN centre terms via double ::sin / ::cos (A9)         1: float sinf / cosf
+//   MM_PSQRT_EXACT     0: psqrt = rsqrtps + one Newton step (A3 EIGEN_FAST_MATH) 1: IEEE sqrt
+// ------------------------------------------------------------------------------------------
+#ifndef MM_ROUND_MODE
+#define MM_ROUND_MODE 0
+#endif
+#ifndef MM_PROD3_MODE
+#define MM_PROD3_MODE 0
+#endif
+#ifndef MM_TAN_CENTRE_MODE
+#define MM_TAN_CENTRE_MODE 0
+#endif
+
 // std::round(float) == roundf: half-way cases away from zero (Eigen 3.3.7 round_impl with
 // EIGEN_HAS_CXX11_MATH -> std::round; MVReprojection.cpp:163-164).
 MM_HD float roundf_(float x) {
@@ -62,6 +83,8 @@ MM_HD float roundf_(float x) {
   uint32_t r = (ix + half) & ~frac_mask;
   return asf(r);
 }
+// _mm_round_ps(x, _MM_FROUND_TO_NEAREST_INT): ties to even (MM_ROUND_MODE 1 packet lanes)
+MM_HD float roundeven_(float x) { return __builtin_rintf(x); }
 
 // ------------------------------------------------------------------------------------------
 // glibc 2.35 sinf / cosf  (sysdeps/ieee754/flt-32/s_sinf.c, s_cosf.c, sincosf.h,
