@@ -143,7 +143,7 @@ static int twin_pred_list(const Twin& t, const mmdev::PicTables& tab, const mm_p
   for (int g = 0; g < m.n_elems; g++)
     reproj_thread_mc(g, find_item(job_off.data(), job_chunk.data(), g, m.n_jobs), t.sc, jobs.data(), job_off.data(),
                      setups.data(), c, mc);
-  const Taps taps{LUMA_T, CHROMA_T, nullptr};
+  const Taps taps{LUMA_T, CHROMA_T, nullptr, RefPool{}};
   Geometry geo = t.geo;
   geo.hp = hp;
   geo.store = store;
@@ -166,7 +166,7 @@ extern "C" int twin_pred(const mm_seq_params* p, int n_epi, const int32_t* epi, 
   EpipoleMap em = epi_of(n_epi, epi);
   std::vector<std::pair<int, RefDev>> refs;
   for (int i = 0; i < n_refs; i++)
-    refs.emplace_back(pocs[i], RefDev{ys[i], cbs ? cbs[i] : nullptr, crs ? crs[i] : nullptr, stride_y, stride_c});
+    refs.emplace_back(pocs[i], RefDev{ys[i], cbs ? cbs[i] : nullptr, crs ? crs[i] : nullptr, stride_y, stride_c, 0u, 0u});
   std::sort(refs.begin(), refs.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
   PicTables tab;
   std::string err;
@@ -187,7 +187,7 @@ extern "C" int twin_pred_list1(const mm_seq_params* p, int n_epi, const int32_t*
   EpipoleMap em = epi_of(n_epi, epi);
   std::vector<std::pair<int, RefDev>> refs;
   for (int i = 0; i < n_refs; i++)
-    refs.emplace_back(pocs[i], RefDev{ys[i], cbs ? cbs[i] : nullptr, crs ? crs[i] : nullptr, stride_y, stride_c});
+    refs.emplace_back(pocs[i], RefDev{ys[i], cbs ? cbs[i] : nullptr, crs ? crs[i] : nullptr, stride_y, stride_c, 0u, 0u});
   std::sort(refs.begin(), refs.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
   PicTables tab;
   std::string err;
@@ -280,7 +280,7 @@ extern "C" int twin_sad_window(const mm_seq_params* p, int n_epi, const int32_t*
   make_twin(p, &t);
   EpipoleMap em = epi_of(n_epi, epi);
   std::vector<std::pair<int, RefDev>> refs;
-  for (int i = 0; i < n_refs; i++) refs.emplace_back(pocs[i], RefDev{ys[i], nullptr, nullptr, stride_y, 0});
+  for (int i = 0; i < n_refs; i++) refs.emplace_back(pocs[i], RefDev{ys[i], nullptr, nullptr, stride_y, 0, 0u, 0u});
   std::sort(refs.begin(), refs.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
   PicTables tab;
   std::string err;
@@ -291,7 +291,7 @@ extern "C" int twin_sad_window(const mm_seq_params* p, int n_epi, const int32_t*
   rc = plan_me_window(seq_info(*p), tab, blocks, n, w, &batches, &err);
   if (rc) return rc;
   for (long i = 0; i < (long)n * w.C; i++) sads[i] = 0;
-  const Taps taps{LUMA_T, CHROMA_T, nullptr};
+  const Taps taps{LUMA_T, CHROMA_T, nullptr, RefPool{}};
   MpaCache c = cache_of(t);
   for (const MeBatch& bt : batches) {
     std::vector<BlockSetup> setups(bt.n_jobs);
@@ -325,7 +325,7 @@ extern "C" int twin_pred_dmvr(const mm_seq_params* p, int n_epi, const int32_t* 
   EpipoleMap em = epi_of(n_epi, epi);
   std::vector<std::pair<int, RefDev>> refs;
   for (int i = 0; i < n_refs; i++)
-    refs.emplace_back(pocs[i], RefDev{ys[i], cbs ? cbs[i] : nullptr, crs ? crs[i] : nullptr, stride_y, stride_c});
+    refs.emplace_back(pocs[i], RefDev{ys[i], cbs ? cbs[i] : nullptr, crs ? crs[i] : nullptr, stride_y, stride_c, 0u, 0u});
   std::sort(refs.begin(), refs.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
   PicTables tab;
   std::string err;
@@ -339,7 +339,7 @@ extern "C" int twin_pred_dmvr(const mm_seq_params* p, int n_epi, const int32_t* 
 #pragma omp parallel for schedule(static)
   for (int j = 0; j < ns * N_OFF * 2; j++) dmvr_setup_thread(j, t.sc, plan.sub.data(), tab.ged, setups.data());
   std::vector<uint32_t> costs((size_t)ns * N_OFF, 0);
-  const Taps taps{LUMA_T, CHROMA_T, nullptr};
+  const Taps taps{LUMA_T, CHROMA_T, nullptr, RefPool{}};
   MpaCache c = cache_of(t);
 #pragma omp parallel for schedule(static, 256)
   for (long g = 0; g < plan.n_elems; g++) {

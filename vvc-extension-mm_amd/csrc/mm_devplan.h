@@ -47,6 +47,7 @@ struct PicTables {
   uint32_t active;
   int nf_mod4;             // (W/4 * H/4) % 4, frame-cache packet tail (MPA chroma aliasing)
   int only_list;           // -1: normal prediction; 0/1: mm_pred_list of that list (other list ignored)
+  RefPool pool;            // the context's reference pool (device interior filters)
 };
 
 // Offsets of everything k_plan_place produced; written by k_plan_place's first thread.

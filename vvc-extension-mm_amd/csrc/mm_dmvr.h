@@ -79,8 +79,8 @@ MM_HD uint32_t dmvr_cost_thread(int g, int si, const SeqConst& sc, const Geometr
       for (int i = 0; i < 16; i++) p[l][i] = 0;
     } else if (window_interior<8, 4, 4>(xPos, yPos, geo.W, geo.H)) {
 #if defined(__HIP_DEVICE_COMPILE__)
-      predict_subblock_interior<8, 4, 4>(r.y, r.stride_y, xPos, yPos, taps.packed->lh[xFrac][(xPos - 3) & 1],
-                                         taps.packed->lv[yFrac], true, geo.bd, p[l]);
+      predict_subblock_pool<8, 4, 4>(taps.pool, r.off_y, 0, r.stride_y, xPos, yPos, taps.packed->lh[xFrac][(xPos - 3) & 1],
+                                     taps.packed->lv[yFrac], true, geo.bd, p[l]);
 #else
       predict_subblock_interior<8, 4, 4>(r.y, r.stride_y, xPos, yPos, taps.luma[xFrac], taps.luma[yFrac], true, geo.bd,
                                          p[l]);

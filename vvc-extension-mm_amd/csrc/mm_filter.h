@@ -13,6 +13,14 @@
 
 namespace mmflt {
 
+// The pool holding every resident reference picture of a context (device address, size, and the
+// constant distance from a picture's Cb plane to its Cr plane).
+struct RefPool {
+  const char* base;
+  uint32_t bytes;
+  int cr_delta;
+};
+
 // m_lumaFilter[16][8] (InterpolationFilter.cpp:82-100)
 #define MM_LUMA_TAPS_INIT                                                                           \
   {{0, 0, 0, 64, 0, 0, 0, 0},        {0, 1, -3, 63, 4, -2, 1, 0},     {-1, 2, -5, 62, 8, -3, 1, 0},   \
@@ -32,12 +40,15 @@ namespace mmflt {
    {0, 4, 62, -2},   {0, 2, 63, -1}}
 
 // Tap pairs for v_dot2 (int16 lo | int16 hi << 16), built at compile time from the tables above.
-// Horizontal pass, per phase and window-start parity p (the row is read from the even sample at
-// or below the window start, so p = 1 shifts every tap by one sample):
+// The device filter reads every window row as dwords from the even sample at or below its first
+// sample (4-byte aligned loads: 2-byte aligned dwordx4 loads measured 15-30 % slower in k_mc), so
+// dword m holds the aligned sample pair m and a window starting at an odd sample (parity p = 1)
+// is one sample into its first dword.  With
 //   A = (f0,f1) (f2,f3) ... (0,0)     B = (0,f0) (f1,f2) ... (f_{N-1},0)     C = (0,0) (f0,f1) ...
 //   p = 0: even outputs A, odd outputs B;   p = 1: even outputs B, odd outputs C
-// all applied to the aligned sample pairs starting at pair (c >> 1).  Vertical pass: even
-// output rows A without its zero pair, odd rows B, on the H-output row pairs (2m, 2m+1).
+// applied to the aligned pairs starting at pair (c >> 1), every output is N/2 + 1 dot2 whatever
+// the lane's parity (no divergence).  Vertical pass: even output rows A without its zero pair,
+// odd rows B, on the H-output row pairs (2m, 2m+1).
 struct PackedTaps {
   uint32_t lh[16][2][10];  // luma H  [phase][parity][even 5 | odd 5]
   uint32_t lv[16][9];      // luma V  [phase][even 4 | odd 5]
@@ -219,9 +230,6 @@ typedef short mm_short2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ int dot2_(uint32_t a, uint32_t b, int c) {
   return __builtin_amdgcn_sdot2(__builtin_bit_cast(mm_short2, a), __builtin_bit_cast(mm_short2, b), c, false);
 }
-__device__ __forceinline__ uint32_t pack2_(int lo, int hi) {
-  return ((uint32_t)lo & 0xffffu) | ((uint32_t)hi << 16);
-}
 __device__ __forceinline__ uint32_t pack_lo16_(uint32_t lo, uint32_t hi) {
   return __builtin_amdgcn_perm(hi, lo, 0x05040100u);  // (lo & 0xffff) | (hi << 16), one v_perm_b32
 }
@@ -232,27 +240,36 @@ __device__ __forceinline__ int dot2_seed_(uint32_t a, uint32_t b, int seed) {
   asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(seed));
   return r;
 }
-// predict_subblock for an interior window (device): the same integer sums, regrouped as packed
-// int16 pairs so that each pair of taps is one v_dot2:
-//  * a window row is loaded as dwords from the even sample at or below its start; dword m holds
-//    the aligned sample pair m;
-//  * output c of a row is the dot product of pairs (c >> 1) .. (c >> 1) + NT/2 with one of the
-//    precomputed tap-pair sets of PackedTaps (chosen by output parity and window parity);
-//  * the rounding offsets seed the dot2 chains; the H outputs (Pel, 16 bits) are packed as row
-//    pairs (one v_perm each) for the vertical pass, which uses the even/odd tap sets the same way.
-// ht: 2 * NQ H tap pairs (even outputs, odd outputs) for this window's phase and parity;
-// vt: NP + NQ V tap pairs (even rows, odd rows).
-// Window rows from a reference plane in global memory: row r starts at base + r * stride_dw.
-struct GlobalRows {
-  const uint32_t* base;  // dword holding the even sample at or below the window's first column
-  int stride_dw;
+
+// Window rows of a pooled reference plane through a flat pointer: `base` is the dword holding the
+// window's first sample; row r is base + r * row_bytes.  (Raw buffer loads with a per-row SGPR
+// offset instead of per-row 64-bit VGPR address arithmetic measured slower: k_mc 140 us vs 114 at
+// C3)
+struct PtrRows {
+  const char* base;
+  int row_bytes;
   template <int ND>
   __device__ __forceinline__ void load(int r, uint32_t* d) const {
-    load_dwords<ND>(base + (long)r * stride_dw, d);
+    typedef uint32_t u4 __attribute__((ext_vector_type(4), aligned(4)));
+    typedef uint32_t u2 __attribute__((ext_vector_type(2), aligned(4)));
+    typedef uint32_t u3 __attribute__((ext_vector_type(3), aligned(4)));
+    const char* p = base + (long)r * row_bytes;
+    if constexpr (ND == 6) {
+      const u4 a = *reinterpret_cast<const u4*>(p);
+      const u2 b = *reinterpret_cast<const u2*>(p + 16);
+      d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w; d[4] = b.x; d[5] = b.y;
+    } else {
+      static_assert(ND == 3, "luma (6) or chroma (3) dwords per window row");
+      const u3 a = *reinterpret_cast<const u3*>(p);
+      d[0] = a.x; d[1] = a.y; d[2] = a.z;
+    }
   }
 };
 
-// The same filter arithmetic over any row source (GlobalRows, or an LDS image of the window).
+// predict_subblock for an interior window (device): the same integer sums, regrouped as packed
+// int16 pairs so that each pair of taps is one v_dot2 (PackedTaps): the rounding offsets seed the
+// dot2 chains; the H outputs (Pel, 16 bits) are packed as row pairs (one v_perm each) for the
+// vertical pass.  ht / vt: the A | B pair sets of this sub-block's phases.
 template <int NT, int SBW, int SBH, class Rows>
 __device__ __forceinline__ void predict_rows(const Rows& rows, const uint32_t* __restrict__ ht,
                                              const uint32_t* __restrict__ vt, bool bi, int bd, int16_t* out) {
@@ -313,14 +330,15 @@ __device__ __forceinline__ void predict_rows(const Rows& rows, const uint32_t* _
     }
   }
 }
+// Interior window of sub-block (xPos, yPos) of a pooled plane whose first sample is at byte
+// `plane_off` of the pool (soff: uniform extra offset, e.g. Cr = Cb + cr_delta).
 template <int NT, int SBW, int SBH>
-__device__ __forceinline__ void predict_subblock_interior(const int16_t* __restrict__ ref, int stride, int xPos, int yPos,
-                                                          const uint32_t* __restrict__ ht,
-                                                          const uint32_t* __restrict__ vt, bool bi, int bd,
-                                                          int16_t* out) {
+__device__ __forceinline__ void predict_subblock_pool(const RefPool& pool, uint32_t plane_off, int soff,
+                                                      int stride, int xPos, int yPos, const uint32_t* __restrict__ ht,
+                                                      const uint32_t* __restrict__ vt, bool bi, int bd, int16_t* out) {
   constexpr int H0 = NT / 2 - 1;
-  const int x0 = xPos - H0;
-  const GlobalRows rows{reinterpret_cast<const uint32_t*>(ref + (long)(yPos - H0) * stride + (x0 & ~1)), stride >> 1};
+  const int x0 = (xPos - H0) & ~1;  // even sample at or below the window start: 4-byte aligned rows
+  const PtrRows rows{pool.base + plane_off + soff + (long)((yPos - H0) * stride + x0) * 2, stride * 2};
   predict_rows<NT, SBW, SBH>(rows, ht, vt, bi, bd, out);
 }
 #else

@@ -298,7 +298,8 @@ __global__ void __launch_bounds__(256) k_reproj_dev(SeqConst sc, const PlanMeta*
 // The tap-pair tables (4 KB) are copied into LDS once per workgroup: every lane indexes them by
 // its own phase, and from __constant__ memory those lookups are ~16 vector loads per wave that
 // compete with the reference-window loads for the texture-address path.
-__global__ void __launch_bounds__(256) k_mc_dev(Geometry geo, const PlanMeta* __restrict__ meta, McRec mc,
+// amdgpu_waves_per_eu(4): 126 VGPRs without spills, 4 waves per SIMD (130 VGPRs -> 3 otherwise)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_mc_dev(Geometry geo, const PlanMeta* __restrict__ meta, McRec mc,
                                                 const PicTables t, int16_t* __restrict__ dst_y, int dsy,
                                                 int16_t* __restrict__ dst_cb, int16_t* __restrict__ dst_cr, int dsc) {
   const int g = xcd_block() * blockDim.x + threadIdx.x;
@@ -309,7 +310,7 @@ __global__ void __launch_bounds__(256) k_mc_dev(Geometry geo, const PlanMeta* __
   if (threadIdx.x < sizeof(PackedTaps) / 16)
     reinterpret_cast<uint4*>(&s_taps)[threadIdx.x] = reinterpret_cast<const uint4*>(&c_packed_taps)[threadIdx.x];
   __syncthreads();
-  const Taps taps{c_luma_taps, c_chroma_taps, &s_taps};
+  const Taps taps{c_luma_taps, c_chroma_taps, &s_taps, t.pool};
   if (g >= n_sb) return;
   mc_thread_rec(g, sb_class(g, meta->sb_base), geo, taps, mc, t.ref, dst_y, dsy, dst_cb, dst_cr, dsc);
 }
@@ -342,7 +343,7 @@ __global__ void __launch_bounds__(256) k_me_sad(SeqConst sc, Geometry geo, MeWin
   int idx = -1 - lane;  // inactive lanes: distinct keys that never merge
   uint32_t v = 0;
   if (active) {
-    const Taps taps{c_luma_taps, c_chroma_taps, &c_packed_taps};
+    const Taps taps{c_luma_taps, c_chroma_taps, &c_packed_taps, t.pool};
     v = me_sad_thread(g, bi, sc, geo, taps, w, blocks, setups, cache, t.ref, org, org_stride, &idx);
   }
 #pragma unroll
@@ -379,7 +380,7 @@ __global__ void __launch_bounds__(256) k_dmvr_cost(SeqConst sc, Geometry geo, co
   int idx = -1 - lane;
   uint32_t v = 0;
   if (active) {
-    const Taps taps{c_luma_taps, c_chroma_taps, &c_packed_taps};
+    const Taps taps{c_luma_taps, c_chroma_taps, &c_packed_taps, t.pool};
     v = dmvr_cost_thread(g, si, sc, geo, taps, sp, setups, cache, t.ref, &idx);
   }
 #pragma unroll
@@ -454,6 +455,7 @@ struct RefHost {
   int16_t* cb = nullptr;
   int16_t* cr = nullptr;
   int stride_y = 0, stride_c = 0;
+  int slot = -1;  // picture slot in the context's reference pool (-1: own allocation, e.g. originals)
 };
 
 template <typename T>
@@ -518,6 +520,13 @@ struct mm_ctx {
   hipStream_t stream = nullptr;
   std::string err;
   std::map<int, RefHost> refs;
+  // Reference pool: every resident reference picture in one allocation of pool_cap picture slots
+  // (Y | Cb | Cr, rows 128-byte aligned); kernels address planes by 32-bit byte offsets from the
+  // pool base (RefDev::off_y / off_cb, mm_filter.h RefPool), so the pool stays below 2 GiB.
+  char* pool = nullptr;
+  size_t pic_bytes = 0;
+  int pool_cap = 0;
+  std::vector<int> pool_free;
   EpipoleMap epipoles;                            // the context's EpipoleList (mm_epipole.h)
   mm_epipole_list epi_handle{&epipoles, false};   // its C-ABI handle (mm_get_epipole_list)
   float* mpa_px[3] = {nullptr, nullptr, nullptr};
@@ -709,11 +718,7 @@ int mm_destroy(mm_ctx* c) {
   if (!c) return MM_ERR_ARG;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
-  for (auto& kv : c->refs) {
-    (void)hipFree(kv.second.y);
-    (void)hipFree(kv.second.cb);
-    (void)hipFree(kv.second.cr);
-  }
+  if (c->pool) (void)hipFree(c->pool);
   for (int pl = 0; pl < 3; pl++) {
     if (c->mpa_px[pl]) (void)hipFree(c->mpa_px[pl]);
     if (c->mpa_py[pl]) (void)hipFree(c->mpa_py[pl]);
@@ -818,29 +823,85 @@ int mm_epipole_derive_predictor(mm_epipole_list* e, int cur, int32_t q24[3]) {
 
 int mm_epipole_count(mm_epipole_list* e) { return e ? e->l->count() : -1; }
 
+static void place_ref(mm_ctx* c, RefHost& r) {
+  const int H = c->geo.H;
+  r.stride_y = (c->geo.W + 63) & ~63;
+  r.stride_c = (c->geo.Wc + 63) & ~63;
+  char* base = c->pool + (size_t)r.slot * c->pic_bytes;
+  r.y = reinterpret_cast<int16_t*>(base);
+  r.cb = c->geo.chroma ? reinterpret_cast<int16_t*>(base + (size_t)r.stride_y * H * 2) : nullptr;
+  r.cr = c->geo.chroma ? r.cb + (size_t)r.stride_c * c->geo.Hc : nullptr;
+}
+
+// A free picture slot of the reference pool; grows the pool (copying the resident pictures) when
+// full.  Growth waits for the context's work so no launch still reads the old allocation.
+static int take_pool_slot(mm_ctx* c, int* slot) {
+  if (!c->pic_bytes) {
+    const size_t sy = (size_t)((c->geo.W + 63) & ~63), sc = (size_t)((c->geo.Wc + 63) & ~63);
+    c->pic_bytes = 2 * (sy * c->geo.H + (c->geo.chroma ? 2 * sc * c->geo.Hc : 0));
+  }
+  if (c->pool_free.empty()) {
+    const size_t limit = ((size_t)1 << 31) - 1;
+    const int max_cap = (int)std::min<size_t>(limit / c->pic_bytes, 64);
+    if (c->pool_cap >= max_cap)
+      return fail(c, MM_ERR_ARG, "reference pool full (" + std::to_string(c->pool_cap) + " pictures, < 2 GiB)");
+    const int cap = std::min(max_cap, std::max(4, 2 * c->pool_cap));
+    char* np = nullptr;
+    HIPCHK(c, hipMalloc(&np, (size_t)cap * c->pic_bytes));
+    if (c->pool) {
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->aux));
+      HIPCHK(c, hipMemcpy(np, c->pool, (size_t)c->pool_cap * c->pic_bytes, hipMemcpyDeviceToDevice));
+      (void)hipFree(c->pool);
+    }
+    c->pool = np;
+    for (int k = cap - 1; k >= c->pool_cap; k--) c->pool_free.push_back(k);
+    c->pool_cap = cap;
+    for (auto& kv : c->refs) place_ref(c, kv.second);
+  }
+  *slot = c->pool_free.back();
+  c->pool_free.pop_back();
+  return MM_OK;
+}
+
+static RefPool pool_of(const mm_ctx* c) {
+  const int cr_delta = c->geo.chroma ? 2 * ((c->geo.Wc + 63) & ~63) * c->geo.Hc : 0;
+  return RefPool{c->pool, (uint32_t)((size_t)c->pool_cap * c->pic_bytes), cr_delta};
+}
+
+// Reference slots of a picture: every resident reference, POC order, with its pool offsets
+static std::vector<std::pair<int, RefDev>> ref_slots(const mm_ctx* c) {
+  std::vector<std::pair<int, RefDev>> refs;
+  for (auto& kv : c->refs) {
+    const RefHost& h = kv.second;
+    const uint32_t oy = (uint32_t)((const char*)h.y - c->pool);
+    const uint32_t oc = h.cb ? (uint32_t)((const char*)h.cb - c->pool) : 0u;
+    refs.emplace_back(kv.first, RefDev{h.y, h.cb, h.cr, h.stride_y, h.stride_c, oy, oc});
+  }
+  return refs;
+}
+
 int mm_upload_ref(mm_ctx* c, int poc, const int16_t* y, ptrdiff_t sy, const int16_t* cb, const int16_t* cr,
                   ptrdiff_t sc_, int src_dev) {
   if (!c || !y) return MM_ERR_ARG;
   if (c->geo.chroma && (!cb || !cr)) return fail(c, MM_ERR_ARG, "chroma planes required for 4:2:0");
   HIPCHK(c, hipSetDevice(c->device));
+  if (!c->refs.count(poc)) {
+    int slot = -1;
+    RCCHK(take_pool_slot(c, &slot));
+    RefHost& r = c->refs[poc];
+    r.slot = slot;
+    place_ref(c, r);
+  }
   RefHost& r = c->refs[poc];
   const int W = c->geo.W, H = c->geo.H, Wc = c->geo.Wc, Hc = c->geo.Hc;
-  if (!r.y) {
-    r.stride_y = (W + 63) & ~63;
-    r.stride_c = (Wc + 63) & ~63;
-    HIPCHK(c, hipMalloc(&r.y, (size_t)r.stride_y * H * sizeof(int16_t)));
-    if (c->geo.chroma) {
-      HIPCHK(c, hipMalloc(&r.cb, (size_t)r.stride_c * Hc * sizeof(int16_t)));
-      HIPCHK(c, hipMalloc(&r.cr, (size_t)r.stride_c * Hc * sizeof(int16_t)));
-    }
-  }
   hipMemcpyKind k = src_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
   HIPCHK(c, hipMemcpy2DAsync(r.y, r.stride_y * 2, y, sy * 2, W * 2, H, k, c->stream));
   if (c->geo.chroma) {
     HIPCHK(c, hipMemcpy2DAsync(r.cb, r.stride_c * 2, cb, sc_ * 2, Wc * 2, Hc, k, c->stream));
     HIPCHK(c, hipMemcpy2DAsync(r.cr, r.stride_c * 2, cr, sc_ * 2, Wc * 2, Hc, k, c->stream));
   }
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (!src_dev) HIPCHK(c, hipStreamSynchronize(c->stream));  // host source buffers may be reused at once
   return MM_OK;
 }
 
@@ -848,11 +909,8 @@ int mm_release_ref(mm_ctx* c, int poc) {
   if (!c) return MM_ERR_ARG;
   auto it = c->refs.find(poc);
   if (it == c->refs.end()) return fail(c, MM_ERR_NOREF, "reference POC not uploaded");
-  (void)hipStreamSynchronize(c->stream);
-  (void)hipFree(it->second.y);
-  (void)hipFree(it->second.cb);
-  (void)hipFree(it->second.cr);
-  c->refs.erase(it);
+  c->pool_free.push_back(it->second.slot);  // stream-ordered: later uploads into the slot follow
+  c->refs.erase(it);                        // every launch already queued on the context stream
   return MM_OK;
 }
 
@@ -939,12 +997,12 @@ static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, in
                               int16_t* dcb, int16_t* dcr, ptrdiff_t sdc, int only_list = -1, int hp = 0,
                               int store = 3) {
   std::vector<std::pair<int, RefDev>> refs;
-  for (auto& kv : c->refs)
-    refs.emplace_back(kv.first, RefDev{kv.second.y, kv.second.cb, kv.second.cr, kv.second.stride_y, kv.second.stride_c});
+  refs = ref_slots(c);
   PicTables t;
   std::string err;
   int rc = build_pic_tables(seq_info(c->prm), c->epipoles, cur_poc, refs, &t, &err);
   if (rc) return fail(c, rc, err);
+  t.pool = pool_of(c);
   t.only_list = only_list;
   Geometry geo = c->geo;
   geo.hp = hp;
@@ -1084,12 +1142,12 @@ int mm_sad_window(mm_ctx* c, int cur_poc, const mm_me_block* blocks, int n, int 
   auto oit = c->orgs.find(cur_poc);
   if (oit == c->orgs.end()) return fail(c, MM_ERR_ARG, "no original picture uploaded for the current POC");
   std::vector<std::pair<int, RefDev>> refs;
-  for (auto& kv : c->refs)
-    refs.emplace_back(kv.first, RefDev{kv.second.y, kv.second.cb, kv.second.cr, kv.second.stride_y, kv.second.stride_c});
+  refs = ref_slots(c);
   PicTables t;
   std::string err;
   int rc = build_pic_tables(seq_info(c->prm), c->epipoles, cur_poc, refs, &t, &err);
   if (rc) return fail(c, rc, err);
+  t.pool = pool_of(c);
   MeWindow w;
   w.range = range;
   w.step = step;
@@ -1126,12 +1184,12 @@ int mm_pred_dmvr(mm_ctx* c, int cur_poc, const mm_pu_desc* pus, int n, int16_t* 
   if (n == 0) return MM_OK;
   HIPCHK(c, hipSetDevice(c->device));
   std::vector<std::pair<int, RefDev>> refs;
-  for (auto& kv : c->refs)
-    refs.emplace_back(kv.first, RefDev{kv.second.y, kv.second.cb, kv.second.cr, kv.second.stride_y, kv.second.stride_c});
+  refs = ref_slots(c);
   PicTables t;
   std::string err;
   int rc = build_pic_tables(seq_info(c->prm), c->epipoles, cur_poc, refs, &t, &err);
   if (rc) return fail(c, rc, err);
+  t.pool = pool_of(c);
   DmvrPlan plan;
   rc = plan_dmvr(seq_info(c->prm), t, pus, n, &plan, &err);
   if (rc) return fail(c, rc, err);

@@ -86,8 +86,8 @@ MM_HD uint32_t me_sad_thread(int g, int bi, const SeqConst& sc, const Geometry& 
     const RefDev r = refs[b.slot];
     if (window_interior<8, 4, 4>(xPos, yPos, geo.W, geo.H)) {
 #if defined(__HIP_DEVICE_COMPILE__)
-      predict_subblock_interior<8, 4, 4>(r.y, r.stride_y, xPos, yPos, taps.packed->lh[xFrac][(xPos - 3) & 1],
-                                         taps.packed->lv[yFrac], false, geo.bd, p);
+      predict_subblock_pool<8, 4, 4>(taps.pool, r.off_y, 0, r.stride_y, xPos, yPos, taps.packed->lh[xFrac][(xPos - 3) & 1],
+                                     taps.packed->lv[yFrac], false, geo.bd, p);
 #else
       predict_subblock_interior<8, 4, 4>(r.y, r.stride_y, xPos, yPos, taps.luma[xFrac], taps.luma[yFrac], false, geo.bd,
                                          p);

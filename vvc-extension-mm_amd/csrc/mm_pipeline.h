@@ -16,6 +16,7 @@ struct RefDev {
   const int16_t* cb;
   const int16_t* cr;
   int stride_y, stride_c;
+  uint32_t off_y, off_cb;  // byte offsets of the Y and Cb planes in the context's RefPool
 };
 
 // One reprojection job == one reprojectMotionVectorSubblocks call
@@ -85,6 +86,7 @@ struct Taps {
   const int8_t (*luma)[8];
   const int8_t (*chroma)[4];
   const PackedTaps* packed;  // tap pairs of the device interior filter
+  RefPool pool;              // the reference pool the device interior filter reads through
 };
 
 // item containing flat index g: chunk_start[g/64] is the item holding g rounded down to 64
@@ -294,8 +296,8 @@ MM_HD void mc_thread_rec(int g, int cls, const Geometry& geo, const Taps& taps, 
         for (int i = 0; i < 16; i++) pl[l][i] = 0;
       } else if (window_interior<8, 4, 4>(xPos, yPos, geo.W, geo.H)) {
 #if defined(__HIP_DEVICE_COMPILE__)
-        predict_subblock_interior<8, 4, 4>(r.y, r.stride_y, xPos, yPos, taps.packed->lh[xFrac][(xPos - 3) & 1],
-                                           taps.packed->lv[yFrac], hp, geo.bd, pl[l]);
+        predict_subblock_pool<8, 4, 4>(taps.pool, r.off_y, 0, r.stride_y, xPos, yPos, taps.packed->lh[xFrac][(xPos - 3) & 1],
+                                       taps.packed->lv[yFrac], hp, geo.bd, pl[l]);
 #else
         predict_subblock_interior<8, 4, 4>(r.y, r.stride_y, xPos, yPos, taps.luma[xFrac], taps.luma[yFrac], hp,
                                            geo.bd, pl[l]);
@@ -330,8 +332,9 @@ MM_HD void mc_thread_rec(int g, int cls, const Geometry& geo, const Taps& taps, 
 #if defined(__HIP_DEVICE_COMPILE__)
       const uint32_t* ht = taps.packed->ch[xFrac][(xPos - 1) & 1];
       const uint32_t* vt = taps.packed->cv[yFrac];
-      predict_subblock_interior<4, 2, 2>(r.cb, r.stride_c, xPos, yPos, ht, vt, hp, geo.bd, pcb[l]);
-      predict_subblock_interior<4, 2, 2>(r.cr, r.stride_c, xPos, yPos, ht, vt, hp, geo.bd, pcr[l]);
+      predict_subblock_pool<4, 2, 2>(taps.pool, r.off_cb, 0, r.stride_c, xPos, yPos, ht, vt, hp, geo.bd, pcb[l]);
+      predict_subblock_pool<4, 2, 2>(taps.pool, r.off_cb, taps.pool.cr_delta, r.stride_c, xPos, yPos, ht, vt, hp, geo.bd,
+                                     pcr[l]);
 #else
       predict_subblock_interior<4, 2, 2>(r.cb, r.stride_c, xPos, yPos, taps.chroma[xFrac], taps.chroma[yFrac], hp,
                                          geo.bd, pcb[l]);
