@@ -149,7 +149,10 @@ static int twin_pred_list(const Twin& t, const mmdev::PicTables& tab, const mm_p
   geo.store = store;
 #pragma omp parallel for schedule(static, 256)
   for (int g = 0; g < m.n_sb; g++)
-    mc_thread_rec(g, sb_class(g, m.sb_base), geo, taps, mc, tab.ref, dy, sdy, dcb, dcr, sdc);
+    if (geo.hp)
+      mc_thread_rec<true>(g, sb_class(g, m.sb_base), geo, taps, mc, tab.ref, dy, sdy, dcb, dcr, sdc);
+    else
+      mc_thread_rec<false>(g, sb_class(g, m.sb_base), geo, taps, mc, tab.ref, dy, sdy, dcb, dcr, sdc);
   return 0;
 }
 

@@ -120,7 +120,11 @@ MM_HD FiltParam filt_param(bool isFirst, bool isLast, int bd) {
   return {shift, offset, isLast};
 }
 
-MM_HD int16_t clip_pel(int v, int maxv) { return (int16_t)(v < 0 ? 0 : (v > maxv ? maxv : v)); }
+// ClipPel to [0, maxv]; written as max/min so that the device compiler emits one v_med3_i32
+MM_HD int16_t clip_pel(int v, int maxv) {
+  const int lo = v > 0 ? v : 0;
+  return (int16_t)(lo < maxv ? lo : maxv);
+}
 
 // Out-of-range rule of xPredInterBlkMM (InterPrediction.cpp:780): sub-block predicts zeros
 MM_HD bool sb_out_of_range(int xPos, int yPos, int Wc, int Hc, int maxCUw, int maxCUh, int sbw, int sbh) {
@@ -324,9 +328,11 @@ __device__ __forceinline__ void predict_rows(const Rows& rows, const uint32_t* _
 #pragma unroll
         for (int k = 1; k < NP; k++) sum = dot2_(pr[(r >> 1) + k], ve[k], sum);
       }
-      int v = (int16_t)(sum >> fv.shift);
-      if (fv.clip) v = clip_pel(v, maxv);
-      out[r * SBW + c] = (int16_t)v;
+      // isLast: ClipPel of the int result (its magnitude is far below 2^15, so the Pel cast
+      // the hp path needs is the identity there); callers pass `bi` as a compile-time constant
+      // through the inlined chain, so only one of the two forms is emitted
+      const int v = sum >> fv.shift;
+      out[r * SBW + c] = fv.clip ? clip_pel(v, maxv) : (int16_t)v;
     }
   }
 }

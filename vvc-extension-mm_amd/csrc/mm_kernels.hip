@@ -299,6 +299,7 @@ __global__ void __launch_bounds__(256) k_reproj_dev(SeqConst sc, const PlanMeta*
 // its own phase, and from __constant__ memory those lookups are ~16 vector loads per wave that
 // compete with the reference-window loads for the texture-address path.
 // amdgpu_waves_per_eu(4): 126 VGPRs without spills, 4 waves per SIMD (130 VGPRs -> 3 otherwise)
+template <bool UNI_HP>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_mc_dev(Geometry geo, const PlanMeta* __restrict__ meta, McRec mc,
                                                 const PicTables t, int16_t* __restrict__ dst_y, int dsy,
                                                 int16_t* __restrict__ dst_cb, int16_t* __restrict__ dst_cr, int dsc) {
@@ -312,7 +313,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   __syncthreads();
   const Taps taps{c_luma_taps, c_chroma_taps, &s_taps, t.pool};
   if (g >= n_sb) return;
-  mc_thread_rec(g, sb_class(g, meta->sb_base), geo, taps, mc, t.ref, dst_y, dsy, dst_cb, dst_cr, dsc);
+  mc_thread_rec<UNI_HP>(g, sb_class(g, meta->sb_base), geo, taps, mc, t.ref, dst_y, dsy, dst_cb, dst_cr, dsc);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -462,14 +463,19 @@ template <typename T>
 struct DevBuf {
   T* p = nullptr;
   size_t cap = 0;
-  hipError_t ensure(size_t n) {
+  // fresh (optional): set when the buffer was (re)allocated by this call
+  hipError_t ensure(size_t n, bool* fresh = nullptr) {
+    if (fresh) *fresh = false;
     if (n <= cap && p) return hipSuccess;
     if (p) (void)hipFree(p);
     p = nullptr;
     cap = 0;
     size_t want = std::max<size_t>(n, 1);
     hipError_t e = hipMalloc(&p, want * sizeof(T));
-    if (e == hipSuccess) cap = want;
+    if (e == hipSuccess) {
+      cap = want;
+      if (fresh) *fresh = true;
+    }
     return e;
   }
   void release() {
@@ -945,14 +951,25 @@ static int ensure_slot_buffers(mm_ctx* c, PlanSlot& S, int n) {
   k.sb = (int)std::min<long>((long)n * 1024, area_sb);
   k.elems = 4 * k.sb;
   S.caps = k;
-  HIPCHK(c, S.jobs.ensure(k.jobs));
+  bool fresh_jobs = false;
+  HIPCHK(c, S.jobs.ensure(k.jobs, &fresh_jobs));
+  if (fresh_jobs) HIPCHK(c, hipMemsetAsync(S.jobs.p, 0, S.jobs.cap * sizeof(JobDev), c->stream));
   HIPCHK(c, S.job_off.ensure(k.jobs));
   HIPCHK(c, S.job_chunk.ensure(k.elems / 64 + 1));
   HIPCHK(c, S.setup.ensure(k.jobs));
   HIPCHK(c, S.meta.ensure(1));
   HIPCHK(c, S.blk.ensure((size_t)((n + PLAN_BLOCK - 1) / PLAN_BLOCK) * N_KEYS));
-  HIPCHK(c, S.mc_meta.ensure(k.sb));
-  for (int l = 0; l < 2; l++) HIPCHK(c, S.mc_pos[l].ensure(k.sb));
+  // The records k_reproj/k_mc exchange are zeroed once when allocated: every record a plan
+  // counts is written before it is read (classify_pu decides counts and emission alike), and a
+  // record that never was written still holds in-picture values (position 0, slot 0), never
+  // uninitialised memory that k_mc would use as a destination offset.
+  bool fresh = false;
+  HIPCHK(c, S.mc_meta.ensure(k.sb, &fresh));
+  if (fresh) HIPCHK(c, hipMemsetAsync(S.mc_meta.p, 0, S.mc_meta.cap * sizeof(mm_int2), c->stream));
+  for (int l = 0; l < 2; l++) {
+    HIPCHK(c, S.mc_pos[l].ensure(k.sb, &fresh));
+    if (fresh) HIPCHK(c, hipMemsetAsync(S.mc_pos[l].p, 0, S.mc_pos[l].cap * sizeof(mm_int4), c->stream));
+  }
   return MM_OK;
 }
 
@@ -981,7 +998,10 @@ static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables
   hipLaunchKernelGGL(k_reproj_dev, dim3(gr), dim3(256), 0, st, c->sc, S.meta.p, S.jobs.p, S.job_off.p, S.job_chunk.p,
                      S.setup.p, make_cache(c), mc);
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[2], st));
-  hipLaunchKernelGGL(k_mc_dev, dim3(gm), dim3(256), 0, st, geo, S.meta.p, mc, t, dy, (int)sdy, dcb, dcr, (int)sdc);
+  if (geo.hp)
+    hipLaunchKernelGGL(k_mc_dev<true>, dim3(gm), dim3(256), 0, st, geo, S.meta.p, mc, t, dy, (int)sdy, dcb, dcr, (int)sdc);
+  else
+    hipLaunchKernelGGL(k_mc_dev<false>, dim3(gm), dim3(256), 0, st, geo, S.meta.p, mc, t, dy, (int)sdy, dcb, dcr, (int)sdc);
   HIPCHK(c, hipGetLastError());
   return MM_OK;
 }

@@ -270,10 +270,13 @@ MM_HD int16_t weighted_avg(int p0, int p1, int w0, int w1, int bd) {
 // (InterPrediction.cpp:776-828), then xWeightedAverage (addAvg / addWeightedAvg for bi, the
 // rndRes uni prediction otherwise, InterPrediction.cpp:1584-1679).  cls = 0 bi, 1 uni L0, 2 uni
 // L1 (sb_class of g's PU bucket).  geo.hp (mm_pred_list): the 14-bit intermediate of the one list.
-MM_HD void mc_thread_rec(int g, int cls, const Geometry& geo, const Taps& taps, const McRec& mc, const RefDev* refs,
-                         int16_t* dst_y, int dsy, int16_t* dst_cb, int16_t* dst_cr, int dsc) {
-  const bool bi = cls == 0;
-  const bool hp = bi || geo.hp;  // keep the 14-bit intermediate (rndRes = !bi)
+// BI / HP are compile-time (mc_thread_rec dispatches on the wave-uniform class), so the bi path
+// carries no clipping and the uni path no runtime rounding-mode selects.
+template <bool BI, bool HP>
+MM_HD void mc_rec_impl(int g, int cls, const Geometry& geo, const Taps& taps, const McRec& mc, const RefDev* refs,
+                       int16_t* dst_y, int dsy, int16_t* dst_cb, int16_t* dst_cr, int dsc) {
+  constexpr bool bi = BI;
+  constexpr bool hp = HP;  // keep the 14-bit intermediate (rndRes = !bi)
   const int uni_list = cls == 2 ? 1 : 0;
   const bool used[2] = {bi || uni_list == 0, bi || uni_list == 1};
   const mm_int2 meta = mc.meta[g];
@@ -361,6 +364,19 @@ MM_HD void mc_thread_rec(int g, int cls, const Geometry& geo, const Taps& taps, 
     store_row<2>(dst_cb + (long)(cy + r) * dsc + cx, ob, geo.vec_store);
     store_row<2>(dst_cr + (long)(cy + r) * dsc + cx, orr, geo.vec_store);
   }
+}
+
+// UNI_HP: mm_pred_list with hp = 1 (every sub-block is uni and keeps the 14-bit intermediate);
+// a separate kernel instance, so the picture path's register allocation does not carry it.
+template <bool UNI_HP = false>
+MM_HD void mc_thread_rec(int g, int cls, const Geometry& geo, const Taps& taps, const McRec& mc, const RefDev* refs,
+                         int16_t* dst_y, int dsy, int16_t* dst_cb, int16_t* dst_cr, int dsc) {
+  if constexpr (UNI_HP)
+    mc_rec_impl<false, true>(g, cls, geo, taps, mc, refs, dst_y, dsy, dst_cb, dst_cr, dsc);
+  else if (cls == 0)
+    mc_rec_impl<true, true>(g, cls, geo, taps, mc, refs, dst_y, dsy, dst_cb, dst_cr, dsc);
+  else
+    mc_rec_impl<false, false>(g, cls, geo, taps, mc, refs, dst_y, dsy, dst_cb, dst_cr, dsc);
 }
 
 }  // namespace mmpipe
