@@ -330,6 +330,41 @@ def bench_c4(args, cfg, params, rank, world, local, dist):
     ctx.close()
 
 
+def bench_c4_emulate(args, cfg, params):
+    """C4 rehearsal on ONE GPU (not a bench line): for N = 2, 4, 8 the per-GPU MC time of every
+    rank's CTU-row stripe (ranks run one after another here, so the max over ranks is the N-GPU
+    step time of the MC part), then the predicted per-picture time of the N-GPU C4 loop, with the
+    stripe all-gather (N-1)/N x 56.6 MB inbound per rank modelled at one xGMI link per direction
+    (ring, ~153 GB/s) and at all 7 links (direct, 7 x 153 GB/s), hidden behind the next picture's MC
+    (two picture buffers: max(mc, allgather)) or not (mc + allgather)."""
+    (cur, pus, refs), = picture_set(cfg, 1)
+    ctx = new_ctx(params, 0, [(cur, pus, refs)])
+    area = W.luma_area(pus)
+    pic_bytes = cfg.width * cfg.height * 2 * 3 // 2
+    dy, dcb, dcr = planes(cfg)
+    out = {"note": "one-GPU rehearsal: measured stripe MC times, all-gather times modelled", "n": {}}
+    link = 153e9
+    for n in (1, 2, 4, 8):
+        worst = 0.0
+        for r in range(n):
+            mine = P.shard_pus(pus, cfg.height, n, r)
+            ctx.prepare(cur, mine)
+            t = timed(args.steps, args.warmup, lambda s: ctx.run(dy, dcb, dcr), None)
+            worst = max(worst, t / args.steps)
+        ag = (n - 1) / n * pic_bytes
+        ring, mesh = ag / link, ag / (7 * link) if n > 1 else 0.0
+        out["n"][n] = {"mc_ms": round(worst * 1e3, 4),
+                       "allgather_ms": {"ring": round(ring * 1e3, 4), "mesh": round(mesh * 1e3, 4)},
+                       "pred_ms_per_picture": {"hidden_ring": round(max(worst, ring) * 1e3, 4),
+                                               "hidden_mesh": round(max(worst, mesh) * 1e3, 4),
+                                               "serial_ring": round((worst + ring) * 1e3, 4)},
+                       "pred_mpix_s": {"hidden_ring": round(area / max(worst, ring) / 1e6, 1),
+                                       "hidden_mesh": round(area / max(worst, mesh) / 1e6, 1),
+                                       "mc_only": round(area / worst / 1e6, 1)}}
+    print(json.dumps(out), flush=True)
+    ctx.close()
+
+
 def bench_me(args, cfg, params, rank, world, local, dist):
     """C5: encoder ME candidate evaluation -- every block of the 16x16 PU grid once per model, a
     33x33 integer window each, reprojection + 8-tap + SAD per candidate (mm_sad_window).  Each
@@ -409,6 +444,8 @@ def main():
     ap.add_argument("--kernel-steps", type=int, default=8, help="extra steps timed per launch with HIP events")
     ap.add_argument("--lib", default=None, help="alternative build of libmm360.so (A/B experiments)")
     ap.add_argument("--stripes", type=int, default=None, help="mm_set_stripes (default: the library's)")
+    ap.add_argument("--c4-emulate", action="store_true",
+                    help="C4 rehearsal on one GPU: per-rank stripe MC times for N = 2, 4, 8 + modelled all-gather")
     ap.add_argument("--coherent-mv", action="store_true",
                     help="experiment: one MV for every PU and list (spatially coherent motion)")
     ap.add_argument("--uniform-model", type=int, default=None,
@@ -439,6 +476,8 @@ def main():
     params = mm360.seq_params(cfg.width, cfg.height, cfg.models)
     if args.config == "C5":
         bench_me(args, cfg, params, rank, world, local, dist)
+    elif args.config == "C4" and args.c4_emulate:
+        bench_c4_emulate(args, cfg, params)
     elif args.config == "C4":
         bench_c4(args, cfg, params, rank, world, local, dist)
     else:

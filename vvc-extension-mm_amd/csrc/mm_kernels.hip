@@ -89,21 +89,28 @@ __device__ __forceinline__ int xcd_block() {
   return grp * (8 * XCD_RUN) + (r & 7) * XCD_RUN + (r >> 3);
 }
 
-// Planning runs in 1024-thread blocks without global atomics: k_plan_count writes each block's
-// bucket counts to its own row of `blk`; every k_plan_place block sums the column of each bucket
-// (the bucket total) and the part of it above its own row (its offset inside the bucket).  PUs
-// therefore land in their buckets in input order, block by block.
+// Planning runs without global atomics: k_plan_count (1024-thread blocks) writes each block's
+// bucket counts to its own row of `blk`, and those of each of its four 256-PU quarters to their
+// rows of `blkq`; every k_plan_place block (256 threads, one quarter) sums the column of each bucket
+// over the count blocks (the bucket total) and the part above its own count block, plus the
+// quarters before it inside that block (its offset inside the bucket).  PUs therefore land in their
+// buckets in input order, quarter by quarter.  Placement uses 256-thread blocks because its
+// scattered record stores are bound by the texture-address path of the CUs it runs on: 1024-thread
+// blocks put 16 storing waves on each of only n / 1024 CUs (profiles/r02_ab_plan_place.txt).
 constexpr int PLAN_BLOCK = 1024;
-constexpr int N_KEYS = N_PU_KEYS + N_JOB_KEYS;  // one row of `blk`: PU buckets, then job buckets
+constexpr int PLACE_BLOCK = 256;
+constexpr int PLAN_Q = PLAN_BLOCK / PLACE_BLOCK;  // quarters per count block
+constexpr int N_KEYS = N_PU_KEYS + N_JOB_KEYS;    // one row of `blk`: PU buckets, then job buckets
 
 // status: the picture's validation word (0 = ok, else ~((pu_index << 8) | code) of the lowest
 // failing PU, combined with atomicMax over every stripe of the picture).
 __global__ void __launch_bounds__(PLAN_BLOCK) k_plan_count(const mm_pu_desc* __restrict__ pus, int n, int pu_base,
                                                     const PicTables t, unsigned long long* __restrict__ status,
-                                                    unsigned long long* __restrict__ blk) {
-  __shared__ unsigned long long s_cnt[N_KEYS], s_status;
-  const int tid = threadIdx.x;
-  if (tid < N_KEYS) s_cnt[tid] = 0;
+                                                    unsigned long long* __restrict__ blk,
+                                                    unsigned long long* __restrict__ blkq, int n_quarters) {
+  __shared__ unsigned long long s_cnt[PLAN_Q][N_KEYS], s_status;
+  const int tid = threadIdx.x, q = tid / PLACE_BLOCK;
+  for (int k = tid; k < PLAN_Q * N_KEYS; k += PLAN_BLOCK) (&s_cnt[0][0])[k] = 0;
   if (tid == 0) s_status = 0;
   __syncthreads();
   const int i = blockIdx.x * blockDim.x + tid;
@@ -114,23 +121,33 @@ __global__ void __launch_bounds__(PLAN_BLOCK) k_plan_count(const mm_pu_desc* __r
     if (p.code != MM_OK) {
       atomicMax(&s_status, status_word(pu_base + i, p.code));
     } else {
-      atomicAdd(&s_cnt[p.key], pack_count(1, p.n_sb));
+      atomicAdd(&s_cnt[q][p.key], pack_count(1, p.n_sb));
 #pragma unroll
       for (int k = 0; k < 4; k++)
-        if (p.job[k].valid) atomicAdd(&s_cnt[N_PU_KEYS + p.job[k].key], pack_count(1, p.job[k].n));
+        if (p.job[k].valid) atomicAdd(&s_cnt[q][N_PU_KEYS + p.job[k].key], pack_count(1, p.job[k].n));
     }
   }
   __syncthreads();
-  if (tid < N_KEYS) blk[(long)blockIdx.x * N_KEYS + tid] = s_cnt[tid];
+  if (tid < N_KEYS) {
+    unsigned long long tot = 0;
+#pragma unroll
+    for (int qq = 0; qq < PLAN_Q; qq++) tot += s_cnt[qq][tid];
+    blk[(long)blockIdx.x * N_KEYS + tid] = tot;
+  }
+  for (int k = tid; k < PLAN_Q * N_KEYS; k += PLAN_BLOCK) {
+    const int r = blockIdx.x * PLAN_Q + k / N_KEYS;
+    if (r < n_quarters) blkq[(long)r * N_KEYS + k % N_KEYS] = (&s_cnt[0][0])[k];
+  }
   if (tid == 0 && s_status) atomicMax(status, s_status);
 }
 
 // `next_status` is the other word of the picture ping-pong pair: the first stripe's block 0 zeroes
 // it for the next picture, so no memset launch precedes k_plan_count.
-__global__ void __launch_bounds__(PLAN_BLOCK) k_plan_place(const mm_pu_desc* __restrict__ pus, int n, const PicTables t,
-                                                    unsigned long long* __restrict__ status,
-                                                    unsigned long long* __restrict__ next_status,
-                                                    const unsigned long long* __restrict__ blk, int n_blocks,
+__global__ void __launch_bounds__(PLACE_BLOCK) k_plan_place(const mm_pu_desc* __restrict__ pus, int n, const PicTables t,
+                                                     unsigned long long* __restrict__ status,
+                                                     unsigned long long* __restrict__ next_status,
+                                                     const unsigned long long* __restrict__ blk, int n_blocks,
+                                                     const unsigned long long* __restrict__ blkq,
                                                     PlanMeta* __restrict__ meta, PlanCaps caps,
                                                     JobDev* __restrict__ jobs, int* __restrict__ job_off,
                                                     int* __restrict__ job_chunk) {
@@ -142,28 +159,31 @@ __global__ void __launch_bounds__(PLAN_BLOCK) k_plan_place(const mm_pu_desc* __r
   if (blockIdx.x == 0 && tid == 0 && next_status) *next_status = 0ull;
   if (tid < N_PU_KEYS) s_pu[tid] = 0;
   if (tid < N_JOB_KEYS) s_job[tid] = 0;
-  // bucket totals and this block's offsets inside the buckets: the column sums of blk, split over
-  // the block's 16 waves (wave w takes rows w, w + 16, ...) so that every thread has only a few
-  // independent loads in flight, then combined through LDS
-  constexpr int NWAVE = PLAN_BLOCK / 64;
+  // bucket totals and this quarter's offsets inside the buckets: the column sums of blk, split
+  // over the block's 4 waves (wave w takes count rows w, w + 4, ...), plus the quarters before this
+  // one in its count block (blkq), combined through LDS
+  constexpr int NWAVE = PLACE_BLOCK / 64;
   __shared__ unsigned long long s_ptot[NWAVE][N_KEYS], s_ppre[NWAVE][N_KEYS];
   {
-    const int lane = tid & 63, w = tid >> 6, b0 = blockIdx.x;
+    const int lane = tid & 63, w = tid >> 6, b0 = blockIdx.x / PLAN_Q, q0 = b0 * PLAN_Q;
 #pragma unroll
     for (int kc = 0; kc < N_KEYS; kc += 64) {
       const int key = kc + lane;
       if (key < N_KEYS) {
         unsigned long long tp = 0, pp = 0;
+#pragma unroll 4
         for (int b = w; b < n_blocks; b += NWAVE) {
           const unsigned long long v = blk[(long)b * N_KEYS + key];
           tp += v;
           if (b < b0) pp += v;
         }
+        if (q0 + w < (int)blockIdx.x) pp += blkq[(long)(q0 + w) * N_KEYS + key];  // PLAN_Q == NWAVE
         s_ptot[w][key] = tp;
         s_ppre[w][key] = pp;
       }
     }
   }
+  static_assert(PLAN_Q == NWAVE, "one wave per preceding quarter");
   __syncthreads();
   unsigned long long tot = 0, pre = 0;
   if (tid < N_KEYS) {
@@ -230,7 +250,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK) k_plan_place(const mm_pu_desc* __r
   }
   __syncthreads();
   if (!s_ok) return;
-  const int i = blockIdx.x * blockDim.x + tid;
+  const int i = blockIdx.x * PLACE_BLOCK + tid;
   PuPlan p;
   p.code = MM_ERR_ARG;
   mm_pu_desc u;
@@ -490,7 +510,8 @@ struct PlanSlot {
   DevBuf<int> job_off, job_chunk;
   DevBuf<JobDev> jobs;
   DevBuf<BlockSetup> setup;
-  DevBuf<unsigned long long> blk;  // per-planning-block bucket counts (k_plan_count rows)
+  DevBuf<unsigned long long> blk;   // per-count-block bucket counts (k_plan_count rows)
+  DevBuf<unsigned long long> blkq;  // per-quarter bucket counts
   DevBuf<PlanMeta> meta;
   DevBuf<mm_int2> mc_meta;
   DevBuf<mm_int4> mc_pos[2];
@@ -501,6 +522,7 @@ struct PlanSlot {
     jobs.release();
     setup.release();
     blk.release();
+    blkq.release();
     meta.release();
     mc_meta.release();
     for (int l = 0; l < 2; l++) mc_pos[l].release();
@@ -959,6 +981,7 @@ static int ensure_slot_buffers(mm_ctx* c, PlanSlot& S, int n) {
   HIPCHK(c, S.setup.ensure(k.jobs));
   HIPCHK(c, S.meta.ensure(1));
   HIPCHK(c, S.blk.ensure((size_t)((n + PLAN_BLOCK - 1) / PLAN_BLOCK) * N_KEYS));
+  HIPCHK(c, S.blkq.ensure((size_t)((n + PLACE_BLOCK - 1) / PLACE_BLOCK) * N_KEYS));
   // The records k_reproj/k_mc exchange are zeroed once when allocated: every record a plan
   // counts is written before it is read (classify_pu decides counts and emission alike), and a
   // record that never was written still holds in-picture values (position 0, slot 0), never
@@ -986,9 +1009,10 @@ static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables
   const int gs = (k.jobs + 255) / 256;
   const int gr = round_grid((k.elems + 255) / 256);
   const int gm = round_grid((k.sb + 255) / 256);
-  hipLaunchKernelGGL(k_plan_count, dim3(gp), dim3(PLAN_BLOCK), 0, st, d_in, n, base, t, status, S.blk.p);
-  hipLaunchKernelGGL(k_plan_place, dim3(gp), dim3(PLAN_BLOCK), 0, st, d_in, n, t, status, next_status, S.blk.p, gp,
-                     S.meta.p, k, S.jobs.p, S.job_off.p, S.job_chunk.p);
+  const int gq = (n + PLACE_BLOCK - 1) / PLACE_BLOCK;
+  hipLaunchKernelGGL(k_plan_count, dim3(gp), dim3(PLAN_BLOCK), 0, st, d_in, n, base, t, status, S.blk.p, S.blkq.p, gq);
+  hipLaunchKernelGGL(k_plan_place, dim3(gq), dim3(PLACE_BLOCK), 0, st, d_in, n, t, status, next_status, S.blk.p, gp,
+                     S.blkq.p, S.meta.p, k, S.jobs.p, S.job_off.p, S.job_chunk.p);
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[0], st));
   hipLaunchKernelGGL(k_setup_dev, dim3(gs), dim3(256), 0, st, c->sc, S.meta.p, S.jobs.p, t, S.setup.p);
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[1], st));
