@@ -70,7 +70,7 @@ enum mm_model_id {
 
 /* Sequence parameters (SPS fields + hard-coded MM settings, EncApp.cpp:754-768) */
 typedef struct mm_seq_params {
-  int32_t width, height;       /* luma picture size of the ERP picture */
+  int32_t width, height;       /* luma picture size of the ERP picture (multiples of 8, <= 16384) */
   int32_t chroma_format;       /* 0 = 4:0:0, 1 = 4:2:0 (ChromaFormat CHROMA_400 / CHROMA_420) */
   int32_t bit_depth;           /* internal bit depth (10 in the RA cfg) */
   int32_t max_cu_width;        /* SPS maxCUWidth (CTU size, 128) -- out-of-range rule */

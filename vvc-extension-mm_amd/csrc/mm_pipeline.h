@@ -20,25 +20,30 @@ struct RefDev {
 };
 
 // One reprojection job == one reprojectMotionVectorSubblocks call
-// 64 bytes, 16-byte aligned: written and read as four 16-byte words (k_plan_place, k_reproj*)
+// 32 bytes, 16-byte aligned: written and read as two 16-byte words (k_plan_place, k_setup*,
+// k_reproj*).  The scattered record stores are a third of k_plan_place's time, so the fields are
+// as narrow as their ranges allow: positions < 2^15 (mm_create limits pictures to 16384 samples),
+// block sizes <= 128, <= 1024 elements, models < 16, GED table index < 19.
 struct alignas(16) JobDev {
-  int x, y;    // block position in LUMA units (grid origin)
-  int cw, ch;  // block size in component units
-  int mv_hor, mv_ver;
-  int n;        // elements = (cw/sbw)*(ch/sbh)
-  int rows;     // ch/sbh (Eigen column-major rows)
-  int offset;   // first element in the result array
+  int16_t x, y;        // block position in LUMA units (grid origin)
+  uint8_t cw, ch;      // block size in component units
+  uint8_t rows;        // ch/sbh (Eigen column-major rows)
+  uint8_t pu_cols;     // device plan: sub-block columns of the PU (cw / sbw)
+  int32_t mv_hor, mv_ver;
+  int32_t offset;      // first element in the result array
   // device-planned prediction: where k_mc finds this job's results (McRec, one record per luma
-  // 4x4 sub-block of the PU, row-major from sb_base)
-  int sb_base, pu_cols;
-  int meta_hi;      // McRec meta word .y of the PU (slots, BCW) | MM_META_PRIMARY if this job writes it
-  int16_t model;
-  int16_t ged_idx;  // index into the GED rotation table (-1 if not GED)
-  int8_t comp;      // 0 luma, 1 chroma (4:2:0)
-  int8_t list, slot;
-  int8_t alias;     // MPA chroma == luma, fill both records
+  // 4x4 sub-block of the PU from sb_base)
+  int32_t sb_base;
+  uint16_t n;          // elements = (cw/sbw)*(ch/sbh)
+  int8_t model;
+  uint8_t comp : 1;    // 0 luma, 1 chroma (4:2:0)
+  uint8_t list : 1;
+  uint8_t alias : 1;   // MPA chroma == luma, fill both records
+  uint8_t slot : 4;
+  int32_t meta_hi : 24;  // McRec meta word .y of the PU (slots, BCW) | MM_META_PRIMARY if this job writes it
+  int32_t ged_idx : 8;   // index into the GED rotation table (-1 if not GED)
 };
-static_assert(sizeof(JobDev) == 64, "JobDev is four 16-byte words");
+static_assert(sizeof(JobDev) == 32, "JobDev is two 16-byte words");
 
 struct alignas(16) mm_int4 {
   int x, y, z, w;
