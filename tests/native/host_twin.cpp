@@ -31,8 +31,6 @@ static void make_twin(const mm_seq_params* p, Twin* t) {
   t->sc.focal = (float)(1. / std::tan(M_PI / p->height));
   t->sc.res = (float)(M_PI / p->height);
   t->sc.ged_flavor = p->ged_flavor;
-  t->sc.fastdiv = 0;  // IEEE divisions (the device's fast quotients are verified equal at mm_create)
-  t->sc.rW = t->sc.rH = t->sc.r2pi = t->sc.rpi = t->sc.rf = 0.0f;
   t->geo = Geometry{p->width,        p->height,           p->width >> 1,        p->height >> 1,
                     p->max_cu_width, p->max_cu_height,    p->max_cu_width >> 1, p->max_cu_height >> 1,
                     p->bit_depth,    p->chroma_format == 1, 0,                     0,

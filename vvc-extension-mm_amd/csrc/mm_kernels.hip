@@ -22,7 +22,6 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
-#include <mutex>
 #include <string>
 #include <utility>
 #include <vector>
@@ -35,9 +34,6 @@
 using namespace mmpipe;
 
 #define MM_VERSION 200
-#ifndef MM_FASTDIV
-#define MM_FASTDIV 1
-#endif
 
 namespace {
 
@@ -49,21 +45,6 @@ __global__ void k_mpa_cache(SeqConst sc, int plane, int cols, int rows, float* p
   int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= cols * rows) return;
   mpa_cache_thread(t, sc, plane, cols, rows, px, py, vip);
-}
-
-// Exhaustive check of the fast constant-divisor quotient (mm_models.h fast_quot_) against the IEEE
-// quotient for one divisor d (r = RN(1/d)) over every finite float x; mismatches counted into *bad.
-__global__ void k_div_verify(float d, float r, unsigned* __restrict__ bad) {
-  const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
-  unsigned n_bad = 0;
-  for (unsigned long long u = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; u < (1ull << 32);
-       u += stride) {
-    const uint32_t bits = (uint32_t)u;
-    if (((bits >> 23) & 0xffu) == 0xffu) continue;  // inf / NaN: never reach these divisions
-    const float x = asf(bits);
-    n_bad += asu(fast_quot_(x, d, r)) != asu(x / d) ? 1u : 0u;
-  }
-  if (n_bad) atomicAdd(bad, n_bad);
 }
 
 __global__ void k_setup(SeqConst sc, const JobDev* __restrict__ jobs, int n_jobs, const M3* __restrict__ ged,
@@ -616,37 +597,6 @@ struct mm_ctx {
 
 static int read_status(mm_ctx* c, int* first_bad);
 
-// fastdiv bits of the five sequence-constant divisors (SeqConst::fastdiv): each divisor is checked
-// once per process (k_div_verify, ~2 ms on MI355X) and remembered by its bit pattern.
-static int fastdiv_bits(SeqConst& sc, hipStream_t st) {
-  const float d[5] = {sc.Wf, sc.Hf, TWO_PI_F, PI_F, sc.focal};
-  float* r[5] = {&sc.rW, &sc.rH, &sc.r2pi, &sc.rpi, &sc.rf};
-  for (int k = 0; k < 5; k++) *r[k] = 1.0f / d[k];
-  if (!MM_FASTDIV) return 0;
-  static std::mutex mu;
-  static std::map<uint64_t, bool> known;
-  std::lock_guard<std::mutex> lock(mu);
-  int bits = 0;
-  unsigned* dbad = nullptr;
-  for (int k = 0; k < 5; k++) {
-    const uint64_t key = ((uint64_t)__builtin_bit_cast(uint32_t, d[k]) << 32) | __builtin_bit_cast(uint32_t, *r[k]);
-    auto it = known.find(key);
-    if (it == known.end()) {
-      if (!dbad && hipMalloc(&dbad, sizeof(unsigned)) != hipSuccess) return bits;
-      unsigned nb = 1;
-      if (hipMemsetAsync(dbad, 0, sizeof(unsigned), st) == hipSuccess) {
-        hipLaunchKernelGGL(k_div_verify, dim3(2048), dim3(256), 0, st, d[k], *r[k], dbad);
-        if (hipGetLastError() != hipSuccess || hipMemcpyAsync(&nb, dbad, sizeof(nb), hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipStreamSynchronize(st) != hipSuccess)
-          nb = 1;
-      }
-      it = known.emplace(key, nb == 0).first;
-    }
-    if (it->second) bits |= 1 << k;
-  }
-  if (dbad) (void)hipFree(dbad);
-  return bits;
-}
 
 static int fail(mm_ctx* c, int code, const std::string& msg) {
   if (c) c->err = msg;
@@ -751,7 +701,6 @@ int mm_create(const mm_seq_params* p, int device, mm_ctx** out_ctx) {
   c->sc.focal = (float)(1. / std::tan(M_PI / p->height));  // Projection.h:127-130
   c->sc.res = (float)(M_PI / p->height);                    // MVReprojection.cpp:27,33,39
   c->sc.ged_flavor = p->ged_flavor;
-  c->sc.fastdiv = fastdiv_bits(c->sc, c->stream);
   c->geo.W = p->width;
   c->geo.H = p->height;
   c->geo.chroma = p->chroma_format == 1;

@@ -48,26 +48,7 @@ struct SeqConst {
   float focal;     // float(1. / tan(M_PI / H)) -- ERP focal, reused by MPA's perspective
   float res;       // float(M_PI / H) -- angle resolution of TAN/ROT/GED
   int ged_flavor;  // 0 VISHWANATH_ORIGINAL, 1 VISHWANATH_MODULATED (EncApp.cpp:755 hard-codes 1)
-  // Division by the five sequence-constant divisors (W, H, 2pi, pi, focal) as a reciprocal multiply
-  // with one FMA correction (div_const).  fastdiv bit k is set only after the divisor passed an
-  // exhaustive check against the IEEE division over every finite float (mm_create, k_div_verify);
-  // 0 (host twin, failed check) = IEEE division.
-  float rW, rH, r2pi, rpi, rf;  // RN(1 / divisor)
-  int fastdiv;
 };
-enum { DIV_W = 1, DIV_H = 2, DIV_2PI = 4, DIV_PI = 8, DIV_F = 16 };
-
-// x / d for a sequence-constant divisor d with r = RN(1 / d): q0 = RN(x r), e = x - q0 d (exact,
-// one FMA), q = RN(q0 + e r), with the sign of q0 (x = -0).  Equal to the IEEE quotient wherever
-// k_div_verify found it so (all finite floats) -- 4 VALU instead of the ~9 VALU + 2 SALU of the
-// correctly rounded division sequence.
-MM_HD float fast_quot_(float x, float d, float r) {
-  const float q0 = x * r;
-  const float e = __builtin_fmaf(-q0, d, x);
-  const float q = __builtin_fmaf(e, r, q0);
-  return asf((asu(q) & 0x7fffffffu) | (asu(q0) & 0x80000000u));
-}
-MM_HD float div_const(float x, float d, float r, int fast) { return fast ? fast_quot_(x, d, r) : x / d; }
 
 // ------------------------------------------------------------------------------------------
 // Coordinate conversions (Coordinate.cpp).  `arr` selects the Eigen array form (clamp as
@@ -102,16 +83,16 @@ MM_HD V3 sph_to_cart(float R, float th, float ph, Math m) {
 // EquirectangularProjection (Projection.cpp:213-249 in SURVEY numbering; pixelOffset = 0)
 // ------------------------------------------------------------------------------------------
 MM_HD V3 erp_to_sphere(float x, float y, const SeqConst& s, Math m) {
-  float phi = ((-div_const(x + 0.0f, s.Wf, s.rW, s.fastdiv & DIV_W)) * 2.0f) * PI_F;
-  float theta = (div_const(y + 0.0f, s.Hf, s.rH, s.fastdiv & DIV_H)) * PI_F;
+  float phi = ((-((x + 0.0f) / s.Wf)) * 2.0f) * PI_F;
+  float theta = ((y + 0.0f) / s.Hf) * PI_F;
   return sph_to_cart(1.0f, theta, phi, m);
 }
 
 MM_HD void erp_from_sphere(V3 p, const SeqConst& s, Math m, bool arr, float* ox, float* oy) {
   V3 sp = cart_to_sph(p, m, arr);
   float phi = sp.z > 0.0f ? sp.z - TWO_PI_F : sp.z;
-  *ox = ((-div_const(phi, TWO_PI_F, s.r2pi, s.fastdiv & DIV_2PI)) * s.Wf) - 0.0f;
-  *oy = (div_const(sp.y, PI_F, s.rpi, s.fastdiv & DIV_PI) * s.Hf) - 0.0f;
+  *ox = ((-(phi / TWO_PI_F)) * s.Wf) - 0.0f;
+  *oy = ((sp.y / PI_F) * s.Hf) - 0.0f;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -131,7 +112,7 @@ MM_HD V3 persp_to_sphere(float x, float y, bool vip, const SeqConst& s, Math m) 
   y = y - 0.0f;
   float r = m.sqrt(x * x + y * y);
   float phi = g_atan2f(y, x);
-  float theta = g_atanf(div_const(r, s.focal, s.rf, s.fastdiv & DIV_F));
+  float theta = g_atanf(r / s.focal);
   float v = vip ? 1.0f : 0.0f;
   theta = theta - v * (2.0f * theta - PI_F);
   phi = phi - v * PI_F;
