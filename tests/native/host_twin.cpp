@@ -34,7 +34,7 @@ static void make_twin(const mm_seq_params* p, Twin* t) {
   t->geo = Geometry{p->width,        p->height,           p->width >> 1,        p->height >> 1,
                     p->max_cu_width, p->max_cu_height,    p->max_cu_width >> 1, p->max_cu_height >> 1,
                     p->bit_depth,    p->chroma_format == 1, 0,                     0,
-                    3};
+                    3,               0};
   const int cols = p->width / 4, rows = p->height / 4, n = cols * rows;
   for (int pl = 0; pl < 3; pl++) {
     if (!(p->active_models & (1u << (MPA_FRONT_BACK + pl)))) continue;

@@ -714,6 +714,7 @@ int mm_create(const mm_seq_params* p, int device, mm_ctx** out_ctx) {
   c->geo.vec_store = 0;
   c->geo.hp = 0;
   c->geo.store = 3;
+  c->geo.padded = 1;
   if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
       hipEventCreate(&c->ev_stage[0]) != hipSuccess || hipEventCreate(&c->ev_stage[1]) != hipSuccess ||
       hipEventCreate(&c->ev_stage[2]) != hipSuccess ||
@@ -853,23 +854,74 @@ int mm_epipole_derive_predictor(mm_epipole_list* e, int cur, int32_t q24[3]) {
 
 int mm_epipole_count(mm_epipole_list* e) { return e ? e->l->count() : -1; }
 
+// Reference picture layout in the pool: each plane carries edge-replicated margins (the role of
+// VTM's extendPicBorder, Picture.cpp:988-1048) wide enough for every window k_mc reads from an
+// in-range sub-block (sb_out_of_range admits positions up to maxCU outside the picture; the
+// 8-tap luma window reaches 4 samples beyond, the 4-tap chroma one 2), so k_mc never clamps.
+// Margins are 64 samples aligned so plane origins stay 128-byte aligned; +8 samples spare.
+struct PlaneLayout {
+  int mx, my, stride;  // margin columns / rows, row stride (samples)
+  size_t bytes;        // whole padded plane
+};
+static PlaneLayout plane_layout(int w, int h, int max_cu_w, int max_cu_h, int reach_x, int reach_y) {
+  PlaneLayout l;
+  l.mx = (max_cu_w + reach_x + 8 + 63) & ~63;
+  l.my = max_cu_h + reach_y + 8;
+  l.stride = (w + 2 * l.mx + 63) & ~63;
+  l.bytes = (size_t)2 * l.stride * (h + 2 * l.my);
+  return l;
+}
+static PlaneLayout luma_layout(const mm_ctx* c) {
+  return plane_layout(c->geo.W, c->geo.H, c->geo.maxCUw, c->geo.maxCUh, 4, 3);
+}
+static PlaneLayout chroma_layout(const mm_ctx* c) {
+  return plane_layout(c->geo.Wc, c->geo.Hc, c->geo.maxCUwc, c->geo.maxCUhc, 2, 1);
+}
+
 static void place_ref(mm_ctx* c, RefHost& r) {
-  const int H = c->geo.H;
-  r.stride_y = (c->geo.W + 63) & ~63;
-  r.stride_c = (c->geo.Wc + 63) & ~63;
+  const PlaneLayout ly = luma_layout(c), lc = chroma_layout(c);
+  r.stride_y = ly.stride;
+  r.stride_c = lc.stride;
   char* base = c->pool + (size_t)r.slot * c->pic_bytes;
-  r.y = reinterpret_cast<int16_t*>(base);
-  r.cb = c->geo.chroma ? reinterpret_cast<int16_t*>(base + (size_t)r.stride_y * H * 2) : nullptr;
-  r.cr = c->geo.chroma ? r.cb + (size_t)r.stride_c * c->geo.Hc : nullptr;
+  r.y = reinterpret_cast<int16_t*>(base + 2 * ((size_t)ly.my * ly.stride + ly.mx));
+  r.cb = c->geo.chroma ? reinterpret_cast<int16_t*>(base + ly.bytes + 2 * ((size_t)lc.my * lc.stride + lc.mx)) : nullptr;
+  r.cr = c->geo.chroma ? reinterpret_cast<int16_t*>(reinterpret_cast<char*>(r.cb) + lc.bytes) : nullptr;
+}
+
+// Fills a plane's margins from its nearest edge sample (corners from the corner sample): thread per
+// margin sample over the top/bottom bands (full padded width) and the left/right bands
+__global__ void __launch_bounds__(256) k_pad_plane(int16_t* __restrict__ o, int stride, int w, int h, int mx, int my) {
+  const int fw = w + 2 * mx;
+  long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long tb = (long)2 * my * fw;
+  int x, y;
+  if (t < tb) {
+    const int r = (int)(t / fw);
+    x = (int)(t - (long)r * fw) - mx;
+    y = r < my ? r - my : h + r - my;
+  } else {
+    t -= tb;
+    if (t >= (long)h * 2 * mx) return;
+    y = (int)(t / (2 * mx));
+    const int k = (int)(t - (long)y * 2 * mx);
+    x = k < mx ? k - mx : w + k - mx;
+  }
+  const int sx = x < 0 ? 0 : (x >= w ? w - 1 : x), sy = y < 0 ? 0 : (y >= h ? h - 1 : y);
+  o[(long)y * stride + x] = o[(long)sy * stride + sx];
+}
+
+static int pad_plane(mm_ctx* c, int16_t* origin, const PlaneLayout& l, int w, int h) {
+  const long n = (long)2 * l.my * (w + 2 * l.mx) + (long)h * 2 * l.mx;
+  hipLaunchKernelGGL(k_pad_plane, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, origin, l.stride, w, h,
+                     l.mx, l.my);
+  HIPCHK(c, hipGetLastError());
+  return MM_OK;
 }
 
 // A free picture slot of the reference pool; grows the pool (copying the resident pictures) when
 // full.  Growth waits for the context's work so no launch still reads the old allocation.
 static int take_pool_slot(mm_ctx* c, int* slot) {
-  if (!c->pic_bytes) {
-    const size_t sy = (size_t)((c->geo.W + 63) & ~63), sc = (size_t)((c->geo.Wc + 63) & ~63);
-    c->pic_bytes = 2 * (sy * c->geo.H + (c->geo.chroma ? 2 * sc * c->geo.Hc : 0));
-  }
+  if (!c->pic_bytes) c->pic_bytes = luma_layout(c).bytes + (c->geo.chroma ? 2 * chroma_layout(c).bytes : 0);
   if (c->pool_free.empty()) {
     const size_t limit = ((size_t)1 << 31) - 1;
     const int max_cap = (int)std::min<size_t>(limit / c->pic_bytes, 64);
@@ -895,7 +947,7 @@ static int take_pool_slot(mm_ctx* c, int* slot) {
 }
 
 static RefPool pool_of(const mm_ctx* c) {
-  const int cr_delta = c->geo.chroma ? 2 * ((c->geo.Wc + 63) & ~63) * c->geo.Hc : 0;
+  const int cr_delta = c->geo.chroma ? (int)chroma_layout(c).bytes : 0;
   return RefPool{c->pool, (uint32_t)((size_t)c->pool_cap * c->pic_bytes), cr_delta};
 }
 
@@ -930,6 +982,11 @@ int mm_upload_ref(mm_ctx* c, int poc, const int16_t* y, ptrdiff_t sy, const int1
   if (c->geo.chroma) {
     HIPCHK(c, hipMemcpy2DAsync(r.cb, r.stride_c * 2, cb, sc_ * 2, Wc * 2, Hc, k, c->stream));
     HIPCHK(c, hipMemcpy2DAsync(r.cr, r.stride_c * 2, cr, sc_ * 2, Wc * 2, Hc, k, c->stream));
+  }
+  RCCHK(pad_plane(c, r.y, luma_layout(c), W, H));
+  if (c->geo.chroma) {
+    RCCHK(pad_plane(c, r.cb, chroma_layout(c), Wc, Hc));
+    RCCHK(pad_plane(c, r.cr, chroma_layout(c), Wc, Hc));
   }
   if (!src_dev) HIPCHK(c, hipStreamSynchronize(c->stream));  // host source buffers may be reused at once
   return MM_OK;

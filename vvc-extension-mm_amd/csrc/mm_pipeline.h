@@ -85,6 +85,8 @@ struct Geometry {
   int vec_store;  // destination planes allow 8-byte luma / 4-byte chroma row stores
   int hp;         // mm_pred_list hp: every list keeps the 14-bit intermediate (bi = true)
   int store;      // components written: bit 0 luma, bit 1 chroma
+  int padded;     // device: the reference planes carry edge-replicated margins wide enough for every
+                  // in-range window (mm_kernels.hip place_ref), so no window needs clamped reads
 };
 
 struct Taps {
@@ -302,11 +304,12 @@ MM_HD void mc_rec_impl(int g, int cls, const Geometry& geo, const Taps& taps, co
       const RefDev r = refs[slot[l]];
       if (sb_out_of_range(xPos, yPos, geo.W, geo.H, geo.maxCUw, geo.maxCUh, 4, 4)) {
         for (int i = 0; i < 16; i++) pl[l][i] = 0;
-      } else if (window_interior<8, 4, 4>(xPos, yPos, geo.W, geo.H)) {
 #if defined(__HIP_DEVICE_COMPILE__)
+      } else if (geo.padded || window_interior<8, 4, 4>(xPos, yPos, geo.W, geo.H)) {
         predict_subblock_pool<8, 4, 4>(taps.pool, r.off_y, 0, r.stride_y, xPos, yPos, taps.packed->lh[xFrac][(xPos - 3) & 1],
                                        taps.packed->lv[yFrac], hp, geo.bd, pl[l]);
 #else
+      } else if (window_interior<8, 4, 4>(xPos, yPos, geo.W, geo.H)) {
         predict_subblock_interior<8, 4, 4>(r.y, r.stride_y, xPos, yPos, taps.luma[xFrac], taps.luma[yFrac], hp,
                                            geo.bd, pl[l]);
 #endif
@@ -336,14 +339,15 @@ MM_HD void mc_rec_impl(int g, int cls, const Geometry& geo, const Taps& taps, co
     const RefDev r = refs[slot[l]];
     if (sb_out_of_range(xPos, yPos, geo.Wc, geo.Hc, geo.maxCUwc, geo.maxCUhc, 2, 2)) {
       for (int i = 0; i < 4; i++) pcb[l][i] = pcr[l][i] = 0;
-    } else if (window_interior<4, 2, 2>(xPos, yPos, geo.Wc, geo.Hc)) {
 #if defined(__HIP_DEVICE_COMPILE__)
+    } else if (geo.padded || window_interior<4, 2, 2>(xPos, yPos, geo.Wc, geo.Hc)) {
       const uint32_t* ht = taps.packed->ch[xFrac][(xPos - 1) & 1];
       const uint32_t* vt = taps.packed->cv[yFrac];
       predict_subblock_pool<4, 2, 2>(taps.pool, r.off_cb, 0, r.stride_c, xPos, yPos, ht, vt, hp, geo.bd, pcb[l]);
       predict_subblock_pool<4, 2, 2>(taps.pool, r.off_cb, taps.pool.cr_delta, r.stride_c, xPos, yPos, ht, vt, hp, geo.bd,
                                      pcr[l]);
 #else
+    } else if (window_interior<4, 2, 2>(xPos, yPos, geo.Wc, geo.Hc)) {
       predict_subblock_interior<4, 2, 2>(r.cb, r.stride_c, xPos, yPos, taps.chroma[xFrac], taps.chroma[yFrac], hp,
                                          geo.bd, pcb[l]);
       predict_subblock_interior<4, 2, 2>(r.cr, r.stride_c, xPos, yPos, taps.chroma[xFrac], taps.chroma[yFrac], hp,
