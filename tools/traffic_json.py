@@ -12,7 +12,8 @@ import json
 import sys
 
 ROOT = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
-OUT = sys.argv[2] if len(sys.argv) > 2 else "profiles/r01_traffic.json"
+OUT = sys.argv[2] if len(sys.argv) > 2 else "profiles/r02_traffic.json"
+PICTURES = 4  # bench.py --pictures default, used by the pmc passes of tools/gpu_run.sh
 KERNEL = "k_mc_dev"
 
 
@@ -29,7 +30,7 @@ def per_dispatch(pattern, counter):
 fetch_kb, nf = per_dispatch(f"{ROOT}/pmc_fetch/*counter_collection.csv", "FETCH_SIZE")
 write_kb, nw = per_dispatch(f"{ROOT}/pmc_write/*counter_collection.csv", "WRITE_SIZE")
 sha = hashlib.sha256(open("vvc-extension-mm_amd/lib/libmm360.so", "rb").read()).hexdigest()
-d = {"kernel": KERNEL, "lib_sha256": sha, "dispatches": [nf, nw],
+d = {"kernel": KERNEL, "lib_sha256": sha, "pictures": PICTURES, "dispatches": [nf, nw],
      "fetch_size_kb": round(fetch_kb, 1), "write_size_kb": round(write_kb, 1),
      "traffic_bytes_per_launch": int(2 * fetch_kb * 1024 + write_kb * 1024),
      "note": "2 x FETCH_SIZE + WRITE_SIZE per k_mc_dev launch (rocprofv3 --pmc, separate passes)"}
