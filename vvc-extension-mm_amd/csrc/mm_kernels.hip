@@ -888,30 +888,39 @@ static void place_ref(mm_ctx* c, RefHost& r) {
   r.cr = c->geo.chroma ? reinterpret_cast<int16_t*>(reinterpret_cast<char*>(r.cb) + lc.bytes) : nullptr;
 }
 
-// Fills a plane's margins from its nearest edge sample (corners from the corner sample): thread per
-// margin sample over the top/bottom bands (full padded width) and the left/right bands
+// Fills a plane's margins from its nearest edge sample (corners from the corner sample), one
+// 4-sample (8-byte) chunk per thread: the top/bottom bands over the full padded width, then the
+// left/right bands.  Chunks never straddle the picture edge (w, mx multiples of 4).
 __global__ void __launch_bounds__(256) k_pad_plane(int16_t* __restrict__ o, int stride, int w, int h, int mx, int my) {
-  const int fw = w + 2 * mx;
+  typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+  const int fq = (w + 2 * mx) >> 2, sq = (2 * mx) >> 2;  // chunks per band row
   long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long tb = (long)2 * my * fw;
+  const long tb = (long)2 * my * fq;
   int x, y;
   if (t < tb) {
-    const int r = (int)(t / fw);
-    x = (int)(t - (long)r * fw) - mx;
+    const int r = (int)(t / fq);
+    x = 4 * (int)(t - (long)r * fq) - mx;
     y = r < my ? r - my : h + r - my;
   } else {
     t -= tb;
-    if (t >= (long)h * 2 * mx) return;
-    y = (int)(t / (2 * mx));
-    const int k = (int)(t - (long)y * 2 * mx);
+    if (t >= (long)h * sq) return;
+    y = (int)(t / sq);
+    const int k = 4 * (int)(t - (long)y * sq);
     x = k < mx ? k - mx : w + k - mx;
   }
-  const int sx = x < 0 ? 0 : (x >= w ? w - 1 : x), sy = y < 0 ? 0 : (y >= h ? h - 1 : y);
-  o[(long)y * stride + x] = o[(long)sy * stride + sx];
+  const int16_t* src = o + (long)(y < 0 ? 0 : (y >= h ? h - 1 : y)) * stride;
+  u2 v;
+  if (x >= 0 && x < w) {
+    v = *reinterpret_cast<const u2*>(src + x);
+  } else {
+    const uint32_t e = (uint16_t)src[x < 0 ? 0 : w - 1];
+    v.x = v.y = e | (e << 16);
+  }
+  *reinterpret_cast<u2*>(o + (long)y * stride + x) = v;
 }
 
 static int pad_plane(mm_ctx* c, int16_t* origin, const PlaneLayout& l, int w, int h) {
-  const long n = (long)2 * l.my * (w + 2 * l.mx) + (long)h * 2 * l.mx;
+  const long n = (long)2 * l.my * ((w + 2 * l.mx) >> 2) + (long)h * ((2 * l.mx) >> 2);
   hipLaunchKernelGGL(k_pad_plane, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, origin, l.stride, w, h,
                      l.mx, l.my);
   HIPCHK(c, hipGetLastError());
