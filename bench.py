@@ -9,7 +9,7 @@ descriptor lists) are resident in HBM before the timed region; nothing is planne
 
 Configurations (BASELINE.json configs):
   C3 (default at 1 GPU)  `--pictures` distinct pictures (PU lists of frames 0..P-1), each with its
-        own pair of reference pictures (2P resident references, 453 MB at P = 4 -- more than the
+        own pair of reference pictures (2P resident references, 529 MB of padded pool at P = 4 -- more than the
         256 MB Infinity Cache), predicted in rotation: step s predicts picture s % P.  After
         timing, every picture's output is compared with the CPU oracle (`bit_exact`).
   C4 (default at N > 1 GPUs)  one C3 picture per step, CTU-row sharded: rank r predicts the PUs
