@@ -243,16 +243,21 @@ MM_HD float fixed_to_float(int32_t v, int prec) {
 // Per-block (per PU x list x component) setup: everything the reference computes once per
 // reprojectMotionVectorSubblocks call, before the per-element arrays.
 // ------------------------------------------------------------------------------------------
+// 56 bytes: the per-model constants share M's storage (k_setup streams one record per job to
+// HBM and k_reproj reads it back per element, so the record is kept to what any one model needs).
 struct BlockSetup {
-  int model;
-  int identity;   // model returns the input grid unchanged (zero-MV shortcut)
-  float mvx, mvy;  // motion vector as float (MVReprojection.cpp:123-124)
-  float cx, cy;    // block centre in component units (MVReprojection.cpp:133)
-  M3 M;            // GED rotation (setEpipole) or ROT rotationMatrixReally
-  float k;         // GED MODULATED parameter
-  float sE, cE, alphaC;  // TAN centre terms
-  float d0, d1, d2;      // 3DT motion vector in 3D
+  int16_t model;
+  int16_t identity;  // model returns the input grid unchanged (zero-MV shortcut)
+  float mvx, mvy;    // motion vector as float (MVReprojection.cpp:123-124)
+  M3 M;              // GED rotation (setEpipole) or ROT rotationMatrixReally; TAN: sE, cE, alphaC
+                     // in m[0..2]; 3DT: the 3D motion vector in m[0..2]
+  float k;           // GED MODULATED parameter
+  float pad_;
 };
+static_assert(sizeof(BlockSetup) == 56, "BlockSetup is seven 8-byte words");
+MM_HD float tan_sE(const BlockSetup& b) { return b.M.m[0]; }
+MM_HD float tan_cE(const BlockSetup& b) { return b.M.m[1]; }
+MM_HD float tan_alphaC(const BlockSetup& b) { return b.M.m[2]; }
 
 MM_HD float mv_to_float(int32_t v) { return (float)(v >> 4) + (float)(v & 15) / 16.0f; }
 // MV as floating point with `shift` fractional bits (MVReprojection.cpp:123-124, 185-186)
@@ -268,15 +273,15 @@ MM_HD void block_setup(BlockSetup* b, const SeqConst& s, int model, bool luma, i
 }
 MM_HD void block_setup_f(BlockSetup* b, const SeqConst& s, int model, bool luma, int pos_x, int pos_y, int size_w,
                          int size_h, float mvx, float mvy, const M3* ged_rot) {
-  b->model = model;
+  b->model = (int16_t)model;
   b->mvx = mvx;
   b->mvy = mvy;
-  b->cx = (float)pos_x + ((float)size_w - 1.0f) / 2.0f;
-  b->cy = (float)pos_y + ((float)size_h - 1.0f) / 2.0f;
+  // block centre in component units (MVReprojection.cpp:133)
+  const float cx = (float)pos_x + ((float)size_w - 1.0f) / 2.0f;
+  const float cy = (float)pos_y + ((float)size_h - 1.0f) / 2.0f;
   b->identity = 0;
   b->k = 0.0f;
-  b->sE = b->cE = b->alphaC = 0.0f;
-  b->d0 = b->d1 = b->d2 = 0.0f;
+  b->pad_ = 0.0f;
   for (int i = 0; i < 9; i++) b->M.m[i] = 0.0f;
   const bool zero = (b->mvx == 0.0f && b->mvy == 0.0f);
   const Math sc{false};
@@ -287,29 +292,29 @@ MM_HD void block_setup_f(BlockSetup* b, const SeqConst& s, int model, bool luma,
       break;  // no shortcut, no per-block constants
     case TANGENTIAL: {  // TangentialMotionModel.cpp:8-48
       if (zero) { b->identity = 1; break; }
-      V3 c3 = erp_to_sphere(b->cx, b->cy, s, sc);
+      V3 c3 = erp_to_sphere(cx, cy, s, sc);
       V3 sp = cart_to_sph(c3, sc, false);
       float epsC = (float)(PI_2_D - (double)sp.y);
-      b->alphaC = sp.z;
+      b->M.m[2] = sp.z;  // alphaC
 #if MM_TAN_CENTRE_MODE
-      b->sE = g_sinf(epsC);
-      b->cE = g_cosf(epsC);
+      b->M.m[0] = g_sinf(epsC);  // sE
+      b->M.m[1] = g_cosf(epsC);  // cE
 #else
-      b->sE = sinf_via_double(epsC);   // unqualified sin(float) -> double ::sin
-      b->cE = cosf_via_double(epsC);
+      b->M.m[0] = sinf_via_double(epsC);  // sE: unqualified sin(float) -> double ::sin
+      b->M.m[1] = cosf_via_double(epsC);  // cE
 #endif
     } break;
     case THREE_D_TRANSLATIONAL: {  // ThreeDTranslationalMotionModel.cpp:7-24
       if (zero) { b->identity = 1; break; }
-      V3 c = erp_to_sphere(b->cx, b->cy, s, sc);
-      V3 cm = erp_to_sphere(b->cx + b->mvx, b->cy + b->mvy, s, sc);
-      b->d0 = cm.x - c.x;
-      b->d1 = cm.y - c.y;
-      b->d2 = cm.z - c.z;
+      V3 c = erp_to_sphere(cx, cy, s, sc);
+      V3 cm = erp_to_sphere(cx + b->mvx, cy + b->mvy, s, sc);
+      b->M.m[0] = cm.x - c.x;
+      b->M.m[1] = cm.y - c.y;
+      b->M.m[2] = cm.z - c.z;
     } break;
     case ROTATIONAL: {  // RotationalMotionModel.cpp:8-78
       if (zero) { b->identity = 1; break; }
-      V3 sp = cart_to_sph(erp_to_sphere(b->cx, b->cy, s, sc), sc, false);
+      V3 sp = cart_to_sph(erp_to_sphere(cx, cy, s, sc), sc, false);
       M3 rot = mat_mul(angle_axis(-b->mvx * s.res, 0.0f, 0.0f, 1.0f),
                        angle_axis(b->mvy * s.res, 0.0f, 1.0f, 0.0f));
       M3 unrotPhi = angle_axis(-sp.z, 0.0f, 0.0f, 1.0f);
@@ -325,7 +330,7 @@ MM_HD void block_setup_f(BlockSetup* b, const SeqConst& s, int model, bool luma,
       b->M = *ged_rot;
       if (!luma && zero) { b->identity = 1; break; }  // only modelMotion shortcuts (:130-132)
       if (s.ged_flavor == 1) {
-        V3 c3 = erp_to_sphere(b->cx, b->cy, s, sc);
+        V3 c3 = erp_to_sphere(cx, cy, s, sc);
         V3 cr = mat_vec(b->M, c3);
         V3 sp = cart_to_sph(cr, sc, false);
         float rm = s.res * b->mvx;
@@ -398,22 +403,23 @@ MM_HD void model_motion_element(const SeqConst& s, const BlockSetup& b, float gx
       const float alpha = sp.z;
       const float se = m.sin(eps);
       const float ce = m.cos(eps);
-      float dA = alpha - b.alphaC;
+      const float sE = tan_sE(b), cE = tan_cE(b), alphaC = tan_alphaC(b);
+      float dA = alpha - alphaC;
       float cdA = m.cos(dA);
-      float cosPsi = b.sE * se + (b.cE * ce) * cdA;
-      float yP = (se * b.cE - (b.sE * ce) * cdA) / cosPsi;
+      float cosPsi = sE * se + (cE * ce) * cdA;
+      float yP = (se * cE - (sE * ce) * cdA) / cosPsi;
       float xP = (m.sin(dA) * ce) / cosPsi;
       float yM = yP - b.mvy * s.res;
       float xM = xP - b.mvx * s.res;
       float rho = m.sqrt(xM * xM + yM * yM);
       float eta = g_atanf(rho);
-      float gamma = (rho * b.cE) * m.cos(eta) - (yM * b.sE) * m.sin(eta);
-      float alphaM = b.alphaC + g_atanf((xM * g_sinf(eta)) / gamma);
-      float epsM = g_asinf(g_cosf(eta) * b.sE + ((yM * g_sinf(eta)) * b.cE) / rho);
+      float gamma = (rho * cE) * m.cos(eta) - (yM * sE) * m.sin(eta);
+      float alphaM = alphaC + g_atanf((xM * g_sinf(eta)) / gamma);
+      float epsM = g_asinf(g_cosf(eta) * sE + ((yM * g_sinf(eta)) * cE) / rho);
       q = sph_to_cart(1.0f, PI_2_F - epsM, alphaM, m);
     } break;
     case THREE_D_TRANSLATIONAL:  // ThreeDTranslationalMotionModel.cpp:7-24
-      q = {p.x + b.d0, p.y + b.d1, p.z + b.d2};
+      q = {p.x + b.M.m[0], p.y + b.M.m[1], p.z + b.M.m[2]};  // 3D motion vector
       break;
     case ROTATIONAL:  // RotationalMotionModel.cpp:66-77
       q = mat_vec(b.M, p);
