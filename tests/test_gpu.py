@@ -171,6 +171,26 @@ def test_pred_extreme_motion_zeroing():
     # large motions wrap around the sphere instead.
 
 
+@pytest.mark.parametrize("max_cu", [8, 32, 64])
+def test_pred_small_max_cu_padded_margins(max_cu):
+    """The reference pool's edge-replicated margins are sized from maxCU (mm_kernels.hip
+    plane_layout: maxCU + filter reach + 8, rounded to 64 columns; maxCU + reach + 8 rows), and the
+    out-of-range rule zeroes with +-maxCU (InterPrediction.cpp:780).  Small maxCU gives the
+    narrowest margins; random large motions put windows on every picture edge."""
+    cfg = W.CONFIGS["C1"]
+    params = mm360.seq_params(cfg.width, cfg.height, W.ALL_MODELS, max_cu=max_cu)
+    pus = W.pu_list(cfg, frame=5)
+    rng = np.random.default_rng(max_cu)
+    pus["model"] = rng.choice(np.array(W.ALL_MODELS), size=pus["model"].shape)
+    pus["mv"] = rng.integers(-(1 << 12), 1 << 12, size=pus["mv"].shape)
+    refs = {poc: W.ref_planes(cfg.width, cfg.height, poc) for poc in W.REF_POCS}
+    want = Oracle(params, EPI).predict(W.CUR_POC, pus, refs, cfg.width, cfg.height)
+    with _ctx(params) as ctx:
+        got = _gpu_predict(ctx, params, W.CUR_POC, pus, refs)
+    for name, g, w in zip("Y Cb Cr".split(), got, want):
+        assert np.array_equal(g, w), f"{name}: {(g != w).sum()} samples differ"
+
+
 def test_pred_deterministic_and_split_api():
     cfg = W.CONFIGS["C2"]
     params = mm360.seq_params(cfg.width, cfg.height, cfg.models)
