@@ -34,6 +34,9 @@ PRIM(g_atan2f, -1.0f, 1.0f, g_atan2f(x, 0.7f - x))
 PRIM(g_acosf, -0.99f, 0.99f, g_acosf(x))
 PRIM(g_asinf, -0.99f, 0.99f, g_asinf(x))
 PRIM(g_tanf, -1.5f, 1.5f, g_tanf(x))
+PRIM(psincos, -3.0f, 3.0f, e_psin(x) + e_pcos(x))
+PRIM(g_sincos, -3.0f, 3.0f, g_sinf(x) + g_cosf(x))
+PRIM(div_y_x, -1.0f, 1.0f, x / (0.7f - x))
 
 int main() {
   float* out;
@@ -50,7 +53,8 @@ int main() {
   } ks[] = {{"empty", k_empty},   {"div", k_div},       {"sqrtf", k_sqrtf},       {"psqrt", k_psqrt},
             {"g_sinf", k_g_sinf}, {"g_cosf", k_g_cosf}, {"psin", k_psin},         {"pcos", k_pcos},
             {"sin_dbl", k_sin_dbl}, {"g_atanf", k_g_atanf}, {"g_atan2f", k_g_atan2f}, {"g_acosf", k_g_acosf},
-            {"g_asinf", k_g_asinf}, {"g_tanf", k_g_tanf}};
+            {"g_asinf", k_g_asinf}, {"g_tanf", k_g_tanf}, {"psincos", k_psincos}, {"g_sincos", k_g_sincos},
+            {"div_y_x", k_div_y_x}};
   float base = 0.0f;
   for (const K& k : ks) {
     float best = 1e30f;
