@@ -200,8 +200,9 @@ int mm_epipole_derive_predictor(mm_epipole_list* list, int cur_poc, int32_t q24[
 int mm_epipole_count(mm_epipole_list* list);                                 /* EpipoleList::count */
 
 /* Reference picture planes (reconstruction, unpadded, picture origin at plane[0]).  `src_is_device`
- * = 1 when the pointers are device memory.  The context keeps its own device copy; padding is
- * implicit (edge replication == coordinate clamping, Picture.cpp:988-1048). */
+ * = 1 when the pointers are device memory.  The context keeps its own device copy with edge-
+ * replicated margins of maxCU + the filter reach (extendPicBorder, Picture.cpp:988-1048), filled on
+ * the device at upload; the caller's planes need no padding. */
 int mm_upload_ref(mm_ctx* ctx, int poc, const int16_t* y, ptrdiff_t stride_y, const int16_t* cb,
                   const int16_t* cr, ptrdiff_t stride_c, int src_is_device);
 int mm_release_ref(mm_ctx* ctx, int poc);
