@@ -29,9 +29,13 @@ constexpr int MAX_SLOTS = 16;  // reference pictures addressable by one picture 
 constexpr int N_PU_KEYS = 6;
 MM_HD int pu_key(int cls, int n_sb) { return cls + ((n_sb & 3) ? 3 : 0); }
 // class of flat luma sub-block g from the bucket bases (PlanMeta::sb_base)
+// sb_base is non-decreasing, so the last bucket starting at or before g is the number of bucket
+// starts k >= 1 at or before g: every start is read unconditionally (one batch of scalar loads in
+// k_mc, not a chain of dependent load-compare-branch steps)
 MM_HD int sb_class(int g, const int* sb_base) {
-  int k = N_PU_KEYS - 1;
-  while (k > 0 && g < sb_base[k]) k--;
+  int k = 0;
+#pragma unroll
+  for (int i = 1; i < N_PU_KEYS; i++) k += g >= sb_base[i] ? 1 : 0;
   return k % 3;
 }
 constexpr int N_JOB_KEYS = 64;

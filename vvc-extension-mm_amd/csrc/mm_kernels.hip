@@ -326,14 +326,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   const int g = xcd_block() * blockDim.x + threadIdx.x;
   const int n_sb = meta->n_sb;
   __shared__ PackedTaps s_taps;
+  __shared__ RefDev s_ref[MAX_SLOTS];
   static_assert(sizeof(PackedTaps) % 16 == 0 && sizeof(PackedTaps) / 16 <= 256, "one 16-byte word per thread");
+  static_assert(sizeof(s_ref) % 8 == 0 && sizeof(s_ref) / 8 <= 256, "one 8-byte word per thread");
   if (g - (int)threadIdx.x >= n_sb) return;  // whole workgroup past the end
   if (threadIdx.x < sizeof(PackedTaps) / 16)
     reinterpret_cast<uint4*>(&s_taps)[threadIdx.x] = reinterpret_cast<const uint4*>(&c_packed_taps)[threadIdx.x];
+  if (threadIdx.x < sizeof(s_ref) / 8)
+    reinterpret_cast<uint2*>(s_ref)[threadIdx.x] = reinterpret_cast<const uint2*>(t.ref)[threadIdx.x];
   __syncthreads();
   const Taps taps{c_luma_taps, c_chroma_taps, &s_taps, t.pool};
   if (g >= n_sb) return;
-  mc_thread_rec<UNI_HP>(g, sb_class(g, meta->sb_base), geo, taps, mc, t.ref, dst_y, dsy, dst_cb, dst_cr, dsc);
+  // s_ref: each lane looks its slots' pool offsets up in LDS; indexing the kernel-argument copy
+  // per lane was a dependent global load between the record loads and the window loads
+  mc_thread_rec<UNI_HP>(g, sb_class(g, meta->sb_base), geo, taps, mc, s_ref, dst_y, dsy, dst_cb, dst_cr, dsc);
 }
 
 // --------------------------------------------------------------------------------------------
