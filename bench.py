@@ -190,6 +190,8 @@ def bench_pictures(args, cfg, params, rank, world, local, dist):
     ctx = new_ctx(params, local, pictures)
     if args.stripes:
         ctx.set_stripes(args.stripes)
+    if args.plan_ahead:
+        ctx.set_plan_ahead(True)
     d_pus = [mm360.pus_to_device(p) for _, p, _ in pictures]
     outs = [planes(cfg) for _ in pictures]
     area = [W.luma_area(p) for _, p, _ in pictures]
@@ -220,6 +222,7 @@ def bench_pictures(args, cfg, params, rank, world, local, dist):
     alg_step = float(np.mean([alg[s % P_] for s in range(args.kernel_steps)]))
     achieved = alg_step / (kernel_ms * 1e-3) / 1e9
     got = [tuple(t.cpu().numpy() for t in o) for o in outs]
+    mvp = mvp_per_picture(ctx, cfg, int(np.mean([len(p) for _, p, _ in pictures]))) if args.config == "C3" else None
 
     cpu, bit_exact, mism = None, None, None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -235,7 +238,7 @@ def bench_pictures(args, cfg, params, rank, world, local, dist):
                            if args.uniform_model is not None else ""),
                        "width": cfg.width, "height": cfg.height, "pictures": P_,
                        "pus_per_picture": int(np.mean([len(p) for _, p, _ in pictures])),
-                       "luma_area": int(area[0]), "resident_refs": 2 * P_,
+                       "luma_area": int(area[0]), "resident_refs": 2 * P_, "plan_ahead": bool(args.plan_ahead),
                        "models": [mm360.MODEL_NAMES[m] for m in cfg.models],
                        "parallelism": "1 GPU" if world == 1 else f"replicas x{world} (own pictures per GPU)"},
             "bit_exact": bit_exact, "mismatching_samples": mism,
@@ -248,8 +251,25 @@ def bench_pictures(args, cfg, params, rank, world, local, dist):
                           "pipeline": round(float(st.sum()), 4)},
             "cpu_baseline": cpu,
         }
+        if mvp is not None:
+            line["mvp"] = mvp
         print(json.dumps(line), flush=True)
     ctx.close()
+
+
+def mvp_per_picture(ctx, cfg, n_pus, reps=5):
+    """MM-MVP (mm_mvp_convert) beside the C3 number, outside its timed region:
+    one conversion per PU and list (2 x PUs queries, the seeded query mix tiled), host buffers in
+    and out as the call takes them; best of `reps` synchronous calls."""
+    q = np.resize(W.mvp_queries(cfg.width, cfg.height, cfg.models, 20000, seed=5), 2 * n_pus)
+    ctx.mvp_convert(q)  # warm-up (buffer growth)
+    best = float("inf")
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        ctx.mvp_convert(q)
+        best = min(best, time.perf_counter() - t0)
+    return {"queries_per_picture": int(len(q)), "ms_per_picture": round(best * 1e3, 4),
+            "note": "synchronous host-buffer call incl. PCIe copies; not part of value"}
 
 
 def bench_c4(args, cfg, params, rank, world, local, dist):
@@ -444,6 +464,9 @@ def main():
     ap.add_argument("--kernel-steps", type=int, default=8, help="extra steps timed per launch with HIP events")
     ap.add_argument("--lib", default=None, help="alternative build of libmm360.so (A/B experiments)")
     ap.add_argument("--stripes", type=int, default=None, help="mm_set_stripes (default: the library's)")
+    ap.add_argument("--plan-ahead", type=int, default=1, choices=(0, 1),
+                    help="mm_set_plan_ahead: planning of picture t+1 overlaps picture t's interpolation "
+                         "(every bench PU list is resident before the timed region)")
     ap.add_argument("--c4-emulate", action="store_true",
                     help="C4 rehearsal on one GPU: per-rank stripe MC times for N = 2, 4, 8 + modelled all-gather")
     ap.add_argument("--coherent-mv", action="store_true",

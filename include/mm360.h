@@ -318,6 +318,16 @@ int mm_last_stage_timing(mm_ctx* ctx, float ms[4]);
  * (No reference counterpart: the reference predicts PU by PU.) */
 int mm_set_stripes(mm_ctx* ctx, int stripes);
 
+/* Plan-ahead for mm_pred_device (default off): a picture's planning and setup kernels run on the
+ * internal auxiliary stream, gated by the context stream's position when the PREVIOUS
+ * mm_pred_device call was issued, so they overlap the previous picture's interpolation; the
+ * reprojection and interpolation stay on the context stream after them.  Contract while on: the
+ * device PU list of a call is complete by the time the previous call is issued (written by the
+ * host, or by work enqueued on the context stream before that call).  Applies to one-stripe calls
+ * without stage timing; results do not depend on the setting.  (No reference counterpart: VTM
+ * decodes a picture's PUs inside its own CTU loop.) */
+int mm_set_plan_ahead(mm_ctx* ctx, int on);
+
 #ifdef __cplusplus
 }
 #endif

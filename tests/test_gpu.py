@@ -324,6 +324,45 @@ def test_pred_stripes_do_not_change_results():
             ctx.set_stripes(0)
 
 
+def test_pred_plan_ahead_rotating_pictures():
+    """mm_set_plan_ahead: three different PU lists predicted back to back (twice round, so each
+    plan slot is reused while the other picture's kernels may still run; a smaller list first, so
+    the slot buffers grow mid-sequence), every output == the oracle; a failing PU in the last
+    call is reported, and switching plan-ahead off and on again keeps the results."""
+    cfg = W.CONFIGS["C2"]
+    params = mm360.seq_params(cfg.width, cfg.height, cfg.models)
+    lists = [W.pu_list(cfg, frame=f) for f in (7, 8, 9)]
+    lists.insert(0, lists[0][: len(lists[0]) // 3])
+    refs = {poc: W.ref_planes(cfg.width, cfg.height, poc) for poc in W.REF_POCS}
+    want = [Oracle(params, EPI).predict(W.CUR_POC, p, refs, cfg.width, cfg.height) for p in lists]
+    with _ctx(params) as ctx:
+        for poc, (y, cb, cr) in refs.items():
+            ctx.upload_ref(poc, torch.from_numpy(y).cuda(), torch.from_numpy(cb).cuda(), torch.from_numpy(cr).cuda())
+        d_lists = [mm360.pus_to_device(p) for p in lists]
+        torch.cuda.synchronize()
+        for mode in (1, 0, 1):
+            ctx.set_plan_ahead(bool(mode))
+            order = [0, 1, 2, 3, 1, 2, 3]
+            outs = [_planes(cfg, 0) for _ in order]  # the short list leaves samples at 0, as the oracle
+            for k, o in zip(order, outs):
+                ctx.predict_device(W.CUR_POC, d_lists[k], *o)
+            assert ctx.status() == (mm360.MM_OK, -1)
+            for k, o in zip(order, outs):
+                for x, t, name in zip(want[k], o, ("y", "cb", "cr")):
+                    got = t.cpu().numpy()
+                    assert np.array_equal(got, x), (mode, k, plane_mismatch(name, got, x))
+        bad = lists[2].copy()
+        k_bad = len(bad) // 2
+        bad[k_bad]["x"] = 2
+        d_bad = mm360.pus_to_device(bad)
+        torch.cuda.synchronize()
+        ctx.predict_device(W.CUR_POC, d_lists[1], *_planes(cfg))
+        ctx.predict_device(W.CUR_POC, d_bad, *_planes(cfg))
+        assert ctx.status() == (mm360.MM_ERR_ARG, k_bad)
+        ctx.predict_device(W.CUR_POC, d_lists[3], *_planes(cfg))
+        assert ctx.status() == (mm360.MM_OK, -1)
+
+
 def test_c4_stripe_sublists_into_packed_picture():
     """C4 on one GPU: each of the 8 CTU-row stripe sub-lists of the C3 PU list (one per rank of an
     8-GPU node) is predicted through the C-ABI straight into its segment of the stripe-major packed
@@ -509,16 +548,15 @@ def test_sad_window_vs_oracle(step, sub_shift):
     assert np.array_equal(got, want), np.argwhere(got != want)[:5]
 
 
-def test_sad_window_c5_full_window_vs_twin():
+def test_sad_window_c5_full_window_vs_oracle():
     """C5 geometry (2048x1024, all models, 33x33 integer window) on a seeded subset of the PU
-    grid: the GPU equals the CPU twin of the same bodies, which the CPU suite ties to the oracle."""
-    import twin
+    grid: the GPU equals the oracle (96 blocks x 1089 candidates, ~2 s of oracle time)."""
     w, h = 2048, 1024
     params = mm360.seq_params(w, h, ME_ALL)
     blocks = W.me_blocks(w, h, ME_ALL, grid=16, seed=11, max_blocks=96)
     refs = {poc: W.ref_planes(w, h, poc)[0] for poc in W.REF_POCS}
     org = W.org_plane(w, h)
-    want = twin.sad_window(params, W.CUR_POC, blocks, 16, 16, refs, org, EPI)
+    want = Oracle(params, EPI).sad_window(W.CUR_POC, blocks, 16, 16, refs, org)
     with _me_ctx(params, w, h) as ctx:
         got = ctx.sad_window(W.CUR_POC, blocks, 16, 16).cpu().numpy().view(np.uint32)
     assert np.array_equal(got, want), np.argwhere(got != want)[:5]

@@ -521,6 +521,7 @@ struct PlanSlot {
   DevBuf<PlanMeta> meta;
   DevBuf<mm_int2> mc_meta;
   DevBuf<mm_int4> mc_pos[2];
+  int n_ensured = 0;  // largest stripe size the buffers were sized for (they only grow)
   PlanCaps caps{};
   void release() {
     job_off.release();
@@ -578,6 +579,14 @@ struct mm_ctx {
   hipStream_t aux = nullptr;    // odd stripes run here, overlapping the even stripes' kernels
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int n_stripes = MM_DEFAULT_STRIPES;
+  // plan-ahead (mm_set_plan_ahead): a picture's planning + setup run on `aux` once the context
+  // stream has reached the gate of the previous call, concurrently with that call's
+  // interpolation; the context stream waits for ev_plan before the reprojection
+  bool plan_ahead = false;
+  int ahead_par = 0;                               // slot of the next plan-ahead picture
+  hipEvent_t ev_gate[2] = {nullptr, nullptr};      // alternate: the last recorded one gates the next call
+  int gate_par = 0;
+  hipEvent_t ev_plan = nullptr;
   // validation status words, one per picture, ping-pong: a picture reports into d_status[pic_par]
   // and its first stripe zeroes the other word for the next picture
   DevBuf<unsigned long long> d_status;
@@ -726,7 +735,11 @@ int mm_create(const mm_seq_params* p, int device, mm_ctx** out_ctx) {
       hipEventCreate(&c->ev_stage[2]) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess) {
+      hipEventCreateWithFlags(&c->ev_gate[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_gate[1], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_plan, hipEventDisableTiming) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
+      hipEventRecord(c->ev_gate[0], c->stream) != hipSuccess) {
     mm_destroy(c);
     return MM_ERR_HIP;
   }
@@ -793,6 +806,9 @@ int mm_destroy(mm_ctx* c) {
   }
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+  for (auto& e : c->ev_gate)
+    if (e) (void)hipEventDestroy(e);
+  if (c->ev_plan) (void)hipEventDestroy(c->ev_plan);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   delete c;
@@ -1067,6 +1083,7 @@ static int ensure_slot_buffers(mm_ctx* c, PlanSlot& S, int n) {
     HIPCHK(c, S.mc_pos[l].ensure(k.sb, &fresh));
     if (fresh) HIPCHK(c, hipMemsetAsync(S.mc_pos[l].p, 0, S.mc_pos[l].cap * sizeof(mm_int4), c->stream));
   }
+  S.n_ensured = std::max(S.n_ensured, n);
   return MM_OK;
 }
 
@@ -1077,7 +1094,7 @@ static int ensure_slot_buffers(mm_ctx* c, PlanSlot& S, int n) {
 static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables& t, const Geometry& geo,
                          const mm_pu_desc* d_in, int n, int base, unsigned long long* status,
                          unsigned long long* next_status, int16_t* dy, ptrdiff_t sdy, int16_t* dcb, int16_t* dcr,
-                         ptrdiff_t sdc) {
+                         ptrdiff_t sdc, hipStream_t st_back = nullptr) {
   const PlanCaps& k = S.caps;
   const int gp = (n + PLAN_BLOCK - 1) / PLAN_BLOCK;
   const int gs = (k.jobs + 255) / 256;
@@ -1089,6 +1106,11 @@ static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables
                      S.blkq.p, S.meta.p, k, S.jobs.p, S.job_off.p, S.job_chunk.p);
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[0], st));
   hipLaunchKernelGGL(k_setup_dev, dim3(gs), dim3(256), 0, st, c->sc, S.meta.p, S.jobs.p, t, S.setup.p);
+  if (st_back) {  // plan-ahead: reprojection and interpolation on the context stream
+    HIPCHK(c, hipEventRecord(c->ev_plan, st));
+    HIPCHK(c, hipStreamWaitEvent(st_back, c->ev_plan, 0));
+    st = st_back;
+  }
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[1], st));
   McRec mc;
   mc.meta = S.mc_meta.p;
@@ -1113,7 +1135,7 @@ static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables
 // only_list / hp / store: mm_pred_list (-1 / 0 / 3 for the normal prediction).
 static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, int n, int16_t* dy, ptrdiff_t sdy,
                               int16_t* dcb, int16_t* dcr, ptrdiff_t sdc, int only_list = -1, int hp = 0,
-                              int store = 3) {
+                              int store = 3, bool may_plan_ahead = false) {
   std::vector<std::pair<int, RefDev>> refs;
   refs = ref_slots(c);
   PicTables t;
@@ -1129,9 +1151,35 @@ static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, in
                   (!geo.chroma || !dcb || ((uintptr_t)dcb % 4 == 0 && (uintptr_t)dcr % 4 == 0 && sdc % 2 == 0));
   const int K = c->stage_timing ? 1 : std::max(1, std::min(c->n_stripes, (n + PLAN_BLOCK - 1) / PLAN_BLOCK));
   const int per = (n + K - 1) / K;
-  for (int s = 0; s < std::min(K, 2); s++) RCCHK(ensure_slot_buffers(c, c->slot[s], per));
   unsigned long long* status = c->d_status.p + c->pic_par;
   unsigned long long* next_status = c->d_status.p + (c->pic_par ^ 1);
+  if (may_plan_ahead && c->plan_ahead && K == 1 && !c->stage_timing) {
+    // Plan-ahead: planning + setup of this picture on `aux`, gated only by the context stream's
+    // position at the start of the previous call (its slot's previous user, two calls back, has
+    // finished there), so they overlap the previous picture's interpolation.
+    if (per > c->slot[0].n_ensured || per > c->slot[1].n_ensured) {
+      // growing frees buffers the other stream may still use, and zeroes on the context stream
+      HIPCHK(c, hipStreamSynchronize(c->aux));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      for (int s = 0; s < 2; s++) RCCHK(ensure_slot_buffers(c, c->slot[s], per));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+    } else {
+      for (int s = 0; s < 2; s++) RCCHK(ensure_slot_buffers(c, c->slot[s], per));  // caps only
+    }
+    HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_gate[c->gate_par], 0));
+    c->gate_par ^= 1;
+    HIPCHK(c, hipEventRecord(c->ev_gate[c->gate_par], c->stream));
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    RCCHK(launch_stripe(c, c->slot[c->ahead_par], c->aux, t, geo, d_in, n, 0, status, next_status, dy, sdy, dcb, dcr,
+                        sdc, c->stream));
+    c->ahead_par ^= 1;
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    c->last_status = status;
+    c->pic_par ^= 1;
+    c->status_pending = true;
+    return MM_OK;
+  }
+  for (int s = 0; s < std::min(K, 2); s++) RCCHK(ensure_slot_buffers(c, c->slot[s], per));
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
   if (K > 1) {
     HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
@@ -1148,9 +1196,18 @@ static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, in
     HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
   }
   HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+  // a following plan-ahead call starts its planning only after this whole call (both slots used)
+  c->gate_par ^= 1;
+  HIPCHK(c, hipEventRecord(c->ev_gate[c->gate_par], c->stream));
   c->last_status = status;
   c->pic_par ^= 1;
   c->status_pending = true;
+  return MM_OK;
+}
+
+int mm_set_plan_ahead(mm_ctx* c, int on) {
+  if (!c) return MM_ERR_ARG;
+  c->plan_ahead = on != 0;
   return MM_OK;
 }
 
@@ -1184,7 +1241,7 @@ int mm_pred_device(mm_ctx* c, int cur_poc, const mm_pu_desc* d_pus, int n, int16
   if (!c || n < 0 || (n > 0 && !d_pus) || !dy || (c->geo.chroma && (!dcb || !dcr))) return MM_ERR_ARG;
   if (n == 0) return MM_OK;
   HIPCHK(c, hipSetDevice(c->device));
-  return launch_device_plan(c, cur_poc, d_pus, n, dy, sdy, dcb, dcr, sdc);
+  return launch_device_plan(c, cur_poc, d_pus, n, dy, sdy, dcb, dcr, sdc, -1, 0, 3, true);
 }
 
 int mm_pred_status(mm_ctx* c, int* first_bad_pu) {

@@ -51,7 +51,7 @@ EXPORTED_SYMBOLS = (
     "mm_set_epipole", "mm_upload_ref", "mm_release_ref", "mm_reproject", "mm_pred",
     "mm_pred_device", "mm_pred_status", "mm_pred_prepare", "mm_pred_run", "mm_filter", "mm_last_timing",
     "mm_set_stage_timing", "mm_last_stage_timing", "mm_upload_org", "mm_sad_window", "mm_pred_dmvr", "mm_mvp_convert",
-    "mm_set_stripes", "mm_pred_list", "mm_derive_effective_blocks", "mm_epipole_list_create",
+    "mm_set_stripes", "mm_set_plan_ahead", "mm_pred_list", "mm_derive_effective_blocks", "mm_epipole_list_create",
     "mm_epipole_list_destroy", "mm_get_epipole_list", "mm_epipole_add", "mm_epipole_make_available", "mm_epipole_has",
     "mm_epipole_find", "mm_epipole_derive_predictor", "mm_epipole_count",
 )
@@ -166,6 +166,7 @@ def load_library() -> ctypes.CDLL:
         "mm_sad_window": (c_int, [vp, c_int, vp, c_int, c_int, c_int, vp]),
         "mm_last_stage_timing": (c_int, [vp, POINTER(c_float)]),
         "mm_set_stripes": (c_int, [vp, c_int]),
+        "mm_set_plan_ahead": (c_int, [vp, c_int]),
         "mm_pred_list": (c_int, [vp, c_int, vp, c_int, c_int, c_int, vp, ctypes.c_ssize_t, vp, vp,
                                  ctypes.c_ssize_t]),
         "mm_derive_effective_blocks": (c_int, [POINTER(ToolFlags), vp, c_int, vp, vp, c_int, POINTER(c_int), vp,
@@ -459,6 +460,11 @@ class MMContext:
     def set_stripes(self, stripes: int):
         """Stripe pipelining of the device-planned path (mm_set_stripes)."""
         self._check(self.lib.mm_set_stripes(self.h, int(stripes)))
+
+    def set_plan_ahead(self, on: bool):
+        """Plan-ahead of the device-planned path (mm_set_plan_ahead): the device PU list of each
+        predict_device call must be complete before the previous call is issued."""
+        self._check(self.lib.mm_set_plan_ahead(self.h, int(on)))
 
     def last_stage_timing_ms(self):
         """(planning, k_setup, k_reproj, k_mc) device milliseconds of the last launch sequence."""
