@@ -276,6 +276,8 @@ def bench_c4(args, cfg, params, rank, world, local, dist):
     """C4: one C3 picture per step, CTU-row sharded over the ranks, one packed all-gather."""
     (cur, pus, refs), = picture_set(cfg, 1)
     ctx = new_ctx(params, local, [(cur, pus, refs)])
+    if args.plan_ahead:  # the stripe list is resident (mm_pred_prepare) before the timed region
+        ctx.set_plan_ahead(True)
     mine = P.shard_pus(pus, cfg.height, world, rank)
     ctx.prepare(cur, mine)
     lay = P.StripeLayout(cfg.width, cfg.height, world)
@@ -335,7 +337,7 @@ def bench_c4(args, cfg, params, rank, world, local, dist):
                                    f"RCCL all-gather per picture", "width": cfg.width, "height": cfg.height,
                        "pus": int(len(pus)), "pus_rank0": int(len(mine)), "luma_area": int(area),
                        "stripe_ctu_rows": lay.rows // 128, "allgather_bytes_in_per_rank": int(ag_bytes),
-                       "parallelism": f"ctu-row stripes x{world}"},
+                       "plan_ahead": bool(args.plan_ahead), "parallelism": f"ctu-row stripes x{world}"},
             "mc_only": {"value": round(area * args.steps / t_mc / 1e6, 2), "ms_per_step": round(t_mc / args.steps * 1e3, 4),
                         "note": "same loop without the all-gather (references pre-replicated)"},
             "bit_exact": bit_exact,
