@@ -361,10 +361,13 @@ def bench_c4_emulate(args, cfg, params):
     (two picture buffers: max(mc, allgather)) or not (mc + allgather)."""
     (cur, pus, refs), = picture_set(cfg, 1)
     ctx = new_ctx(params, 0, [(cur, pus, refs)])
+    if args.plan_ahead:
+        ctx.set_plan_ahead(True)
     area = W.luma_area(pus)
     pic_bytes = cfg.width * cfg.height * 2 * 3 // 2
     dy, dcb, dcr = planes(cfg)
-    out = {"note": "one-GPU rehearsal: measured stripe MC times, all-gather times modelled", "n": {}}
+    out = {"note": "one-GPU rehearsal: measured stripe MC times, all-gather times modelled", "n": {},
+           "plan_ahead": bool(args.plan_ahead)}
     link = 153e9
     for n in (1, 2, 4, 8):
         worst = 0.0
