@@ -84,7 +84,7 @@ def cpu_threads():
     return max(1, min(16, n))  # the GPU box's CPU share is 16 threads per GPU
 
 
-def picture_set(cfg, n, frame0=0, uniform_model=None, coherent=False):
+def picture_set(cfg, n, frame0=0, uniform_model=None, coherent=False, dmvr_share=0.0):
     """n pictures: (cur_poc, PU list, {poc: planes}) with disjoint reference pairs."""
     out = []
     for f in range(n):
@@ -92,7 +92,7 @@ def picture_set(cfg, n, frame0=0, uniform_model=None, coherent=False):
         if uniform_model is not None:
             pus = W.pu_list(cfg, frame=frame0 + f, uniform=True, uniform_model=uniform_model)
         else:
-            pus = W.pu_list(cfg, frame=frame0 + f)
+            pus = W.pu_list(cfg, frame=frame0 + f, dmvr_share=dmvr_share)
         if coherent:
             pus["mv"][:, 0, :] = (85, -43)
             pus["mv"][:, 1, :] = (-37, 91)
@@ -152,21 +152,22 @@ def cpu_baseline_and_check(args, cfg, params, pictures, gpu_out):
     padded = [orc.padded_refs(refs) for _, _, refs in pictures]
     pad_s = (time.perf_counter() - t) / len(pictures)
     threads = cpu_threads()
-    # (b) all threads, every picture once -> bit-exact check
+    # (b) all threads, every picture once -> bit-exact check (MM_PUF_DMVR PUs: the oracle's serial
+    # DMVR restatement after the PU-parallel rest)
     mismatches = 0
     t_all, area_all = 0.0, 0
-    for (cur, pus, _), pr, got in zip(pictures, padded, gpu_out):
+    for (cur, pus, refs), pr, got in zip(pictures, padded, gpu_out):
         t = time.perf_counter()
-        want = orc.predict_padded(pr, cur, pus, cfg.width, cfg.height, threads)
+        want = orc.predict_mixed(cur, pus, refs, cfg.width, cfg.height, prefs=pr, threads=threads)
         t_all += time.perf_counter() - t
         area_all += W.luma_area(pus)
         mismatches += sum(int((g != w).sum()) for g, w in zip(got, want))
     # (a) one thread, bounded sample
     t_one, area_one, n_one = 0.0, 0, 0
     while t_one < args.cpu_seconds:
-        cur, pus, _ = pictures[n_one % len(pictures)]
+        cur, pus, refs = pictures[n_one % len(pictures)]
         t = time.perf_counter()
-        orc.predict_padded(padded[n_one % len(pictures)], cur, pus, cfg.width, cfg.height, 1)
+        orc.predict_mixed(cur, pus, refs, cfg.width, cfg.height, prefs=padded[n_one % len(pictures)], threads=1)
         t_one += time.perf_counter() - t
         area_one += W.luma_area(pus)
         n_one += 1
@@ -186,8 +187,10 @@ def cpu_baseline_and_check(args, cfg, params, pictures, gpu_out):
 def bench_pictures(args, cfg, params, rank, world, local, dist):
     """C3 (and C2 / uniform-model variants): rotating pictures, one per step."""
     pictures = picture_set(cfg, args.pictures, frame0=rank * args.pictures, uniform_model=args.uniform_model,
-                           coherent=args.coherent_mv)
+                           coherent=args.coherent_mv, dmvr_share=args.dmvr_share)
     ctx = new_ctx(params, local, pictures)
+    if args.dmvr_share > 0:
+        ctx.set_dmvr(True)
     if args.stripes:
         ctx.set_stripes(args.stripes)
     if args.plan_ahead:
@@ -195,6 +198,7 @@ def bench_pictures(args, cfg, params, rank, world, local, dist):
     d_pus = [mm360.pus_to_device(p) for _, p, _ in pictures]
     outs = [planes(cfg) for _ in pictures]
     area = [W.luma_area(p) for _, p, _ in pictures]
+    dmvr_area_frac = float(np.mean([W.luma_area(p[W.dmvr_flagged(p)]) / W.luma_area(p) for _, p, _ in pictures]))
     alg = [W.algorithmic_bytes(p) for _, p, _ in pictures]
     P_ = len(pictures)
 
@@ -235,7 +239,9 @@ def bench_pictures(args, cfg, params, rank, world, local, dist):
             "data": "synthetic (seeded ERP planes + PU lists, SURVEY 8(d))",
             "config": {"workload": f"{args.config}: {cfg.description}" + (
                            f" [uniform 16x16 PUs, model {mm360.MODEL_NAMES[args.uniform_model]}]"
-                           if args.uniform_model is not None else ""),
+                           if args.uniform_model is not None else "") + (
+                           f" [MM-DMVR: {args.dmvr_share:.0%} of the DMVR-eligible bi leaves, "
+                           f"{dmvr_area_frac:.1%} of the luma area]" if args.dmvr_share > 0 else ""),
                        "width": cfg.width, "height": cfg.height, "pictures": P_,
                        "pus_per_picture": int(np.mean([len(p) for _, p, _ in pictures])),
                        "luma_area": int(area[0]), "resident_refs": 2 * P_, "plan_ahead": bool(args.plan_ahead),
@@ -257,19 +263,38 @@ def bench_pictures(args, cfg, params, rank, world, local, dist):
     ctx.close()
 
 
-def mvp_per_picture(ctx, cfg, n_pus, reps=5):
-    """MM-MVP (mm_mvp_convert) beside the C3 number, outside its timed region:
-    one conversion per PU and list (2 x PUs queries, the seeded query mix tiled), host buffers in
-    and out as the call takes them; best of `reps` synchronous calls."""
+def mvp_per_picture(ctx, cfg, n_pus, reps=10):
+    """MM-MVP (mm_mvp_convert_device) beside the C3 number, outside its timed
+    region: one conversion per PU and list (2 x PUs queries, the seeded query mix tiled), queries
+    and results resident in HBM, stream-ordered on the context stream; device time of each call
+    from HIP events around its launch (mm_last_timing), and wall time per call over `reps`
+    back-to-back calls.  The synchronous host-buffer call (PCIe copies in and out) is reported
+    beside it."""
     q = np.resize(W.mvp_queries(cfg.width, cfg.height, cfg.models, 20000, seed=5), 2 * n_pus)
-    ctx.mvp_convert(q)  # warm-up (buffer growth)
-    best = float("inf")
+    d_q = mm360.queries_to_device(q)
+    d_out = torch.zeros((len(q), 2), dtype=torch.int32, device="cuda")
+    ctx.mvp_convert_device(d_q, d_out)  # warm-up (epipole table upload)
+    ctx.mvp_status()
+    dev = []
     for _ in range(reps):
+        ctx.mvp_convert_device(d_q, d_out)
+        dev.append(ctx.last_timing_ms())
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ctx.mvp_convert_device(d_q, d_out)
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / reps
+    ctx.mvp_status()
+    ctx.mvp_convert(q)  # host-buffer form (warm-up of its buffers)
+    host = float("inf")
+    for _ in range(3):
         t0 = time.perf_counter()
         ctx.mvp_convert(q)
-        best = min(best, time.perf_counter() - t0)
-    return {"queries_per_picture": int(len(q)), "ms_per_picture": round(best * 1e3, 4),
-            "note": "synchronous host-buffer call incl. PCIe copies; not part of value"}
+        host = min(host, time.perf_counter() - t0)
+    return {"queries_per_picture": int(len(q)), "ms_per_picture": round(wall * 1e3, 4),
+            "kernel_ms": round(float(np.mean(dev)), 4), "host_buffer_call_ms": round(host * 1e3, 4),
+            "note": "device-resident queries (mm_mvp_convert_device), back-to-back calls; not part of value"}
 
 
 def bench_c4(args, cfg, params, rank, world, local, dist):
@@ -476,6 +501,9 @@ def main():
                     help="C4 rehearsal on one GPU: per-rank stripe MC times for N = 2, 4, 8 + modelled all-gather")
     ap.add_argument("--coherent-mv", action="store_true",
                     help="experiment: one MV for every PU and list (spatially coherent motion)")
+    ap.add_argument("--dmvr-share", type=float, default=0.0,
+                    help="C2/C3: this share of the DMVR-eligible bi leaves are merge/mvRefine PUs that run MM-DMVR "
+                         "inside the picture's launch sequence (mm_set_dmvr, MM_PUF_DMVR)")
     ap.add_argument("--uniform-model", type=int, default=None,
                     help="per-model workload: all PUs 16x16 with this MotionModelID (SURVEY 8(d))")
     ap.add_argument("--dist-backend", default="nccl",

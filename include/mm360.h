@@ -93,18 +93,28 @@ typedef struct mm_block_desc {
  * (CommonDef.h:348-349) is the plain addAvg.  Only bi PUs use it. */
 #define MM_BCW_DEFAULT 2
 
+/* mm_pu_desc.flags */
+#define MM_PUF_DMVR 0x1u  /* bi PU that passed PU::checkDMVRCondition (UnitTools.cpp:1698-1726): mm_pred_device
+                             runs xProcessDMVRProjected's search on its 16x16 sub-PUs before predicting them
+                             (needs mm_set_dmvr(ctx, 1), the picture's DMVR enable) */
+
 /* One prediction unit (or sub-PU after the host's xSubPuBio / DMVR / SbTMVP split; the helpers in
  * host/mm360_vtm.hpp derive these effective blocks).  64 bytes.  The PUs of one call must not
  * overlap (every luma sample is predicted by at most one PU, as in a decoded picture); the result
  * of an overlapping list is undefined, and a list whose PUs cover more sub-blocks than the
- * picture has is rejected with MM_ERR_ARG. */
+ * picture has is rejected with MM_ERR_ARG.
+ * NOTE for zero-initialised descriptors: bcw_idx uses the reference encoding, in which 0 is the
+ * (-2, 10) weight pair, not the plain average -- bi PUs must set bcw_idx = MM_BCW_DEFAULT (2).
+ * flags bits other than MM_PUF_* and nonzero reserved words are rejected with MM_ERR_ARG (so a
+ * stale 48-byte layout fails loudly instead of predicting garbage). */
 typedef struct mm_pu_desc {
   int32_t x, y, w, h;          /* luma area */
   int32_t mv[2][2];            /* [list][hor, ver], 1/16 luma */
   int32_t ref_poc[2];          /* reference POC per list, -1 = list unused */
   int32_t model[2];            /* mm_model_id per list (non-CLASSIC for MM MC) */
   int32_t bcw_idx;             /* CU::bcwIdx 0..4 (bi PUs; MM_BCW_DEFAULT = addAvg); ignored for uni */
-  int32_t reserved[3];         /* must be zero */
+  uint32_t flags;              /* MM_PUF_* */
+  int32_t reserved[2];         /* must be zero */
 } mm_pu_desc;
 
 /* ---- Effective blocks (host-side, no GPU) ----------------------------------------------------
@@ -208,7 +218,8 @@ int mm_upload_ref(mm_ctx* ctx, int poc, const int16_t* y, ptrdiff_t stride_y, co
 int mm_release_ref(mm_ctx* ctx, int poc);
 
 /* Parity API: n blocks, results written to out_xy (host memory) as int32 pairs
- * [X0, Y0, X1, Y1, ...] block after block, N_b = (w/sbw)*(h/sbh) pairs per block. */
+ * [X0, Y0, X1, Y1, ...] block after block, N_b = (w/sbw)*(h/sbh) pairs per block.  Blocks are at
+ * most 128 x 128 in component units (VVC's MAX_CU_SIZE; MM_ERR_ARG beyond). */
 int mm_reproject(mm_ctx* ctx, const mm_block_desc* blocks, int n, int32_t* out_xy);
 
 /* Batched motion compensation of one picture's PU list (host descriptor array).
@@ -264,15 +275,25 @@ int mm_pred_list(mm_ctx* ctx, int cur_poc, const mm_pu_desc* pus, int n, int lis
  * refinement on 14-bit luma predictions, then is predicted as a bi PU at the refined MVs (all
  * components, addAvg) into the destination planes (device memory).  mvd_out (host, optional):
  * the refined L0 delta (1/16 luma, pu.mvdL0SubPu) of every sub-PU, PU after PU, sub-PUs in raster
- * order.  Synchronous. */
+ * order.  Synchronous.  (The same device path as MM_PUF_DMVR PUs under mm_set_dmvr, with every PU
+ * of the list flagged.) */
 int mm_pred_dmvr(mm_ctx* ctx, int cur_poc, const mm_pu_desc* pus, int n, int16_t* dst_y,
                  ptrdiff_t dst_stride_y, int16_t* dst_cb, int16_t* dst_cr, ptrdiff_t dst_stride_c,
                  int32_t* mvd_out);
 
 /* MM-MVP, batched: motionVectorInDesiredMotionModel for n queries (the candidate's modelMotion
  * at `pos` on a 1x1 array, then the desired model's motionVectorForEquivalentPixelShiftAt,
- * NaN -> zero MV, std::round to fixed point).  mv_out (host): 2 int32 per query.  Synchronous. */
+ * NaN -> zero MV, std::round to fixed point).  mv_out (host): 2 int32 per query.  Synchronous;
+ * the first failing query's code is returned (MM_ERR_MODEL / MM_ERR_ARG / MM_ERR_NOEPIPOLE). */
 int mm_mvp_convert(mm_ctx* ctx, const mm_mvp_query* queries, int n, int32_t* mv_out);
+
+/* The same with queries and results in device memory: validation, GEODESIC_CAMPOSE epipole lookup
+ * (a device copy of the context's EpipoleList, refreshed when the list changed) and both model
+ * evaluations run on the device, stream-ordered on the context stream with no host
+ * synchronisation.  The lowest failing query's code is reported by the next mm_mvp_status /
+ * mm_synchronize (its result words are 0). */
+int mm_mvp_convert_device(mm_ctx* ctx, const mm_mvp_query* d_queries, int n, int32_t* d_mv_out);
+int mm_mvp_status(mm_ctx* ctx, int* first_bad_query);
 
 /* Single-block interpolation (InterpolationFilter::filterHor/filterVer on the device), for
  * parity tests of the integer pel pipeline.  comp 0 = luma 8-tap (16 phases), else chroma 4-tap
@@ -317,6 +338,14 @@ int mm_last_stage_timing(mm_ctx* ctx, float ms[4]);
  * write disjoint samples: results do not depend on the setting.  Stage timing forces one stripe.
  * (No reference counterpart: the reference predicts PU by PU.) */
 int mm_set_stripes(mm_ctx* ctx, int stripes);
+
+/* The picture's DMVR enable (sps DMVR && !ph_dmvr_disabled; default off): with it on, PUs of an
+ * mm_pred / mm_pred_device list flagged MM_PUF_DMVR run xProcessDMVRProjected's search (25-point
+ * integer + parabolic sub-pel, InterPrediction.cpp:2442-2634) on their <= 16x16 sub-PUs inside the
+ * same asynchronous launch sequence -- planning, search, decision, then the refined sub-PUs'
+ * setup / reprojection / interpolation with the rest of the picture.  Forces one stripe.  With it
+ * off, a flagged PU is rejected (MM_ERR_ARG). */
+int mm_set_dmvr(mm_ctx* ctx, int on);
 
 /* Plan-ahead for mm_pred_device (default off): a picture's planning and setup kernels run on the
  * internal auxiliary stream, gated by the context stream's position when the PREVIOUS

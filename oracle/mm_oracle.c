@@ -1522,7 +1522,8 @@ static int o_check_dmvr(const OEff* x, const mm_pu_desc* pu, int poc, unsigned f
 
 static void o_emit(OEff* x, const mm_pu_desc* pu, int to_dmvr) {
   mm_pu_desc d = *pu;
-  d.reserved[0] = d.reserved[1] = d.reserved[2] = 0;
+  d.flags = 0;
+  d.reserved[0] = d.reserved[1] = 0;
   if (to_dmvr) {
     if (x->n_dmvr < x->cap_dmvr) x->dmvr[x->n_dmvr] = d;
     x->n_dmvr++;

@@ -169,16 +169,20 @@ class Oracle:
             raise RuntimeError(f"oracle predict_list failed: {rc}")
         return dy, dcb, dcr
 
-    def predict_dmvr(self, cur_poc, pus, refs, W, H):
-        """MM-DMVR PUs (xProcessDMVRProjected): predicted planes and the per-sub-PU L0 deltas."""
+    def predict_dmvr(self, cur_poc, pus, refs, W, H, out=None):
+        """MM-DMVR PUs (xProcessDMVRProjected): predicted planes and the per-sub-PU L0 deltas.
+        out: (Y, Cb, Cr) planes to predict into (only the PUs' samples are written)."""
         pus = np.ascontiguousarray(pus)
         pocs = sorted(refs)
         ys = [np.ascontiguousarray(refs[p][0]) for p in pocs]
         cbs = [np.ascontiguousarray(refs[p][1]) for p in pocs]
         crs = [np.ascontiguousarray(refs[p][2]) for p in pocs]
-        dy = np.zeros((H, W), dtype=np.int16)
-        dcb = np.zeros((H // 2, W // 2), dtype=np.int16)
-        dcr = np.zeros((H // 2, W // 2), dtype=np.int16)
+        if out is None:
+            dy = np.zeros((H, W), dtype=np.int16)
+            dcb = np.zeros((H // 2, W // 2), dtype=np.int16)
+            dcr = np.zeros((H // 2, W // 2), dtype=np.int16)
+        else:
+            dy, dcb, dcr = out
         nsub = int(sum(((int(u["w"]) + 15) // 16) * ((int(u["h"]) + 15) // 16) for u in pus))
         mvd = np.zeros((max(nsub, 1), 2), dtype=np.int32)
         pa = np.array(pocs, dtype=np.int32)
@@ -190,6 +194,22 @@ class Oracle:
         if rc:
             raise RuntimeError(f"oracle predict_dmvr failed: {rc}")
         return (dy, dcb, dcr), mvd[:nsub]
+
+    def predict_mixed(self, cur_poc, pus, refs, W, H, prefs=None, threads=1):
+        """A picture list in which PUs flagged MM_PUF_DMVR (flags bit 0) run MM-DMVR: the other PUs
+        through predict (predict_padded when prefs is given), then the flagged ones through
+        predict_dmvr into the same planes (PUs do not overlap)."""
+        dm = (np.asarray(pus["flags"]) & 1) != 0
+        rest = np.ascontiguousarray(pus[~dm])
+        if prefs is not None:
+            planes = self.predict_padded(prefs, cur_poc, rest, W, H, threads)
+        else:
+            planes = self.predict(cur_poc, rest, refs, W, H)
+        if dm.any():
+            d = np.ascontiguousarray(pus[dm]).copy()
+            d["flags"] = 0
+            self.predict_dmvr(cur_poc, d, refs, W, H, out=planes)
+        return planes
 
     def mvp(self, queries):
         """MM-MVP conversions: int32 [n, 2]."""

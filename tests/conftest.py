@@ -19,6 +19,7 @@ def _native_builds():
     """Make sure the oracle and the CPU twin are built (cheap no-op when up to date)."""
     for d in ("oracle", os.path.join("tests", "native")):
         subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, d)])
+    subprocess.check_call(["make", "-s", "-j4", "-C", os.path.join(ROOT, "tests", "native"), "variants"])
     yield
 
 

@@ -22,6 +22,7 @@ struct Twin {
   Geometry geo;
   std::vector<float> px[3], py[3];
   std::vector<uint8_t> vip[3];
+  std::vector<float> trig;  // separable toSphere table (MpaCache::trig_col / trig_row)
 };
 
 static void make_twin(const mm_seq_params* p, Twin* t) {
@@ -36,6 +37,8 @@ static void make_twin(const mm_seq_params* p, Twin* t) {
                     p->bit_depth,    p->chroma_format == 1, 0,                     0,
                     3,               0};
   const int cols = p->width / 4, rows = p->height / 4, n = cols * rows;
+  t->trig.assign((size_t)4 * (cols + rows), 0.0f);
+  for (int i = 0; i < 2 * (cols + rows); i++) erp_trig_thread(i, t->sc, cols, rows, t->trig.data(), t->trig.data() + 4 * cols);
   for (int pl = 0; pl < 3; pl++) {
     if (!(p->active_models & (1u << (MPA_FRONT_BACK + pl)))) continue;
     t->px[pl].resize(n);
@@ -57,6 +60,8 @@ static MpaCache cache_of(const Twin& t) {
   }
   c.cols = t.geo.W / 4;
   c.rows = t.geo.H / 4;
+  c.trig_col = t.trig.data();
+  c.trig_row = t.trig.data() + 4 * c.cols;
   return c;
 }
 
@@ -95,37 +100,65 @@ extern "C" int twin_reproject(const mm_seq_params* p, int n_epi, const int32_t* 
   return 0;
 }
 
-// The device-planned prediction path (mm_devplan.h + mm_pipeline.h bodies), run sequentially.
+// The device-planned prediction path (mm_devplan.h + mm_pipeline.h bodies), run sequentially,
+// including the MM-DMVR search of MM_PUF_DMVR PUs (mm_dmvr.h bodies) between placement and setup.
+// mvd (optional): the refined deltas of the DMVR sub-PUs in placement order.
 static int twin_pred_list(const Twin& t, const mmdev::PicTables& tab, const mm_pu_desc* pus, int n, int16_t* dy,
-                          int sdy, int16_t* dcb, int16_t* dcr, int sdc, int hp = 0, int store = 3) {
+                          int sdy, int16_t* dcb, int16_t* dcr, int sdc, int hp = 0, int store = 3,
+                          std::vector<int32_t>* mvd = nullptr) {
   using namespace mmdev;
+  using namespace mmdmvr;
   std::vector<PuPlan> plans(n);
   PlanCounters cnt{};
   for (int i = 0; i < n; i++) {
     classify_pu(pus[i], tab, &plans[i]);
     if (plans[i].code) return plans[i].code;
-    cnt.pu_tot[plans[i].key] += pack_count(1, plans[i].n_sb);
+    cnt.pu_tot[plans[i].key] += pu_count(plans[i]);
     for (int k = 0; k < 4; k++)
-      if (plans[i].job[k].valid) cnt.job_tot[plans[i].job[k].key] += pack_count(1, plans[i].job[k].n);
+      if (plans[i].job[k].valid) cnt.job_tot[plans[i].job[k].key] += job_count(plans[i], k);
+    if (plans[i].dmvr) cnt.dmvr_tot += dmvr_count(plans[i]);
   }
   PlanMeta m;
   plan_meta(cnt, &m);
   std::vector<JobDev> jobs(m.n_jobs);
   std::vector<int> job_off(m.n_jobs), job_chunk(m.n_elems / 64 + 1);
+  std::vector<SubPuDev> subs(m.n_sub);
+  std::vector<int> sub_off(m.n_sub), sub_chunk(m.n_dmvr_elems / 64 + 1);
   for (int i = 0; i < n; i++) {
     const PuPlan& pp = plans[i];
     const unsigned long long bp = cnt.pu_cur[pp.key];
-    cnt.pu_cur[pp.key] += pack_count(1, pp.n_sb);
+    cnt.pu_cur[pp.key] += pu_count(pp);
     int jidx[4] = {0, 0, 0, 0}, joff[4] = {0, 0, 0, 0};
     for (int k = 0; k < 4; k++) {
       if (!pp.job[k].valid) continue;
       const int key = pp.job[k].key;
       jidx[k] = m.job_base[key] + packed_items(cnt.job_cur[key]);
       joff[k] = m.elem_base[key] + packed_elems(cnt.job_cur[key]);
-      cnt.job_cur[key] += pack_count(1, pp.job[k].n);
+      cnt.job_cur[key] += job_count(pp, k);
     }
+    const unsigned long long bd = cnt.dmvr_cur;
+    if (pp.dmvr) cnt.dmvr_cur += dmvr_count(pp);
     emit_pu(pus[i], pp, m.sb_base[pp.key] + packed_elems(bp), jidx, joff, jobs.data(), job_off.data(),
-            job_chunk.data());
+            job_chunk.data(), packed_items(bd), packed_elems(bd), subs.data(), sub_off.data(), sub_chunk.data());
+  }
+  const Taps taps{LUMA_T, CHROMA_T, nullptr, RefPool{}};
+  MpaCache c = cache_of(t);
+  if (m.n_sub) {
+    std::vector<BlockSetup> dset((size_t)m.n_sub * N_OFF * 2);
+#pragma omp parallel for schedule(static)
+    for (int j = 0; j < m.n_sub * N_OFF * 2; j++) dmvr_setup_thread(j, t.sc, subs.data(), tab.ged, dset.data());
+    std::vector<uint32_t> costs((size_t)m.n_sub * N_OFF, 0);
+#pragma omp parallel for schedule(static, 256)
+    for (long g = 0; g < m.n_dmvr_elems; g++) {
+      int idx;
+      const int si = find_item(sub_off.data(), sub_chunk.data(), (int)g, m.n_sub);
+      uint32_t v = dmvr_cost_thread((int)g, si, t.sc, t.geo, taps, subs.data(), dset.data(), c, tab.ref, &idx);
+#pragma omp atomic
+      costs[idx] += v;
+    }
+    if (mvd) mvd->assign(2 * (size_t)m.n_sub, 0);
+    for (int s = 0; s < m.n_sub; s++)
+      dmvr_decide_jobs_thread(s, subs.data(), costs.data(), jobs.data(), mvd ? mvd->data() : nullptr);
   }
   std::vector<BlockSetup> setups(m.n_jobs);
 #pragma omp parallel for schedule(static)
@@ -138,21 +171,19 @@ static int twin_pred_list(const Twin& t, const mmdev::PicTables& tab, const mm_p
     pos[l].assign(std::max(m.n_sb, 1), mm_int4{});
     mc.pos[l] = pos[l].data();
   }
-  MpaCache c = cache_of(t);
 #pragma omp parallel for schedule(static, 256)
   for (int g = 0; g < m.n_elems; g++)
     reproj_thread_mc(g, find_item(job_off.data(), job_chunk.data(), g, m.n_jobs), t.sc, jobs.data(), job_off.data(),
                      setups.data(), c, mc);
-  const Taps taps{LUMA_T, CHROMA_T, nullptr, RefPool{}};
   Geometry geo = t.geo;
   geo.hp = hp;
   geo.store = store;
 #pragma omp parallel for schedule(static, 256)
   for (int g = 0; g < m.n_sb; g++)
     if (geo.hp)
-      mc_thread_rec<true>(g, sb_class(g, m.sb_base), geo, taps, mc, tab.ref, dy, sdy, dcb, dcr, sdc);
+      mc_thread_rec<true>(g, geo, taps, mc, tab.ref, dy, sdy, dcb, dcr, sdc);
     else
-      mc_thread_rec<false>(g, sb_class(g, m.sb_base), geo, taps, mc, tab.ref, dy, sdy, dcb, dcr, sdc);
+      mc_thread_rec<false>(g, geo, taps, mc, tab.ref, dy, sdy, dcb, dcr, sdc);
   return 0;
 }
 
@@ -314,15 +345,14 @@ extern "C" int twin_sad_window(const mm_seq_params* p, int n_epi, const int32_t*
   return 0;
 }
 
-// MM-DMVR (mm_pred_dmvr): the product's planner and mm_dmvr.h bodies, then the refined sub-PUs
-// through the device-planned prediction path.
+// MM-DMVR (mm_pred_dmvr): every PU flagged MM_PUF_DMVR through the device-planned path (the
+// product's planner, mm_dmvr.h search bodies and the prediction bodies).
 extern "C" int twin_pred_dmvr(const mm_seq_params* p, int n_epi, const int32_t* epi, int cur_poc,
                               const mm_pu_desc* pus, int n, int n_refs, const int32_t* pocs,
                               const int16_t* const* ys, const int16_t* const* cbs, const int16_t* const* crs,
                               int stride_y, int stride_c, int16_t* dy, int sdy, int16_t* dcb, int16_t* dcr, int sdc,
                               int32_t* mvd_out) {
   using namespace mmdev;
-  using namespace mmdmvr;
   Twin t;
   make_twin(p, &t);
   EpipoleMap em = epi_of(n_epi, epi);
@@ -334,43 +364,50 @@ extern "C" int twin_pred_dmvr(const mm_seq_params* p, int n_epi, const int32_t* 
   std::string err;
   int rc = build_pic_tables(seq_info(*p), em, cur_poc, refs, &tab, &err);
   if (rc) return rc;
-  DmvrPlan plan;
-  rc = plan_dmvr(seq_info(*p), tab, pus, n, &plan, &err);
+  tab.dmvr = 1;
+  std::vector<mm_pu_desc> flagged(pus, pus + n);
+  for (auto& u : flagged) u.flags |= MM_PUF_DMVR;
+  std::vector<int32_t> mvd;
+  rc = twin_pred_list(t, tab, flagged.data(), n, dy, sdy, dcb, dcr, sdc, 0, 3, &mvd);
   if (rc) return rc;
-  const int ns = (int)plan.sub.size();
-  std::vector<BlockSetup> setups((size_t)ns * N_OFF * 2);
-#pragma omp parallel for schedule(static)
-  for (int j = 0; j < ns * N_OFF * 2; j++) dmvr_setup_thread(j, t.sc, plan.sub.data(), tab.ged, setups.data());
-  std::vector<uint32_t> costs((size_t)ns * N_OFF, 0);
-  const Taps taps{LUMA_T, CHROMA_T, nullptr, RefPool{}};
-  MpaCache c = cache_of(t);
-#pragma omp parallel for schedule(static, 256)
-  for (long g = 0; g < plan.n_elems; g++) {
-    int idx;
-    const int si = find_item(plan.off.data(), plan.chunk.data(), (int)g, ns);
-    uint32_t v = dmvr_cost_thread((int)g, si, t.sc, t.geo, taps, plan.sub.data(), setups.data(), c, tab.ref, &idx);
-#pragma omp atomic
-    costs[idx] += v;
-  }
-  std::vector<mm_pu_desc> refined(ns);
-  std::vector<int32_t> mvd(2 * (size_t)ns);
-  for (int s = 0; s < ns; s++) dmvr_decide_thread(s, plan.sub.data(), costs.data(), refined.data(), mvd.data());
   if (mvd_out) std::copy(mvd.begin(), mvd.end(), mvd_out);
-  return twin_pred_list(t, tab, refined.data(), ns, dy, sdy, dcb, dcr, sdc);
+  return 0;
 }
 
-// MM-MVP (mm_mvp_convert) through the product's planner and mm_mvp.h bodies.
+// Device-planned prediction with MM-DMVR on: PUs flagged MM_PUF_DMVR in the list run the search.
+extern "C" int twin_pred_mixed(const mm_seq_params* p, int n_epi, const int32_t* epi, int cur_poc,
+                               const mm_pu_desc* pus, int n, int n_refs, const int32_t* pocs,
+                               const int16_t* const* ys, const int16_t* const* cbs, const int16_t* const* crs,
+                               int stride_y, int stride_c, int16_t* dy, int sdy, int16_t* dcb, int16_t* dcr, int sdc) {
+  using namespace mmdev;
+  Twin t;
+  make_twin(p, &t);
+  EpipoleMap em = epi_of(n_epi, epi);
+  std::vector<std::pair<int, RefDev>> refs;
+  for (int i = 0; i < n_refs; i++)
+    refs.emplace_back(pocs[i], RefDev{ys[i], cbs ? cbs[i] : nullptr, crs ? crs[i] : nullptr, stride_y, stride_c, 0u, 0u});
+  std::sort(refs.begin(), refs.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+  PicTables tab;
+  std::string err;
+  int rc = build_pic_tables(seq_info(*p), em, cur_poc, refs, &tab, &err);
+  if (rc) return rc;
+  tab.dmvr = 1;
+  return twin_pred_list(t, tab, pus, n, dy, sdy, dcb, dcr, sdc);
+}
+
+// MM-MVP (mm_mvp_convert) through the product's epipole table and mm_mvp.h bodies, query by query.
 extern "C" int twin_mvp(const mm_seq_params* p, int n_epi, const int32_t* epi, const mm_mvp_query* q, int n,
                         int32_t* out) {
   Twin t;
   make_twin(p, &t);
   EpipoleMap em = epi_of(n_epi, epi);
-  std::vector<mmmvp::MvpQueryDev> qs;
-  std::vector<M3> ged;
-  std::string err;
-  int rc = plan_mvp(seq_info(*p), em, q, n, &qs, &ged, &err);
-  if (rc) return rc;
+  std::vector<mmmvp::EpiDev> entries;
+  epi_entries(em, &entries);
+  const mmmvp::EpiTable et{entries.data(), (int)entries.size()};
+  std::vector<int> codes(n, 0);
 #pragma omp parallel for schedule(static)
-  for (int i = 0; i < n; i++) mmmvp::mvp_thread(i, t.sc, qs.data(), ged.data(), out);
+  for (int i = 0; i < n; i++) codes[i] = mmmvp::mvp_query(t.sc, q[i], p->active_models, et, out + 2 * i);
+  for (int i = 0; i < n; i++)
+    if (codes[i]) return codes[i];  // the first failing query, as the device status reports it
   return 0;
 }

@@ -30,6 +30,8 @@ def load():
                                    c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int,
                                    c_void_p]
     lib.twin_mvp.argtypes = [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p]
+    lib.twin_pred_mixed.argtypes = [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
+                                    c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int]
     lib.twin_pred_list1.argtypes = [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p,
                                     c_int]
@@ -57,7 +59,8 @@ def reproject(params, blocks, epipoles=()):
     return out[:total]
 
 
-def predict(params, cur_poc, pus, refs, W, H, epipoles=()):
+def predict(params, cur_poc, pus, refs, W, H, epipoles=(), dmvr=False):
+    """mm_pred_device twin; dmvr: mm_set_dmvr on (MM_PUF_DMVR PUs run the search)."""
     lib = load()
     pus = np.ascontiguousarray(pus)
     pocs = sorted(refs)
@@ -68,10 +71,11 @@ def predict(params, cur_poc, pus, refs, W, H, epipoles=()):
     dcr = np.zeros((H // 2, W // 2), dtype=np.int16)
     pa = np.array(pocs, dtype=np.int32)
     n_epi, ea = _epi(epipoles)
-    rc = lib.twin_pred(ctypes.addressof(params), n_epi, c_void_p(ea.ctypes.data), cur_poc, c_void_p(pus.ctypes.data),
-                       len(pus), len(pocs), c_void_p(pa.ctypes.data), ptrs[0], ptrs[1], ptrs[2], arrs[0][0].shape[1],
-                       arrs[1][0].shape[1], c_void_p(dy.ctypes.data), W, c_void_p(dcb.ctypes.data),
-                       c_void_p(dcr.ctypes.data), W // 2)
+    fn = lib.twin_pred_mixed if dmvr else lib.twin_pred
+    rc = fn(ctypes.addressof(params), n_epi, c_void_p(ea.ctypes.data), cur_poc, c_void_p(pus.ctypes.data),
+            len(pus), len(pocs), c_void_p(pa.ctypes.data), ptrs[0], ptrs[1], ptrs[2], arrs[0][0].shape[1],
+            arrs[1][0].shape[1], c_void_p(dy.ctypes.data), W, c_void_p(dcb.ctypes.data),
+            c_void_p(dcr.ctypes.data), W // 2)
     if rc:
         raise RuntimeError(f"twin predict failed: {rc}")
     return dy, dcb, dcr

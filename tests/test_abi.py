@@ -27,7 +27,7 @@ def test_library_exports_every_symbol():
 
 
 def test_version():
-    assert mm360.load_library().mm_get_version() >= 100
+    assert mm360.load_library().mm_get_version() == 300
 
 
 def test_create_without_gpu_fails_loudly():

@@ -46,3 +46,23 @@ def test_dmvr_rejects_ineligible_pus():
     bad[2]["ref_poc"][1] = -1  # uni
     with pytest.raises(RuntimeError, match="1"):
         twin.predict_dmvr(params, W.CUR_POC, bad, refs, 256, 128)
+
+
+@pytest.mark.parametrize("w,h,models,share", [(256, 128, W.MPA3, 0.5), (1024, 512, ALL, 0.3)])
+def test_twin_mixed_picture_matches_oracle(w, h, models, share):
+    """A picture list mixing MM_PUF_DMVR PUs with ordinary PUs (mm_set_dmvr): the DMVR search runs
+    inside the planned picture (placement -> search -> decision patches the sub-PUs' jobs ->
+    setup / reprojection / interpolation) == the oracle's predict + predict_dmvr."""
+    cfg = _cfg(w, h, models)
+    params = mm360.seq_params(w, h, models)
+    pus = W.pu_list(cfg, frame=1, dmvr_share=share)
+    dm = W.dmvr_flagged(pus)
+    assert dm.sum() > 5 and (~dm).sum() > 5
+    refs = {poc: W.ref_planes(w, h, poc) for poc in W.REF_POCS}
+    want = Oracle(params, EPI).predict_mixed(W.CUR_POC, pus, refs, w, h)
+    got = twin.predict(params, W.CUR_POC, pus, refs, w, h, EPI, dmvr=True)
+    for name, a, b in zip(("y", "cb", "cr"), got, want):
+        assert np.array_equal(a, b), describe_mismatch(name, a, b)
+    # without the picture's DMVR enable the flagged PUs are rejected
+    with pytest.raises(RuntimeError, match="1"):
+        twin.predict(params, W.CUR_POC, pus, refs, w, h, EPI)

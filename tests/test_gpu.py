@@ -262,6 +262,33 @@ def test_error_paths():
         with pytest.raises(mm360.MMError) as e:
             ctx.reproject(blk)  # outside the picture
         assert e.value.code == mm360.MM_ERR_ARG
+        blk = np.array([(0, 0, 256, 128, 16, 16, 1, 0, 8, 0)], dtype=mm360.BLOCK_DTYPE)
+        with pytest.raises(mm360.MMError) as e:
+            ctx.reproject(blk)  # wider than one CTU (JobDev's 8-bit block sizes)
+        assert e.value.code == mm360.MM_ERR_ARG
+
+
+def test_pu_descriptor_guards():
+    """Unknown flag bits, nonzero reserved words and MM_PUF_DMVR without mm_set_dmvr are rejected
+    (a stale 48-byte layout fails loudly); a clean descriptor still predicts."""
+    cfg = W.CONFIGS["C1"]
+    params = mm360.seq_params(cfg.width, cfg.height, cfg.models)
+    pus = W.pu_list(cfg)
+    refs = {poc: W.ref_planes(cfg.width, cfg.height, poc) for poc in W.REF_POCS}
+    with mm360.MMContext(params) as ctx:
+        for poc, (y, cb, cr) in refs.items():
+            ctx.upload_ref(poc, y, cb, cr)
+        dst = _planes(cfg)
+        for field, val in (("flags", 0x2), ("flags", mm360.PUF_DMVR), ("reserved", 1)):
+            bad = pus.copy()
+            if field == "reserved":
+                bad["reserved"][7, 1] = val
+            else:
+                bad[field][7] = val
+            with pytest.raises(mm360.MMError) as e:
+                ctx.predict(W.CUR_POC, bad, *dst)
+            assert e.value.code == mm360.MM_ERR_ARG and "PU 7" in str(e.value), (field, str(e.value))
+        ctx.predict(W.CUR_POC, pus, *dst)
 
 
 def _planes(cfg, fill=0):
@@ -592,4 +619,130 @@ def test_mvp_convert_vs_oracle():
     want = Oracle(params, EPI2).mvp(q)
     with _ctx(params, EPI2) as ctx:
         got = ctx.mvp_convert(q)
+        # device-resident form: same results, stream-ordered, no host buffers
+        d_q = mm360.queries_to_device(q)
+        d_out = torch.full((len(q), 2), -7, dtype=torch.int32, device="cuda")
+        ctx.mvp_convert_device(d_q, d_out)
+        ctx.mvp_status()
+        got_dev = d_out.cpu().numpy()
     assert np.array_equal(got, want), np.argwhere((got != want).any(axis=1))[:5]
+    assert np.array_equal(got_dev, want), np.argwhere((got_dev != want).any(axis=1))[:5]
+
+
+def test_mvp_device_errors_and_epipole_refresh():
+    """mm_mvp_convert_device: the lowest failing query's code is deferred to mvp_status; the device
+    epipole table follows later mm_set_epipole calls."""
+    from test_mvp import ALL as MVP_ALL, EPI2
+    params = mm360.seq_params(256, 128, MVP_ALL)
+    q = W.mvp_queries(256, 128, MVP_ALL, 700, seed=4)
+    q["model_orig"][300:] = mm360.GEODESIC_CAMPOSE
+    q["mv_hor"][300:] |= 1
+    with _ctx(params, []) as ctx:  # no epipoles yet
+        d_q = mm360.queries_to_device(q)
+        d_out = torch.zeros((len(q), 2), dtype=torch.int32, device="cuda")
+        ctx.mvp_convert_device(d_q, d_out)
+        with pytest.raises(mm360.MMError) as e:
+            ctx.mvp_status()
+        assert e.value.code == mm360.MM_ERR_NOEPIPOLE
+        cam = (q["model_orig"] == mm360.GEODESIC_CAMPOSE) | (q["model_desired"] == mm360.GEODESIC_CAMPOSE)
+        first = int(np.argmax(cam & ~((q["mv_hor"] == 0) & (q["mv_ver"] == 0))))
+        assert f"MVP query {first}:" in str(e.value), str(e.value)
+        for (cur, ref, qq) in EPI2:
+            ctx.set_epipole(cur, ref, qq)
+        ctx.mvp_convert_device(d_q, d_out)
+        ctx.mvp_status()
+        want = Oracle(params, EPI2).mvp(q)
+        assert np.array_equal(d_out.cpu().numpy(), want)
+        bad = q.copy()
+        bad["shift_hor"][123] = 9
+        bad["model_desired"][456] = 99
+        ctx.mvp_convert_device(mm360.queries_to_device(bad), d_out)
+        with pytest.raises(mm360.MMError) as e:
+            ctx.synchronize()
+        assert e.value.code == mm360.MM_ERR_ARG and "MVP query 123" in str(e.value)
+
+
+@pytest.mark.parametrize("plan_ahead", [False, True])
+def test_pred_device_mixed_dmvr_picture_vs_oracle(plan_ahead):
+    """A full C2 picture mixing MM_PUF_DMVR PUs (30 % of the DMVR-eligible bi leaves) with ordinary
+    PUs, predicted by ONE asynchronous mm_pred_device launch sequence with mm_set_dmvr on (search,
+    decision and refined prediction inside the picture's plan; InterPrediction.cpp:591-592,
+    2442-2634), == the oracle's predict + predict_dmvr.  Twice in a row, with and without
+    plan-ahead (the search runs on the context stream after the planning on the auxiliary one)."""
+    cfg = W.CONFIGS["C2"]
+    params = mm360.seq_params(cfg.width, cfg.height, cfg.models)
+    refs = {poc: W.ref_planes(cfg.width, cfg.height, poc) for poc in W.REF_POCS}
+    lists = [W.pu_list(cfg, frame=f, dmvr_share=0.3) for f in (0, 1)]
+    orc = Oracle(params, EPI)
+    with _ctx(params) as ctx:
+        ctx.set_dmvr(True)
+        ctx.set_plan_ahead(plan_ahead)
+        for poc, (y, cb, cr) in refs.items():
+            ctx.upload_ref(poc, torch.from_numpy(y).cuda(), torch.from_numpy(cb).cuda(), torch.from_numpy(cr).cuda())
+        d_lists = [mm360.pus_to_device(p) for p in lists]
+        outs = [_planes(cfg, fill=-1) for _ in lists]
+        torch.cuda.synchronize()  # plan-ahead contract: the lists are complete before the calls
+        for d, o in zip(d_lists, outs):
+            ctx.predict_device(W.CUR_POC, d, *o)
+        ctx.synchronize()
+        got = [[t.cpu().numpy() for t in o] for o in outs]
+    for pus, g in zip(lists, got):
+        assert W.dmvr_flagged(pus).sum() > 100
+        want = orc.predict_mixed(W.CUR_POC, pus, refs, cfg.width, cfg.height)
+        for name, a, b in zip(("y", "cb", "cr"), g, want):
+            assert np.array_equal(a, b), plane_mismatch(name, a, b)
+
+
+def test_effective_blocks_end_to_end_vs_oracle():
+    """a2 wired end to end: decoded PUs of a C2 picture (merge / mvRefine DMVR PUs, SbTMVP PUs with
+    8x8 motion fields, BDOF-split bi PUs) -> the product's mm_derive_effective_blocks -> one
+    mm_pred_device list (DMVR PUs flagged) on the GPU, against the oracle's own derivation
+    (motionCompensation restated) + predict + predict_dmvr."""
+    from oracle.oracle import effective_blocks
+    cfg = W.CONFIGS["C2"]
+    params = mm360.seq_params(cfg.width, cfg.height, cfg.models)
+    dec, tools = W.decoded_pus(cfg, frame=5, dmvr_share=0.3)
+    rng = np.random.default_rng(77)
+    fields, n_sub = [], 0
+    for p in dec:
+        u = p["pu"]
+        if p["flags"] or u["w"] < 16 or u["h"] < 16 or rng.random() > 0.2:
+            continue
+        cols, rows = int(u["w"]) // 8, int(u["h"]) // 8
+        base = mm360.new_pus(3)
+        for b in base:
+            bi = rng.random() < 0.6
+            lst = int(rng.integers(0, 2))
+            b["ref_poc"] = [W.REF_POCS[0] if (bi or lst == 0) else -1, W.REF_POCS[1] if (bi or lst == 1) else -1]
+            b["mv"] = rng.integers(-400, 400, size=(2, 2))
+            b["model"] = [int(rng.choice(cfg.models)), int(rng.choice(cfg.models))]
+        field = mm360.new_pus(cols * rows)
+        for k in range(cols * rows):  # runs of equal motion, merged into strips by xSubPuMC
+            field[k] = base[int(rng.integers(0, 3))] if (k == 0 or rng.random() < 0.4) else field[k - 1]
+        field["mv"][field["ref_poc"] < 0] = 0
+        p["flags"] = mm360.PU_SUBPU | mm360.PU_MERGE
+        p["sub_motion"] = n_sub
+        fields.append(field)
+        n_sub += len(field)
+    sub = np.concatenate(fields)
+    mc, dm = mm360.derive_effective_blocks(tools, dec, sub)
+    omc, odm = effective_blocks(tools, dec, sub, mm360.PU_DTYPE)
+    assert mc.tobytes() == omc.tobytes() and dm.tobytes() == odm.tobytes()
+    assert len(dm) > 50 and len(fields) > 50
+    flagged = dm.copy()
+    flagged["flags"] |= mm360.PUF_DMVR
+    pus = np.concatenate([mc, flagged])
+    refs = {poc: W.ref_planes(cfg.width, cfg.height, poc) for poc in W.REF_POCS}
+    orc = Oracle(params, EPI)
+    want = orc.predict(W.CUR_POC, omc, refs, cfg.width, cfg.height)
+    orc.predict_dmvr(W.CUR_POC, odm, refs, cfg.width, cfg.height, out=want)
+    with _ctx(params) as ctx:
+        ctx.set_dmvr(True)
+        for poc, (y, cb, cr) in refs.items():
+            ctx.upload_ref(poc, torch.from_numpy(y).cuda(), torch.from_numpy(cb).cuda(), torch.from_numpy(cr).cuda())
+        out = _planes(cfg, fill=-1)
+        ctx.predict_device(W.CUR_POC, mm360.pus_to_device(pus), *out)
+        ctx.synchronize()
+        got = [t.cpu().numpy() for t in out]
+    for name, a, b in zip(("y", "cb", "cr"), got, want):
+        assert np.array_equal(a, b), plane_mismatch(name, a, b)

@@ -1,4 +1,5 @@
 """Synthetic workload generator and host-side sub-PU split rules."""
+import mm360
 import numpy as np
 import pytest
 
@@ -33,3 +34,26 @@ def test_ref_planes_deterministic_10bit():
     for x, y in zip(a, b):
         assert np.array_equal(x, y) and x.dtype == np.int16 and x.min() >= 0 and x.max() <= 1023
     assert a[0].shape == (128, 256) and a[1].shape == (64, 128)
+
+
+def test_pu_lists_come_from_the_effective_block_derivation():
+    """The bench / test PU lists are the product's mm_derive_effective_blocks output on the decoded
+    PUs (InterPrediction::motionCompensation's BDOF split), equal to the oracle's own derivation;
+    with a DMVR share the merge/mvRefine PUs come out unsplit and flagged MM_PUF_DMVR."""
+    from oracle.oracle import effective_blocks
+    cfg = W.CONFIGS["C2"]
+    for share in (0.0, 0.4):
+        dec, tools = W.decoded_pus(cfg, frame=3, dmvr_share=share)
+        mc, dm = effective_blocks(tools, dec, mm360.new_pus(0), mm360.PU_DTYPE)
+        got = W.pu_list(cfg, frame=3, dmvr_share=share)
+        flag = W.dmvr_flagged(got)
+        assert got[~flag].tobytes() == mc.tobytes()
+        g = got[flag].copy()
+        g["flags"] = 0
+        assert g.tobytes() == dm.tobytes()
+        assert (len(dm) > 0) == (share > 0)
+        # every bi PU of the plain list is at most 16x16 (xSubPuBio), DMVR PUs keep their size
+        bi = (got["ref_poc"][:, 0] >= 0) & (got["ref_poc"][:, 1] >= 0)
+        assert (got["w"][bi & ~flag] <= 16).all() and (got["h"][bi & ~flag] <= 16).all()
+        if share:
+            assert (got["w"][flag] * got["h"][flag] > 256).any()

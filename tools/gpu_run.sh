@@ -21,6 +21,10 @@ for step in "$@"; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     bench_c4) run bench_c4 600 python bench.py --config C4 ;;
+    bench_dmvr) run bench_dmvr 600 python bench.py --dmvr-share 0.3 --cpu-seconds 5 ;;
+    bench_c5) run bench_c5 600 python bench.py --config C5 ;;
+    prof_dmvr) run prof_dmvr 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_dmvr -o run --output-format csv -- python3 bench.py --steps 12 --warmup 4 --no-cpu-baseline --dmvr-share 0.3 ;;
+    prof_c5) run prof_c5 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c5 -o run --output-format csv -- python3 bench.py --config C5 --steps 5 --warmup 2 --no-cpu-baseline ;;
     c4_emulate) run c4_emulate 600 python bench.py --config C4 --c4-emulate ;;
     c4_gloo2) run c4_gloo2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --dist-backend gloo --steps 6 --warmup 2 ;;
     ubench) run ubench 300 bash -c "tools/ubench/load_check && tools/ubench/valu_rate2" ;;

@@ -17,28 +17,41 @@
 // shared with the CPU twin (tests/native/host_twin.cpp), which places PUs sequentially.
 #pragma once
 #include "../../include/mm360.h"
+#include "mm_dmvr.h"
 #include "mm_pipeline.h"
 
 namespace mmdev {
 using namespace mmpipe;
+using mmdmvr::N_OFF;
+using mmdmvr::SubPuDev;
 
 constexpr int MAX_SLOTS = 16;  // reference pictures addressable by one picture (2 lists x 8)
-// PU buckets: class (bi, uni L0, uni L1) x sub-block alignment.  PUs whose sub-block count is a
-// multiple of 4 come first (buckets 0-2), so every aligned group of 4 consecutive sub-blocks
-// (a lane quad of k_mc) lies inside one PU; the rest (4x8 / 8x4 / 4x4 ...) follow (buckets 3-5).
-constexpr int N_PU_KEYS = 6;
-MM_HD int pu_key(int cls, int n_sb) { return cls + ((n_sb & 3) ? 3 : 0); }
-// class of flat luma sub-block g from the bucket bases (PlanMeta::sb_base)
-// sb_base is non-decreasing, so the last bucket starting at or before g is the number of bucket
-// starts k >= 1 at or before g: every start is read unconditionally (one batch of scalar loads in
-// k_mc, not a chain of dependent load-compare-branch steps)
-MM_HD int sb_class(int g, const int* sb_base) {
+// PU buckets: N_PU_KEYS horizontal bins of the picture, by the PU's top row.  Inside a bin the PUs
+// keep the list's (decode) order, so the sub-block enumeration k_mc reads is spatial.  k_plan_place
+// cuts the bins into N_BANDS bands of about equal sub-block counts (PlanMeta::band), and k_mc runs
+// band r on the workgroups that share one XCD (mm_kernels.hip k_mc_dev): the reference windows of
+// neighbouring PUs -- which overlap by the MV spread plus the filter reach -- are fetched into that
+// XCD's L2 once, instead of once per XCD and per PU class.  k_mc handles bi and uni sub-blocks in
+// one body (the McRec meta word says which lists a sub-block uses), so no class buckets are needed.
+// The cut balances bands also for a stripe of the picture (mm360/parallel.py shards by CTU rows).
+constexpr int N_PU_KEYS = 64;
+constexpr int N_BANDS = 8;
+MM_HD int pu_key(int y, int H) { return (int)(((long)y * N_PU_KEYS) / H); }
+
+// Band cut of the bins: band r = sub-blocks [band[r], band[r + 1]), bin boundaries at the nearest
+// bin start at or after r / N_BANDS of the sub-blocks (one thread; sb_base = the bins' starts).
+MM_HD void band_cut(const int* sb_base, int n_sb, int* band) {
   int k = 0;
-#pragma unroll
-  for (int i = 1; i < N_PU_KEYS; i++) k += g >= sb_base[i] ? 1 : 0;
-  return k % 3;
+  band[0] = 0;
+  for (int r = 1; r < N_BANDS; r++) {
+    const long target = (long)n_sb * r / N_BANDS;
+    while (k < N_PU_KEYS && sb_base[k] < target) k++;
+    band[r] = k < N_PU_KEYS ? sb_base[k] : n_sb;
+  }
+  band[N_BANDS] = n_sb;
 }
 constexpr int N_JOB_KEYS = 64;
+constexpr int DMVR_KEY = N_PU_KEYS + N_JOB_KEYS;  // one bucket of MM-DMVR sub-PUs after the PU and job keys
 
 // Per-picture constant tables, passed by value as kernel arguments.
 struct PicTables {
@@ -51,6 +64,7 @@ struct PicTables {
   uint32_t active;
   int nf_mod4;             // (W/4 * H/4) % 4, frame-cache packet tail (MPA chroma aliasing)
   int only_list;           // -1: normal prediction; 0/1: mm_pred_list of that list (other list ignored)
+  int dmvr;                // MM_PUF_DMVR PUs allowed (mm_set_dmvr: the picture's DMVR enable)
   RefPool pool;            // the context's reference pool (device interior filters)
 };
 
@@ -59,6 +73,8 @@ struct PlanMeta {
   int n_pus, n_sb, n_jobs, n_elems;
   int pu_base[N_PU_KEYS], sb_base[N_PU_KEYS];
   int job_base[N_JOB_KEYS], elem_base[N_JOB_KEYS];
+  int n_sub, n_dmvr_elems;  // MM-DMVR sub-PU records and their cost elements (N_OFF * n each)
+  int band[N_BANDS + 1];    // k_mc's bands of the sub-block enumeration (band_cut)
 };
 
 // Host-side bucket counters of the sequential planners (CPU twin).  64-bit words pack
@@ -66,6 +82,7 @@ struct PlanMeta {
 struct PlanCounters {
   unsigned long long pu_tot[N_PU_KEYS], pu_cur[N_PU_KEYS];
   unsigned long long job_tot[N_JOB_KEYS], job_cur[N_JOB_KEYS];
+  unsigned long long dmvr_tot, dmvr_cur;
 };
 
 struct JobPlan {
@@ -76,11 +93,15 @@ struct PuPlan {
   int code;     // MM_OK or the error this PU raises
   int cls;      // 0 bi, 1 uni L0, 2 uni L1
   int key;      // PU bucket (pu_key)
-  int n_sb;     // luma 4x4 sub-blocks
+  int n_sb;     // luma 4x4 sub-blocks (of the whole PU)
   int slot[2];
   int bcw;      // BCW weight index (bi), MM_BCW_DEFAULT otherwise
-  JobPlan job[4];   // [2 * list + comp]; fixed slots keep the struct in registers
+  JobPlan job[4];   // [2 * list + comp]; fixed slots keep the struct in registers (per sub-PU for DMVR)
   int alias[2]; // list's chroma job aliases its luma job
+  // MM_PUF_DMVR: the PU is placed as n_items = sx * sy sub-PUs of sub_w x sub_h luma samples
+  // (xProcessDMVRProjected, InterPrediction.cpp:2452-2486: min(w, 16) x min(h, 16)), each one bi PU
+  // bucket item with its own jobs and one DMVR record; n_items = 1 otherwise
+  int dmvr, n_items, sub_w, sub_h, sx;
 };
 
 MM_HD int job_key(int comp, int model, int n) { return (comp * 16 + model) * 2 + (n < 4 ? 1 : 0); }
@@ -111,10 +132,35 @@ MM_HD void classify_pu(const mm_pu_desc& u, const PicTables& t, PuPlan* p) {
   p->slot[0] = p->slot[1] = -1;
   p->alias[0] = p->alias[1] = 0;
   p->bcw = MM_BCW_DEFAULT;
+  p->dmvr = 0;
+  p->n_items = 1;
+  p->sub_w = u.w;
+  p->sub_h = u.h;
+  p->sx = 1;
   if (u.w < 4 || u.h < 4 || u.w > 128 || u.h > 128 || (u.w & 3) || (u.h & 3) || (u.x & 3) || (u.y & 3) || u.x < 0 ||
       u.y < 0 || u.x > t.W - u.w || u.y > t.H - u.h) {
     p->code = MM_ERR_ARG;
     return;
+  }
+  // unknown flag bits and nonzero reserved words (a stale 48-byte descriptor layout) fail loudly
+  if (u.reserved[0] | u.reserved[1] | (int)(u.flags & ~MM_PUF_DMVR) | (int)((u.flags & MM_PUF_DMVR) && !t.dmvr)) {
+    p->code = MM_ERR_ARG;
+    return;
+  }
+  if (u.flags & MM_PUF_DMVR) {
+    // the parts of PU::checkDMVRCondition (UnitTools.cpp:1698-1726) the descriptor carries: bi, equal
+    // models, BCW_DEFAULT, w, h >= 8, w * h >= 128; sub-PUs tile the PU (16-multiples beyond 16)
+    if (u.w < 8 || u.h < 8 || u.w * u.h < 128 || (u.w > 16 && (u.w & 15)) || (u.h > 16 && (u.h & 15)) ||
+        u.ref_poc[0] < 0 || u.ref_poc[1] < 0 || u.model[0] != u.model[1] || u.bcw_idx != MM_BCW_DEFAULT ||
+        t.only_list >= 0) {
+      p->code = MM_ERR_ARG;
+      return;
+    }
+    p->dmvr = 1;
+    p->sub_w = u.w < 16 ? u.w : 16;
+    p->sub_h = u.h < 16 ? u.h : 16;
+    p->sx = u.w / p->sub_w;
+    p->n_items = p->sx * (u.h / p->sub_h);
   }
   // mm_pred_list: the PU must use the list (selects, not an index: a runtime index into `u` would
   // demote the descriptor from registers to LDS)
@@ -153,15 +199,15 @@ MM_HD void classify_pu(const mm_pu_desc& u, const PicTables& t, PuPlan* p) {
 #pragma unroll
     for (int comp = 0; comp < 2; comp++) {
       if (comp == 1 && !t.chroma) continue;
-      if (comp == 1 && mpa_chroma_aliases(t, m, u.w, u.h)) {
+      if (comp == 1 && mpa_chroma_aliases(t, m, p->sub_w, p->sub_h)) {
         p->alias[l] = 1;
         continue;
       }
       const int sb = comp ? 2 : 4;
       JobPlan& j = p->job[2 * l + comp];
       j.valid = 1;
-      j.cw = u.w >> comp;
-      j.ch = u.h >> comp;
+      j.cw = p->sub_w >> comp;
+      j.ch = p->sub_h >> comp;
       j.rows = j.ch / sb;
       j.n = (j.cw / sb) * j.rows;
       j.comp = comp;
@@ -186,8 +232,9 @@ MM_HD void classify_pu(const mm_pu_desc& u, const PicTables& t, PuPlan* p) {
     p->bcw = u.bcw_idx;
   }
   p->n_sb = (u.w / 4) * (u.h / 4);
-  p->key = pu_key(p->cls, p->n_sb);
+  p->key = pu_key(u.y, t.H);
 }
+
 
 MM_HD unsigned long long status_word(int pu_index, int code) {
   return ~(((unsigned long long)(unsigned)pu_index << 8) | (unsigned)code);  // atomicMax keeps the lowest PU
@@ -198,6 +245,14 @@ MM_HD unsigned long long pack_count(int items, int elems) {
 }
 MM_HD int packed_items(unsigned long long v) { return (int)(v & 0xffffffffull); }
 MM_HD int packed_elems(unsigned long long v) { return (int)(v >> 32); }
+
+// The bucket counts one classified PU adds: (items, elements) of its PU bucket, of each job key, and
+// of the DMVR bucket (sub-PU records, cost elements)
+MM_HD unsigned long long pu_count(const PuPlan& p) { return pack_count(p.n_items, p.n_sb); }
+MM_HD unsigned long long job_count(const PuPlan& p, int k) { return pack_count(p.n_items, p.n_items * p.job[k].n); }
+MM_HD unsigned long long dmvr_count(const PuPlan& p) {
+  return pack_count(p.n_items, p.n_items * N_OFF * (p.sub_w / 4) * (p.sub_h / 4));
+}
 
 // Exclusive prefix of the bucket totals -> PlanMeta (one thread).
 MM_HD void plan_meta(const PlanCounters& c, PlanMeta* m) {
@@ -210,6 +265,7 @@ MM_HD void plan_meta(const PlanCounters& c, PlanMeta* m) {
   }
   m->n_pus = acc;
   m->n_sb = sacc;
+  band_cut(m->sb_base, m->n_sb, m->band);
   acc = sacc = 0;
   for (int k = 0; k < N_JOB_KEYS; k++) {
     m->job_base[k] = acc;
@@ -219,6 +275,8 @@ MM_HD void plan_meta(const PlanCounters& c, PlanMeta* m) {
   }
   m->n_jobs = acc;
   m->n_elems = sacc;
+  m->n_sub = packed_items(c.dmvr_tot);
+  m->n_dmvr_elems = packed_elems(c.dmvr_tot);
 }
 
 // Item `idx` covers flat elements [off, off + n): it starts every 64-element chunk whose first
@@ -230,35 +288,69 @@ MM_HD void write_chunks(int* chunk, int idx, int off, int n) {
 // Emit the jobs of the PU placed at luma sub-block offset sb_off; job_idx/job_elem_off are the
 // placed positions of the valid p.job[k].  The PU itself needs no record: its luma job of the
 // first used list writes the per-sub-block meta word k_mc reads (JobDev::meta_hi).
+// An MM_PUF_DMVR PU is emitted as its p.n_items sub-PUs in raster order (InterPrediction.cpp:
+// 2481-2484): sub-PU s takes job job_idx[k] + s of every key, its sub-blocks follow sub-PU s - 1's,
+// and its DMVR record (merge MVs, the indices of its jobs) goes to sub_idx + s, with its cost
+// elements at sub_elem_off + s * N_OFF * n.
 MM_HD void emit_pu(const mm_pu_desc& u, const PuPlan& p, int sb_off, const int* job_idx, const int* job_elem_off,
-                   JobDev* jobs, int* job_off, int* job_chunk) {
+                   JobDev* jobs, int* job_off, int* job_chunk, int sub_idx = 0, int sub_elem_off = 0,
+                   SubPuDev* subs = nullptr, int* sub_off = nullptr, int* sub_chunk = nullptr) {
   const int primary = p.cls == 2 ? 1 : 0;
-  const int meta_hi = (p.slot[0] < 0 ? 0 : p.slot[0]) | ((p.slot[1] < 0 ? 0 : p.slot[1]) << 4) | (p.bcw << 8);
-  for (int i = 0; i < 4; i++) {
-    const JobPlan& jp = p.job[i];
-    if (!jp.valid) continue;
-    JobDev j;
-    j.x = u.x;
-    j.y = u.y;
-    j.cw = jp.cw;
-    j.ch = jp.ch;
-    j.comp = jp.comp;
-    j.model = jp.model;
-    j.mv_hor = jp.mv_hor;
-    j.mv_ver = jp.mv_ver;
-    j.ged_idx = jp.ged_idx;
-    j.n = jp.n;
-    j.rows = jp.rows;
-    j.offset = job_elem_off[i];
-    j.sb_base = sb_off;
-    j.pu_cols = u.w / 4;
-    j.list = jp.list;
-    j.slot = p.slot[jp.list];
-    j.alias = jp.comp == 0 ? p.alias[jp.list] : 0;
-    j.meta_hi = meta_hi | ((jp.comp == 0 && jp.list == primary) ? MM_META_PRIMARY : 0);
-    jobs[job_idx[i]] = j;
-    job_off[job_idx[i]] = job_elem_off[i];
-    write_chunks(job_chunk, job_idx[i], job_elem_off[i], jp.n);
+  const int meta_hi = (p.slot[0] < 0 ? 0 : p.slot[0]) | ((p.slot[1] < 0 ? 0 : p.slot[1]) << 4) | (p.bcw << 8) |
+                      (p.slot[0] >= 0 ? MM_META_USE0 : 0) | (p.slot[1] >= 0 ? MM_META_USE1 : 0);
+  const int n_sb_sub = (p.sub_w / 4) * (p.sub_h / 4);
+  for (int s = 0; s < p.n_items; s++) {
+    const int x = u.x + (s % p.sx) * p.sub_w, y = u.y + (s / p.sx) * p.sub_h;
+    int jk[4] = {-1, -1, -1, -1};
+    for (int i = 0; i < 4; i++) {
+      const JobPlan& jp = p.job[i];
+      if (!jp.valid) continue;
+      JobDev j;
+      j.x = x;
+      j.y = y;
+      j.cw = jp.cw;
+      j.ch = jp.ch;
+      j.comp = jp.comp;
+      j.model = jp.model;
+      j.mv_hor = jp.mv_hor;
+      j.mv_ver = jp.mv_ver;
+      j.ged_idx = jp.ged_idx;
+      j.n = jp.n;
+      j.rows = jp.rows;
+      j.offset = job_elem_off[i] + s * jp.n;
+      j.sb_base = sb_off + s * n_sb_sub;
+      j.pu_cols = p.sub_w / 4;
+      j.list = jp.list;
+      j.slot = p.slot[jp.list];
+      j.alias = jp.comp == 0 ? p.alias[jp.list] : 0;
+      j.meta_hi = meta_hi | ((jp.comp == 0 && jp.list == primary) ? MM_META_PRIMARY : 0);
+      jk[i] = job_idx[i] + s;
+      jobs[jk[i]] = j;
+      job_off[jk[i]] = j.offset;
+      write_chunks(job_chunk, jk[i], j.offset, jp.n);
+    }
+    if (p.dmvr) {
+      SubPuDev d;
+      d.x = x;
+      d.y = y;
+      d.w = p.sub_w;
+      d.h = p.sub_h;
+      for (int l = 0; l < 2; l++) {
+        d.mv[l][0] = u.mv[l][0];
+        d.mv[l][1] = u.mv[l][1];
+        d.ref_poc[l] = u.ref_poc[l];
+        d.slot[l] = p.slot[l];
+        d.ged_idx[l] = p.job[2 * l].ged_idx;
+      }
+      d.model = u.model[0];
+      d.n = n_sb_sub;
+      d.rows = p.sub_h / 4;
+      d.elem_off = sub_elem_off + s * N_OFF * n_sb_sub;
+      for (int k = 0; k < 4; k++) d.jidx[k] = jk[k];
+      subs[sub_idx + s] = d;
+      sub_off[sub_idx + s] = d.elem_off;
+      write_chunks(sub_chunk, sub_idx + s, d.elem_off, N_OFF * n_sb_sub);
+    }
   }
 }
 

@@ -11,8 +11,11 @@
 //   3. parabolic sub-pel refinement from the 5 costs around the best offset unless it lies on the
 //      window border (xDMVRSubPixelErrorSurface :2157-2175, xSubPelErrorSrfc :1996-2048);
 //   4. the sub-PU is predicted as a bi PU at merge0 + mvd / merge1 - mvd (all components, addAvg).
-// Steps 1-3 run here (k_dmvr_setup, k_dmvr_cost, k_dmvr_decide); step 4 is the ordinary
-// device-planned prediction path run on the refined sub-PU list.
+// Steps 1-3 run here (k_dmvr_setup, k_dmvr_cost, k_dmvr_decide) inside the picture's device-planned
+// launch sequence: the planner (mm_devplan.h) places every sub-PU of an MM_PUF_DMVR PU as a bi PU
+// with its reprojection jobs and a SubPuDev record pointing at them, the search runs on the
+// records, and k_dmvr_decide writes the refined MVs into those jobs before k_setup reads them --
+// step 4 is then the ordinary setup / reprojection / interpolation of the picture.
 #pragma once
 #include "../../include/mm360.h"
 #include "mm_pipeline.h"
@@ -31,6 +34,7 @@ struct SubPuDev {
   int model;           // both lists (checkDMVRCondition: equal models)
   int n, rows;         // luma 4x4 sub-blocks, Eigen rows
   int elem_off;        // first cost element: N_OFF * n per sub-PU
+  int jidx[4];         // the sub-PU's reprojection jobs [2 * list + comp] in the picture plan (-1: none)
 };
 
 // m_pSearchOffset[i] = (i % 5 - 2, i / 5 - 2)
@@ -68,11 +72,18 @@ MM_HD uint32_t dmvr_cost_thread(int g, int si, const SeqConst& sc, const Geometr
     py = cache.py[pl][ci];
     vip = cache.vip[pl][ci] != 0;
   }
+  const bool packet = packet_lane(e, u.n);
+  V3 pg;
+  const V3* pgp = nullptr;
+  if (!mpa && cache.trig_col) {
+    pg = grid_sphere(cache, (u.x >> 2) + col, (u.y >> 2) + row, packet);
+    pgp = &pg;
+  }
   int16_t p[2][16];
 #pragma unroll
   for (int l = 0; l < 2; l++) {
     int32_t fx, fy;
-    reproject_element(sc, setups[(si * N_OFF + o) * 2 + l], gx, gy, packet_lane(e, u.n), mpa, px, py, vip, 0, &fx, &fy);
+    reproject_element(sc, setups[(si * N_OFF + o) * 2 + l], gx, gy, packet, mpa, px, py, vip, 0, &fx, &fy, pgp);
     const int xPos = fx >> 4, yPos = fy >> 4, xFrac = fx & 15, yFrac = fy & 15;
     const RefDev r = refs[u.slot[l]];
     if (sb_out_of_range(xPos, yPos, geo.W, geo.H, geo.maxCUw, geo.maxCUh, 4, 4)) {
@@ -144,10 +155,8 @@ MM_HD int clip_mv_storage(int v) {  // Mv::clipToStorageBitDepth, MV_BITS = 18
   return v < lo ? lo : (v > hi ? hi : v);
 }
 
-// thread per sub-PU: the refinement decision and the refined bi descriptor
-MM_HD void dmvr_decide_thread(int s, const SubPuDev* sp, const uint32_t* costs, mm_pu_desc* out, int32_t* mvd) {
-  const SubPuDev& u = sp[s];
-  const uint32_t* c = costs + (size_t)s * N_OFF;
+// The refinement decision of one sub-PU from its 25 costs: the total L0 delta (1/16 luma)
+MM_HD void dmvr_decide(const SubPuDev& u, const uint32_t* c, int* tdx_out, int* tdy_out) {
   unsigned long long sad[N_OFF];
   for (int i = 0; i < N_OFF; i++) sad[i] = c[i];
   int tdx = 0, tdy = 0;  // total delta, 1/16
@@ -170,22 +179,28 @@ MM_HD void dmvr_decide_thread(int s, const SubPuDev* sp, const uint32_t* costs, 
       tdy += d[1];
     }
   }
-  mm_pu_desc& o = out[s];
-  o.x = u.x;
-  o.y = u.y;
-  o.w = u.w;
-  o.h = u.h;
-  o.mv[0][0] = clip_mv_storage(u.mv[0][0] + tdx);
-  o.mv[0][1] = clip_mv_storage(u.mv[0][1] + tdy);
-  o.mv[1][0] = clip_mv_storage(u.mv[1][0] - tdx);
-  o.mv[1][1] = clip_mv_storage(u.mv[1][1] - tdy);
-  o.ref_poc[0] = u.ref_poc[0];
-  o.ref_poc[1] = u.ref_poc[1];
-  o.model[0] = o.model[1] = u.model;
-  o.bcw_idx = MM_BCW_DEFAULT;  // PU::checkDMVRCondition requires BCW_DEFAULT (UnitTools.cpp:1698-1726)
-  o.reserved[0] = o.reserved[1] = o.reserved[2] = 0;
-  mvd[2 * s] = tdx;
-  mvd[2 * s + 1] = tdy;
+  *tdx_out = tdx;
+  *tdy_out = tdy;
+}
+
+// thread per sub-PU: the decision, and the refined MVs (merge0 + delta, merge1 - delta, clipped to
+// the MV storage range as pu.mvdL0SubPu is applied) written into the sub-PU's planned jobs, which
+// k_setup reads next.  mvd (optional): the delta per sub-PU.
+MM_HD void dmvr_decide_jobs_thread(int s, const SubPuDev* sp, const uint32_t* costs, JobDev* jobs, int32_t* mvd) {
+  const SubPuDev& u = sp[s];
+  int tdx, tdy;
+  dmvr_decide(u, costs + (size_t)s * N_OFF, &tdx, &tdy);
+  for (int k = 0; k < 4; k++) {
+    if (u.jidx[k] < 0) continue;
+    const int l = k >> 1, sg = l ? -1 : 1;
+    JobDev& j = jobs[u.jidx[k]];
+    j.mv_hor = clip_mv_storage(u.mv[l][0] + sg * tdx);
+    j.mv_ver = clip_mv_storage(u.mv[l][1] + sg * tdy);
+  }
+  if (mvd) {
+    mvd[2 * s] = tdx;
+    mvd[2 * s + 1] = tdy;
+  }
 }
 
 }  // namespace mmdmvr

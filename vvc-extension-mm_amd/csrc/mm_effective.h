@@ -111,7 +111,8 @@ class Deriver {
   // mergeType == DEFAULT_N branch: xCheckIdenticalMotion, else xPredInterBi (DMVR inside)
   void leaf(const mm_pu_desc& d, bool dmvr) {
     mm_pu_desc o = d;
-    o.reserved[0] = o.reserved[1] = o.reserved[2] = 0;
+    o.flags = 0;
+    o.reserved[0] = o.reserved[1] = 0;
     if (is_bi(d) && !t_.wp_bi && d.ref_poc[0] == d.ref_poc[1] && d.mv[0][0] == d.mv[1][0] &&
         d.mv[0][1] == d.mv[1][1]) {
       o.ref_poc[1] = -1;  // xPredInterUni(pu, REF_PIC_LIST_0, ..., bi = false)

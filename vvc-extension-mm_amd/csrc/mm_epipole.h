@@ -41,7 +41,10 @@ class EpipoleList {
   EpipoleList() { add({0, 0, 0}, -1, -1, false); }
 
   // addEpipole (EpipoleList.cpp:8-11): insert or replace; the caller converts to Q24
-  void add(const Q3& q, int cur, int ref, bool make_available) { m_[{cur, ref}] = Entry{q, make_available}; }
+  void add(const Q3& q, int cur, int ref, bool make_available) {
+    m_[{cur, ref}] = Entry{q, make_available};
+    version_++;
+  }
 
   // findEpipoleFixed (EpipoleList.cpp:19-36): (cur, ref), then (cur, -1), then (-1, -1), available
   // entries only; false where the reference CHECKs "No epipole for given (curPOC, refPOC)"
@@ -67,6 +70,7 @@ class EpipoleList {
   void make_available(int cur) {
     for (auto& kv : m_)
       if (kv.first.first == cur) kv.second.available = true;
+    version_++;
   }
 
   // count() (EpipoleList.h:21-24): entries, not counting a zero global epipole
@@ -112,9 +116,12 @@ class EpipoleList {
   }
 
   const std::map<std::pair<int, int>, Entry>& entries() const { return m_; }
+  // bumped by every change (a device copy of the list is refreshed when it moves)
+  unsigned long long version() const { return version_; }
 
  private:
   std::map<std::pair<int, int>, Entry> m_;
+  unsigned long long version_ = 0;
 };
 
 }  // namespace mmepi

@@ -33,7 +33,7 @@
 
 using namespace mmpipe;
 
-#define MM_VERSION 200
+#define MM_VERSION 300
 
 namespace {
 
@@ -45,6 +45,12 @@ __global__ void k_mpa_cache(SeqConst sc, int plane, int cols, int rows, float* p
   int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= cols * rows) return;
   mpa_cache_thread(t, sc, plane, cols, rows, px, py, vip);
+}
+
+__global__ void k_erp_trig(SeqConst sc, int cols, int rows, float* col, float* row) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 2 * (cols + rows)) return;
+  erp_trig_thread(t, sc, cols, rows, col, row);
 }
 
 __global__ void k_setup(SeqConst sc, const JobDev* __restrict__ jobs, int n_jobs, const M3* __restrict__ ged,
@@ -74,6 +80,14 @@ using namespace mmdev;
 // Buffer capacities of the device plan (the host sizes them; k_plan_place enforces them).
 struct PlanCaps {
   int pus, sb, jobs, elems;
+  int subs, dmvr_elems;  // MM-DMVR sub-PU records and cost elements (0 unless DMVR is enabled)
+};
+// Where k_plan_place puts the MM-DMVR sub-PU records (mm_dmvr.h SubPuDev), their cost-element
+// offsets and the 64-element chunk starts of those elements.
+struct DmvrRecs {
+  SubPuDev* sub;
+  int* off;
+  int* chunk;
 };
 
 // Workgroups are dispatched round-robin over the 8 XCDs, each with its own L2.  Within every
@@ -100,7 +114,7 @@ __device__ __forceinline__ int xcd_block() {
 constexpr int PLAN_BLOCK = 1024;
 constexpr int PLACE_BLOCK = 256;
 constexpr int PLAN_Q = PLAN_BLOCK / PLACE_BLOCK;  // quarters per count block
-constexpr int N_KEYS = N_PU_KEYS + N_JOB_KEYS;    // one row of `blk`: PU buckets, then job buckets
+constexpr int N_KEYS = DMVR_KEY + 1;  // one row of `blk`: PU buckets, job buckets, the DMVR bucket
 
 // status: the picture's validation word (0 = ok, else ~((pu_index << 8) | code) of the lowest
 // failing PU, combined with atomicMax over every stripe of the picture).
@@ -121,10 +135,11 @@ __global__ void __launch_bounds__(PLAN_BLOCK) k_plan_count(const mm_pu_desc* __r
     if (p.code != MM_OK) {
       atomicMax(&s_status, status_word(pu_base + i, p.code));
     } else {
-      atomicAdd(&s_cnt[q][p.key], pack_count(1, p.n_sb));
+      atomicAdd(&s_cnt[q][p.key], pu_count(p));
 #pragma unroll
       for (int k = 0; k < 4; k++)
-        if (p.job[k].valid) atomicAdd(&s_cnt[q][N_PU_KEYS + p.job[k].key], pack_count(1, p.job[k].n));
+        if (p.job[k].valid) atomicAdd(&s_cnt[q][N_PU_KEYS + p.job[k].key], job_count(p, k));
+      if (p.dmvr) atomicAdd(&s_cnt[q][DMVR_KEY], dmvr_count(p));
     }
   }
   __syncthreads();
@@ -150,9 +165,9 @@ __global__ void __launch_bounds__(PLACE_BLOCK) k_plan_place(const mm_pu_desc* __
                                                      const unsigned long long* __restrict__ blkq,
                                                     PlanMeta* __restrict__ meta, PlanCaps caps,
                                                     JobDev* __restrict__ jobs, int* __restrict__ job_off,
-                                                    int* __restrict__ job_chunk) {
+                                                    int* __restrict__ job_chunk, DmvrRecs dm) {
   __shared__ unsigned long long s_pu[N_PU_KEYS], s_job[N_JOB_KEYS];
-  __shared__ unsigned long long g_pu[N_PU_KEYS], g_job[N_JOB_KEYS];
+  __shared__ unsigned long long g_pu[N_PU_KEYS], g_job[N_JOB_KEYS], g_dm;
   __shared__ PlanMeta s_meta;
   __shared__ int s_ok;
   const int tid = threadIdx.x;
@@ -194,8 +209,10 @@ __global__ void __launch_bounds__(PLACE_BLOCK) k_plan_place(const mm_pu_desc* __
     }
     if (tid < N_PU_KEYS)
       g_pu[tid] = pre;
-    else
+    else if (tid < DMVR_KEY)
       g_job[tid - N_PU_KEYS] = pre;
+    else
+      g_dm = pre;
   }
   // PlanMeta = exclusive prefix of the bucket totals: the job buckets are one wave (lanes 6..69
   // are threads N_PU_KEYS..N_KEYS-1, scanned in two waves' halves through LDS), the PU buckets
@@ -233,16 +250,19 @@ __global__ void __launch_bounds__(PLACE_BLOCK) k_plan_place(const mm_pu_desc* __
       }
       s_meta.n_pus = acc;
       s_meta.n_sb = sacc;
+      band_cut(s_meta.sb_base, sacc, s_meta.band);
+      s_meta.n_sub = packed_items(s_tot[DMVR_KEY]);
+      s_meta.n_dmvr_elems = packed_elems(s_tot[DMVR_KEY]);
     }
   }
   __syncthreads();
   if (tid == 0) {
     s_ok = s_meta.n_pus <= caps.pus && s_meta.n_sb <= caps.sb && s_meta.n_jobs <= caps.jobs &&
-           s_meta.n_elems <= caps.elems;
+           s_meta.n_elems <= caps.elems && s_meta.n_sub <= caps.subs && s_meta.n_dmvr_elems <= caps.dmvr_elems;
     if (blockIdx.x == 0) {
       PlanMeta m = s_meta;
       if (!s_ok) {  // over capacity (overlapping PUs): nothing is predicted, the call fails
-        m.n_pus = m.n_sb = m.n_jobs = m.n_elems = 0;
+        m.n_pus = m.n_sb = m.n_jobs = m.n_elems = m.n_sub = m.n_dmvr_elems = 0;
         atomicMax(status, status_word(0, MM_ERR_ARG));
       }
       *meta = m;
@@ -254,16 +274,34 @@ __global__ void __launch_bounds__(PLACE_BLOCK) k_plan_place(const mm_pu_desc* __
   PuPlan p;
   p.code = MM_ERR_ARG;
   mm_pu_desc u;
-  unsigned long long lp = 0, lj[4] = {0, 0, 0, 0};
+  unsigned long long lp = 0, lj[4] = {0, 0, 0, 0}, ld = 0;
   if (i < n) {
     u = pus[i];
     classify_pu(u, t, &p);
     if (p.code == MM_OK) {
-      lp = atomicAdd(&s_pu[p.key], pack_count(1, p.n_sb));
+      lp = atomicAdd(&s_pu[p.key], pu_count(p));
 #pragma unroll
       for (int k = 0; k < 4; k++)
-        if (p.job[k].valid) lj[k] = atomicAdd(&s_job[p.job[k].key], pack_count(1, p.job[k].n));
+        if (p.job[k].valid) lj[k] = atomicAdd(&s_job[p.job[k].key], job_count(p, k));
     }
+  }
+  // DMVR sub-PUs are placed in list order (an exclusive scan over the block, not LDS-atomic arrival
+  // order): mm_pred_dmvr returns their refined deltas PU after PU
+  {
+    __shared__ unsigned long long s_wsum[PLACE_BLOCK / 64];
+    const unsigned long long v = (p.code == MM_OK && p.dmvr) ? dmvr_count(p) : 0ull;
+    const int lane = tid & 63, w = tid >> 6;
+    unsigned long long incl = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const unsigned long long u = __shfl_up(incl, d);
+      if (lane >= d) incl += u;
+    }
+    if (lane == 63) s_wsum[w] = incl;
+    __syncthreads();
+    unsigned long long before = 0;
+    for (int k = 0; k < w; k++) before += s_wsum[k];
+    ld = before + incl - v;
   }
   if (p.code != MM_OK) return;
   const unsigned long long bp = g_pu[p.key] + lp;
@@ -279,7 +317,9 @@ __global__ void __launch_bounds__(PLACE_BLOCK) k_plan_place(const mm_pu_desc* __
       joff[k] = s_meta.elem_base[key] + packed_elems(bj);
     }
   }
-  emit_pu(u, p, sb_off, jidx, joff, jobs, job_off, job_chunk);
+  const unsigned long long bd = g_dm + ld;
+  emit_pu(u, p, sb_off, jidx, joff, jobs, job_off, job_chunk, packed_items(bd), packed_elems(bd), dm.sub, dm.off,
+          dm.chunk);
 }
 
 // The 256 setups of a block are contiguous in `out`: each thread builds its BlockSetup in LDS and
@@ -319,28 +359,39 @@ __global__ void __launch_bounds__(256) k_reproj_dev(SeqConst sc, const PlanMeta*
 // its own phase, and from __constant__ memory those lookups are ~16 vector loads per wave that
 // compete with the reference-window loads for the texture-address path.
 // amdgpu_waves_per_eu(4): 126 VGPRs without spills, 4 waves per SIMD (130 VGPRs -> 3 otherwise)
+//
+// Band-per-XCD mapping: the sub-blocks are enumerated bin by bin in picture order and cut into
+// N_BANDS = 8 bands of about equal size (mm_devplan.h band_cut).  Workgroup b predicts band b % 8 --
+// workgroups b and b + 8 share an XCD under the round-robin dealing (MI355X_MICROARCH.md, workgroup
+// dispatch; speed only, results do not depend on it) -- looping over the band's 256-sub-block
+// blocks b / 8, b / 8 + gridDim / 8, ..., so each XCD walks one band of the picture in decode order
+// and keeps the reference rows that the band's neighbouring PUs share in its own L2.  Every
+// workgroup stages the tap tables and the reference table in LDS once for all its blocks.
+static_assert(N_BANDS == 8, "one band per XCD");
 template <bool UNI_HP>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_mc_dev(Geometry geo, const PlanMeta* __restrict__ meta, McRec mc,
                                                 const PicTables t, int16_t* __restrict__ dst_y, int dsy,
                                                 int16_t* __restrict__ dst_cb, int16_t* __restrict__ dst_cr, int dsc) {
-  const int g = xcd_block() * blockDim.x + threadIdx.x;
-  const int n_sb = meta->n_sb;
+  const int band = blockIdx.x & 7, stride = (int)(gridDim.x >> 3) * 256;
+  const int b0 = meta->band[band], b1 = meta->band[band + 1];
   __shared__ PackedTaps s_taps;
   __shared__ RefDev s_ref[MAX_SLOTS];
   static_assert(sizeof(PackedTaps) % 16 == 0 && sizeof(PackedTaps) / 16 <= 256, "one 16-byte word per thread");
   static_assert(sizeof(s_ref) % 8 == 0 && sizeof(s_ref) / 8 <= 256, "one 8-byte word per thread");
-  if (g - (int)threadIdx.x >= n_sb) return;  // whole workgroup past the end
+  const int first = b0 + (int)(blockIdx.x >> 3) * 256;
+  if (first >= b1) return;  // whole workgroup past the band's end
   if (threadIdx.x < sizeof(PackedTaps) / 16)
     reinterpret_cast<uint4*>(&s_taps)[threadIdx.x] = reinterpret_cast<const uint4*>(&c_packed_taps)[threadIdx.x];
   if (threadIdx.x < sizeof(s_ref) / 8)
     reinterpret_cast<uint2*>(s_ref)[threadIdx.x] = reinterpret_cast<const uint2*>(t.ref)[threadIdx.x];
   __syncthreads();
   const Taps taps{c_luma_taps, c_chroma_taps, &s_taps, t.pool};
-  if (g >= n_sb) return;
   // s_ref: each lane looks its slots' pool offsets up in LDS; indexing the kernel-argument copy
   // per lane was a dependent global load between the record loads and the window loads
-  mc_thread_rec<UNI_HP>(g, sb_class(g, meta->sb_base), geo, taps, mc, s_ref, dst_y, dsy, dst_cb, dst_cr, dsc);
+  for (int g = first + (int)threadIdx.x; g - (int)threadIdx.x < b1; g += stride)
+    if (g < b1) mc_thread_rec<UNI_HP>(g, geo, taps, mc, s_ref, dst_y, dsy, dst_cb, dst_cr, dsc);
 }
+constexpr int MC_BLOCKS_PER_XCD = 128;  // 32 CUs x 4 workgroups (16 waves per CU at 4 per SIMD)
 
 // --------------------------------------------------------------------------------------------
 // Encoder candidate windows (mm_sad_window, mm_me.h)
@@ -384,58 +435,148 @@ __global__ void __launch_bounds__(256) k_me_sad(SeqConst sc, Geometry geo, MeWin
 }
 
 // --------------------------------------------------------------------------------------------
-// MM-DMVR (mm_pred_dmvr, mm_dmvr.h)
+// MM-DMVR inside the device-planned picture (MM_PUF_DMVR PUs, mm_dmvr.h): k_plan_place placed the
+// sub-PU records; these run between k_plan_place and k_setup_dev.  Their sizes live on the device
+// (the DMVR share of a device-resident list is unknown to the host), so they are grid-stride loops
+// over a fixed grid instead of capacity-sized grids of mostly idle workgroups.
 // --------------------------------------------------------------------------------------------
 using namespace mmdmvr;
+constexpr int DMVR_GRID = 2048;  // workgroups of 256 of the grid-stride DMVR kernels
 
-__global__ void __launch_bounds__(256) k_dmvr_setup(SeqConst sc, const SubPuDev* __restrict__ sp, int n_jobs,
-                                                    const PicTables t, BlockSetup* __restrict__ out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_jobs) return;
-  dmvr_setup_thread(i, sc, sp, t.ged, out);
+// thread per (sub-PU, offset, list) setup; the (sub-PU, offset) cost word is zeroed with list 0's
+__global__ void __launch_bounds__(256) k_dmvr_setup_dev(SeqConst sc, const PlanMeta* __restrict__ meta,
+                                                        const SubPuDev* __restrict__ sp, const PicTables t,
+                                                        BlockSetup* __restrict__ out, uint32_t* __restrict__ costs) {
+  const int n_jobs = meta->n_sub * N_OFF * 2;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n_jobs; i += gridDim.x * blockDim.x) {
+    dmvr_setup_thread(i, sc, sp, t.ged, out);
+    if ((i & 1) == 0) costs[i >> 1] = 0u;
+  }
 }
 
-__global__ void __launch_bounds__(256) k_dmvr_cost(SeqConst sc, Geometry geo, const SubPuDev* __restrict__ sp,
-                                                   int n_sub, const int* __restrict__ off, const int* __restrict__ chunk,
-                                                   int n_elems, const BlockSetup* __restrict__ setups, MpaCache cache,
-                                                   const PicTables t, uint32_t* __restrict__ costs) {
-  const int g = xcd_block() * blockDim.x + threadIdx.x;
+// thread per (sub-PU, offset, 4x4 sub-block); each wave's segments of equal cost index are summed
+// across lanes (shuffle scan) and added by their last lane
+__global__ void __launch_bounds__(256) k_dmvr_cost_dev(SeqConst sc, Geometry geo, const PlanMeta* __restrict__ meta,
+                                                       const SubPuDev* __restrict__ sp, const int* __restrict__ off,
+                                                       const int* __restrict__ chunk, const BlockSetup* __restrict__ setups,
+                                                       MpaCache cache, const PicTables t, uint32_t* __restrict__ costs) {
+  const int n_elems = meta->n_dmvr_elems, n_sub = meta->n_sub;
   const int lane = __lane_id();
-  if (g - lane >= n_elems) return;
-  const int si = wave_find_item(off, chunk, g, n_sub);
-  const bool active = g < n_elems;
-  int idx = -1 - lane;
-  uint32_t v = 0;
-  if (active) {
-    const Taps taps{c_luma_taps, c_chroma_taps, &c_packed_taps, t.pool};
-    v = dmvr_cost_thread(g, si, sc, geo, taps, sp, setups, cache, t.ref, &idx);
-  }
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, n_waves = (gridDim.x * blockDim.x) >> 6;
+  const Taps taps{c_luma_taps, c_chroma_taps, &c_packed_taps, t.pool};
+  for (int g0 = wave * 64; g0 < n_elems; g0 += n_waves * 64) {
+    const int g = g0 + lane;
+    const int si = wave_find_item(off, chunk, g, n_sub);
+    const bool active = g < n_elems;
+    int idx = -1 - lane;
+    uint32_t v = 0;
+    if (active) v = dmvr_cost_thread(g, si, sc, geo, taps, sp, setups, cache, t.ref, &idx);
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t vu = __shfl_up(v, d);
-    const int iu = __shfl_up(idx, d);
-    if (lane >= d && iu == idx) v += vu;
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t vu = __shfl_up(v, d);
+      const int iu = __shfl_up(idx, d);
+      if (lane >= d && iu == idx) v += vu;
+    }
+    const int inext = __shfl_down(idx, 1);
+    if (active && (lane == 63 || inext != idx)) atomicAdd(&costs[idx], v);
   }
-  const int inext = __shfl_down(idx, 1);
-  if (active && (lane == 63 || inext != idx)) atomicAdd(&costs[idx], v);
 }
 
-__global__ void __launch_bounds__(256) k_dmvr_decide(const SubPuDev* __restrict__ sp, int n_sub,
-                                                     const uint32_t* __restrict__ costs, mm_pu_desc* __restrict__ out,
-                                                     int32_t* __restrict__ mvd) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= n_sub) return;
-  dmvr_decide_thread(s, sp, costs, out, mvd);
+// thread per sub-PU: decision, refined MVs into the sub-PU's planned jobs (read next by k_setup_dev)
+__global__ void __launch_bounds__(256) k_dmvr_decide_dev(const PlanMeta* __restrict__ meta, const SubPuDev* __restrict__ sp,
+                                                         const uint32_t* __restrict__ costs, JobDev* __restrict__ jobs,
+                                                         int32_t* __restrict__ mvd) {
+  const int n_sub = meta->n_sub;
+  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < n_sub; s += gridDim.x * blockDim.x)
+    dmvr_decide_jobs_thread(s, sp, costs, jobs, mvd);
 }
 
 // --------------------------------------------------------------------------------------------
 // MM-MVP (mm_mvp_convert, mm_mvp.h)
 // --------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_mvp(SeqConst sc, const mmmvp::MvpQueryDev* __restrict__ q, int n,
-                                             const M3* __restrict__ ged, int32_t* __restrict__ out) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n) return;
-  mmmvp::mvp_thread(t, sc, q, ged, out);
+// One workgroup converts 256 queries.  The two model evaluations of a query (the candidate's
+// modelMotion, then the desired model's equivalent MV) each branch on a model id, and a wave of
+// arbitrary queries would run every model's code one after another.  So between the steps the
+// workgroup regroups its queries through LDS: step 1 runs on the queries ordered by the candidate's
+// model, step 2 on them ordered by the desired model (a counting sort of 256 keys each time), and
+// each wave then runs one or two models' code.  Early returns and failing queries take no slot.
+constexpr int MVP_BLOCK = 256;
+constexpr int MVP_KEYS = NUM_MODELS;
+__device__ __forceinline__ void mvp_regroup(int key, int* s_cnt, int* s_perm, int* n_work) {
+  const int tid = threadIdx.x;
+  if (tid < MVP_KEYS) s_cnt[tid] = 0;
+  __syncthreads();
+  int rank = 0;
+  if (key >= 0) rank = atomicAdd(&s_cnt[key], 1);
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0;
+    for (int k = 0; k < MVP_KEYS; k++) {
+      const int c = s_cnt[k];
+      s_cnt[k] = acc;
+      acc += c;
+    }
+    s_cnt[MVP_KEYS] = acc;
+  }
+  __syncthreads();
+  if (key >= 0) s_perm[s_cnt[key] + rank] = tid;
+  __syncthreads();
+  *n_work = s_cnt[MVP_KEYS];
+}
+
+__global__ void __launch_bounds__(MVP_BLOCK) k_mvp_dev(SeqConst sc, const mm_mvp_query* __restrict__ q, int n,
+                                                       uint32_t active, mmmvp::EpiTable et, int32_t* __restrict__ out,
+                                                       unsigned long long* __restrict__ status,
+                                                       unsigned long long* __restrict__ next_status) {
+  using namespace mmmvp;
+  __shared__ mm_mvp_query s_q[MVP_BLOCK];
+  __shared__ float s_sx[MVP_BLOCK], s_sy[MVP_BLOCK];
+  __shared__ int s_perm[MVP_BLOCK], s_cnt[MVP_KEYS + 1], s_ok[MVP_BLOCK];
+  __shared__ unsigned long long s_status;
+  const int tid = threadIdx.x, i0 = blockIdx.x * MVP_BLOCK, i = i0 + tid;
+  if (tid == 0) s_status = 0;
+  if (blockIdx.x == 0 && tid == 0) *next_status = 0ull;
+  int key = -1;
+  if (i < n) {
+    const mm_mvp_query x = q[i];
+    s_q[tid] = x;
+    int32_t o[2] = {0, 0};
+    int code = mvp_validate(x, active);
+    if (code == MM_OK && !mvp_early(x, et, o, &code)) key = x.model_orig;
+    if (key < 0) {
+      out[2 * i] = o[0];
+      out[2 * i + 1] = o[1];
+    }
+    if (code) atomicMax(&s_status, status_word(i, code));
+  }
+  int nw;
+  mvp_regroup(key, s_cnt, s_perm, &nw);
+  // step 1 in candidate-model order
+  if (tid < nw) {
+    const int k = s_perm[tid];
+    float sx = 0.0f, sy = 0.0f;
+    const bool ok = mvp_candidate_motion(sc, s_q[k], et, &sx, &sy);
+    if (!ok) {
+      atomicMax(&s_status, status_word(i0 + k, MM_ERR_NOEPIPOLE));
+      out[2 * (i0 + k)] = out[2 * (i0 + k) + 1] = 0;
+    }
+    s_sx[k] = sx;
+    s_sy[k] = sy;
+    s_ok[k] = ok ? 1 : 0;
+  }
+  __syncthreads();
+  const int key2 = (key >= 0 && s_ok[tid]) ? s_q[tid].model_desired : -1;
+  mvp_regroup(key2, s_cnt, s_perm, &nw);
+  // step 2 in desired-model order
+  if (tid < nw) {
+    const int k = s_perm[tid];
+    int32_t o[2] = {0, 0};
+    if (!mvp_desired_mv(sc, s_q[k], et, s_sx[k], s_sy[k], o)) atomicMax(&s_status, status_word(i0 + k, MM_ERR_NOEPIPOLE));
+    out[2 * (i0 + k)] = o[0];
+    out[2 * (i0 + k) + 1] = o[1];
+  }
+  __syncthreads();
+  if (tid == 0 && s_status) atomicMax(status, s_status);
 }
 
 // InterpolationFilter::filter<N, isVertical, isFirst, isLast> / filterCopy on a raw block
@@ -521,9 +662,15 @@ struct PlanSlot {
   DevBuf<PlanMeta> meta;
   DevBuf<mm_int2> mc_meta;
   DevBuf<mm_int4> mc_pos[2];
+  DevBuf<SubPuDev> dmvr_sub;  // MM-DMVR sub-PU records (k_plan_place) and their element offsets / chunks
+  DevBuf<int> dmvr_off, dmvr_chunk;
   int n_ensured = 0;  // largest stripe size the buffers were sized for (they only grow)
+  bool dmvr_ensured = false;
   PlanCaps caps{};
   void release() {
+    dmvr_sub.release();
+    dmvr_off.release();
+    dmvr_chunk.release();
     job_off.release();
     job_chunk.release();
     jobs.release();
@@ -564,6 +711,7 @@ struct mm_ctx {
   std::vector<int> pool_free;
   EpipoleMap epipoles;                            // the context's EpipoleList (mm_epipole.h)
   mm_epipole_list epi_handle{&epipoles, false};   // its C-ABI handle (mm_get_epipole_list)
+  float* trig = nullptr;  // separable toSphere table of the frame grid (MpaCache::trig_col / trig_row)
   float* mpa_px[3] = {nullptr, nullptr, nullptr};
   float* mpa_py[3] = {nullptr, nullptr, nullptr};
   uint8_t* mpa_vip[3] = {nullptr, nullptr, nullptr};
@@ -598,13 +746,26 @@ struct mm_ctx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::map<int, RefHost> orgs;  // original luma pictures for mm_sad_window
   DevBuf<MeBlockDev> d_me_blocks;
-  DevBuf<SubPuDev> d_dmvr_sub;
-  DevBuf<int> d_dmvr_off, d_dmvr_chunk, d_dmvr_mvd;
+  // MM-DMVR of the device-planned picture (mm_set_dmvr / mm_pred_dmvr): the per-(sub-PU, offset,
+  // list) setups, the 25 costs and the refined deltas of every sub-PU; used on the context stream only
+  bool dmvr = false;
+  DevBuf<int> d_dmvr_mvd;
   DevBuf<uint32_t> d_dmvr_cost;
   DevBuf<BlockSetup> d_dmvr_setup;
-  DevBuf<mmmvp::MvpQueryDev> d_mvp_q;
+  // MM-MVP: the device copy of the epipole list (refreshed when its version moves, staged through a
+  // pinned buffer on the context stream), the host-buffer API's query / result buffers and the
+  // deferred status words (ping-pong: a call's block 0 zeroes the next call's word)
+  DevBuf<mmmvp::EpiDev> d_epi;
+  mmmvp::EpiDev* h_epi = nullptr;
+  size_t h_epi_cap = 0;
+  hipEvent_t ev_epi = nullptr;
+  unsigned long long epi_version = ~0ull;
+  int epi_n = 0;
+  DevBuf<mm_mvp_query> d_mvp_q;
   DevBuf<int32_t> d_mvp_out;
-  DevBuf<mm_pu_desc> d_dmvr_pus;
+  DevBuf<unsigned long long> d_mvp_status;
+  int mvp_par = 0;
+  bool mvp_pending = false;
   DevBuf<int> d_me_off, d_me_chunk;
   bool stage_timing = false;
   hipEvent_t ev_stage[3] = {nullptr, nullptr, nullptr};  // after planning, setup, reprojection
@@ -644,6 +805,8 @@ static MpaCache make_cache(mm_ctx* c) {
   }
   mc.cols = c->geo.W / 4;
   mc.rows = c->geo.H / 4;
+  mc.trig_col = c->trig;
+  mc.trig_row = c->trig ? c->trig + 4 * mc.cols : nullptr;
   return mc;
 }
 
@@ -738,6 +901,7 @@ int mm_create(const mm_seq_params* p, int device, mm_ctx** out_ctx) {
       hipEventCreateWithFlags(&c->ev_gate[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_gate[1], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_plan, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_epi, hipEventDisableTiming) != hipSuccess ||
       hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
       hipEventRecord(c->ev_gate[0], c->stream) != hipSuccess) {
     mm_destroy(c);
@@ -755,7 +919,16 @@ int mm_create(const mm_seq_params* p, int device, mm_ctx** out_ctx) {
     hipLaunchKernelGGL(k_mpa_cache, dim3((n + 255) / 256), dim3(256), 0, c->stream, c->sc, MPA_FRONT_BACK + pl, cols,
                        rows, c->mpa_px[pl], c->mpa_py[pl], c->mpa_vip[pl]);
   }
+  // separable toSphere table (MpaCache::trig_col / trig_row): 2 flavours x (cols + rows) pairs
+  if (hipMalloc(&c->trig, (size_t)4 * (cols + rows) * sizeof(float)) != hipSuccess) {
+    mm_destroy(c);
+    return MM_ERR_HIP;
+  }
+  hipLaunchKernelGGL(k_erp_trig, dim3((2 * (cols + rows) + 255) / 256), dim3(256), 0, c->stream, c->sc, cols, rows,
+                     c->trig, c->trig + 4 * cols);
   if (c->d_status.ensure(2) != hipSuccess || hipMemsetAsync(c->d_status.p, 0, 2 * sizeof(unsigned long long), c->stream) != hipSuccess ||
+      c->d_mvp_status.ensure(2) != hipSuccess ||
+      hipMemsetAsync(c->d_mvp_status.p, 0, 2 * sizeof(unsigned long long), c->stream) != hipSuccess ||
       hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) {
     mm_destroy(c);
     return MM_ERR_HIP;
@@ -769,6 +942,7 @@ int mm_destroy(mm_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   if (c->pool) (void)hipFree(c->pool);
+  if (c->trig) (void)hipFree(c->trig);
   for (int pl = 0; pl < 3; pl++) {
     if (c->mpa_px[pl]) (void)hipFree(c->mpa_px[pl]);
     if (c->mpa_py[pl]) (void)hipFree(c->mpa_py[pl]);
@@ -787,15 +961,15 @@ int mm_destroy(mm_ctx* c) {
   c->d_ged.release();
   for (auto& kv : c->orgs) (void)hipFree(kv.second.y);
   c->d_me_blocks.release();
-  c->d_dmvr_sub.release();
-  c->d_dmvr_off.release();
-  c->d_dmvr_chunk.release();
   c->d_dmvr_mvd.release();
   c->d_dmvr_cost.release();
   c->d_dmvr_setup.release();
   c->d_mvp_q.release();
   c->d_mvp_out.release();
-  c->d_dmvr_pus.release();
+  c->d_mvp_status.release();
+  c->d_epi.release();
+  if (c->h_epi) (void)hipHostFree(c->h_epi);
+  if (c->ev_epi) (void)hipEventDestroy(c->ev_epi);
   c->d_me_off.release();
   c->d_me_chunk.release();
   for (auto& e : c->ev_stage)
@@ -821,9 +995,12 @@ int mm_set_stream(mm_ctx* c, void* s) {
   return MM_OK;
 }
 
+static int read_mvp_status(mm_ctx* c, int* first_bad);
 int mm_synchronize(mm_ctx* c) {
   if (!c) return MM_ERR_ARG;
-  return read_status(c, nullptr);
+  const int rc = read_status(c, nullptr);
+  const int rm = read_mvp_status(c, nullptr);
+  return rc ? rc : rm;
 }
 
 int mm_set_epipole(mm_ctx* c, int cur, int ref, const int32_t q24[3]) {
@@ -1055,14 +1232,29 @@ static int round_grid(long v) { return (int)((v + 8 * XCD_RUN - 1) / (8 * XCD_RU
 // once, so sub-blocks are bounded by the picture's sub-block count (and by n * 1024, 128x128
 // PUs); a PU has at most 4 jobs and 4 reprojection elements per luma sub-block (2 lists x
 // {luma, chroma}).  k_plan_place refuses a list beyond these capacities (overlapping PUs).
-static int ensure_slot_buffers(mm_ctx* c, PlanSlot& S, int n) {
+// With MM-DMVR a PU is placed as up to 64 sub-PUs (128x128 / 16x16); a sub-PU covers at least 128
+// luma samples (PU::checkDMVRCondition), so the picture bounds them by W * H / 128, and their cost
+// elements (N_OFF per luma sub-block) by N_OFF times the picture's sub-blocks.
+static int ensure_slot_buffers(mm_ctx* c, PlanSlot& S, int n, bool dmvr) {
   PlanCaps k;
-  k.pus = n;
-  k.jobs = 4 * n;
   const long area_sb = (long)(c->geo.W / 4) * (c->geo.H / 4);
+  const int subs = dmvr ? (int)std::min<long>((long)n * 64, (long)c->geo.W * c->geo.H / 128) : 0;
+  k.pus = n + subs;
+  k.jobs = 4 * k.pus;
   k.sb = (int)std::min<long>((long)n * 1024, area_sb);
   k.elems = 4 * k.sb;
+  k.subs = subs;
+  k.dmvr_elems = dmvr ? (int)std::min<long>((long)N_OFF * area_sb, (long)subs * N_OFF * 16) : 0;
   S.caps = k;
+  if (dmvr) {
+    HIPCHK(c, S.dmvr_sub.ensure(k.subs));
+    HIPCHK(c, S.dmvr_off.ensure(k.subs));
+    HIPCHK(c, S.dmvr_chunk.ensure((size_t)k.dmvr_elems / 64 + 1));
+    HIPCHK(c, c->d_dmvr_setup.ensure((size_t)k.subs * N_OFF * 2));
+    HIPCHK(c, c->d_dmvr_cost.ensure((size_t)k.subs * N_OFF));
+    HIPCHK(c, c->d_dmvr_mvd.ensure(2 * (size_t)k.subs));
+    S.dmvr_ensured = true;
+  }
   bool fresh_jobs = false;
   HIPCHK(c, S.jobs.ensure(k.jobs, &fresh_jobs));
   if (fresh_jobs) HIPCHK(c, hipMemsetAsync(S.jobs.p, 0, S.jobs.cap * sizeof(JobDev), c->stream));
@@ -1086,6 +1278,7 @@ static int ensure_slot_buffers(mm_ctx* c, PlanSlot& S, int n) {
   S.n_ensured = std::max(S.n_ensured, n);
   return MM_OK;
 }
+static bool slot_fits(const PlanSlot& S, int n, bool dmvr) { return n <= S.n_ensured && (!dmvr || S.dmvr_ensured); }
 
 // One stripe (PUs [base, base + n) of the picture's list) through k_plan_count + k_plan_place +
 // k_setup_dev + k_reproj_dev + k_mc_dev on `st`.  Stage events only in single-stripe timing mode.
@@ -1094,19 +1287,42 @@ static int ensure_slot_buffers(mm_ctx* c, PlanSlot& S, int n) {
 static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables& t, const Geometry& geo,
                          const mm_pu_desc* d_in, int n, int base, unsigned long long* status,
                          unsigned long long* next_status, int16_t* dy, ptrdiff_t sdy, int16_t* dcb, int16_t* dcr,
-                         ptrdiff_t sdc, hipStream_t st_back = nullptr) {
+                         ptrdiff_t sdc, bool plan_ahead = false, bool want_mvd = false) {
+  // plan-ahead: `st` is the auxiliary stream for the planning kernels; the rest runs on the
+  // context stream (which may be the null stream, so a flag, not a null handle, says so)
+  hipStream_t st_back = c->stream;
+  bool back = plan_ahead;
   const PlanCaps& k = S.caps;
   const int gp = (n + PLAN_BLOCK - 1) / PLAN_BLOCK;
   const int gs = (k.jobs + 255) / 256;
   const int gr = round_grid((k.elems + 255) / 256);
-  const int gm = round_grid((k.sb + 255) / 256);
+  const int gm = 8 * std::max(1, std::min(MC_BLOCKS_PER_XCD, (k.sb / 8 + 255) / 256));
   const int gq = (n + PLACE_BLOCK - 1) / PLACE_BLOCK;
   hipLaunchKernelGGL(k_plan_count, dim3(gp), dim3(PLAN_BLOCK), 0, st, d_in, n, base, t, status, S.blk.p, S.blkq.p, gq);
+  const DmvrRecs dm{S.dmvr_sub.p, S.dmvr_off.p, S.dmvr_chunk.p};
   hipLaunchKernelGGL(k_plan_place, dim3(gq), dim3(PLACE_BLOCK), 0, st, d_in, n, t, status, next_status, S.blk.p, gp,
-                     S.blkq.p, S.meta.p, k, S.jobs.p, S.job_off.p, S.job_chunk.p);
+                     S.blkq.p, S.meta.p, k, S.jobs.p, S.job_off.p, S.job_chunk.p, dm);
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[0], st));
+  if (t.dmvr) {
+    // MM-DMVR reads the reference pictures: from here on the context stream (plan-ahead gates only
+    // the PU list, not the references)
+    if (back) {
+      HIPCHK(c, hipEventRecord(c->ev_plan, st));
+      HIPCHK(c, hipStreamWaitEvent(st_back, c->ev_plan, 0));
+      st = st_back;
+      back = false;
+    }
+    const int gd = (int)std::min<long>(DMVR_GRID, ((long)k.subs * N_OFF * 2 + 255) / 256 + 1);
+    const int gc = (int)std::min<long>(DMVR_GRID, ((long)k.dmvr_elems + 255) / 256 + 1);
+    hipLaunchKernelGGL(k_dmvr_setup_dev, dim3(gd), dim3(256), 0, st, c->sc, S.meta.p, S.dmvr_sub.p, t, c->d_dmvr_setup.p,
+                       c->d_dmvr_cost.p);
+    hipLaunchKernelGGL(k_dmvr_cost_dev, dim3(gc), dim3(256), 0, st, c->sc, geo, S.meta.p, S.dmvr_sub.p, S.dmvr_off.p,
+                       S.dmvr_chunk.p, c->d_dmvr_setup.p, make_cache(c), t, c->d_dmvr_cost.p);
+    hipLaunchKernelGGL(k_dmvr_decide_dev, dim3(std::max(1, std::min(DMVR_GRID, (k.subs + 255) / 256))), dim3(256), 0, st,
+                       S.meta.p, S.dmvr_sub.p, c->d_dmvr_cost.p, S.jobs.p, want_mvd ? c->d_dmvr_mvd.p : nullptr);
+  }
   hipLaunchKernelGGL(k_setup_dev, dim3(gs), dim3(256), 0, st, c->sc, S.meta.p, S.jobs.p, t, S.setup.p);
-  if (st_back) {  // plan-ahead: reprojection and interpolation on the context stream
+  if (back) {  // plan-ahead: reprojection and interpolation on the context stream
     HIPCHK(c, hipEventRecord(c->ev_plan, st));
     HIPCHK(c, hipStreamWaitEvent(st_back, c->ev_plan, 0));
     st = st_back;
@@ -1133,9 +1349,12 @@ static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables
 // stream forks from and joins back into the context stream.  Validation errors of every stripe
 // go to the picture's status word and are reported by mm_pred_status.
 // only_list / hp / store: mm_pred_list (-1 / 0 / 3 for the normal prediction).
+// dmvr: MM_PUF_DMVR PUs allowed (the context's mm_set_dmvr, or mm_pred_dmvr); want_mvd: keep the
+// refined delta of every DMVR sub-PU, in placement order, in d_dmvr_mvd.
 static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, int n, int16_t* dy, ptrdiff_t sdy,
                               int16_t* dcb, int16_t* dcr, ptrdiff_t sdc, int only_list = -1, int hp = 0,
-                              int store = 3, bool may_plan_ahead = false) {
+                              int store = 3, bool may_plan_ahead = false, bool dmvr = false,
+                              bool want_mvd = false) {
   std::vector<std::pair<int, RefDev>> refs;
   refs = ref_slots(c);
   PicTables t;
@@ -1144,12 +1363,14 @@ static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, in
   if (rc) return fail(c, rc, err);
   t.pool = pool_of(c);
   t.only_list = only_list;
+  t.dmvr = dmvr ? 1 : 0;
   Geometry geo = c->geo;
   geo.hp = hp;
   geo.store = store;
   geo.vec_store = (!dy || ((uintptr_t)dy % 8 == 0 && sdy % 4 == 0)) &&
                   (!geo.chroma || !dcb || ((uintptr_t)dcb % 4 == 0 && (uintptr_t)dcr % 4 == 0 && sdc % 2 == 0));
-  const int K = c->stage_timing ? 1 : std::max(1, std::min(c->n_stripes, (n + PLAN_BLOCK - 1) / PLAN_BLOCK));
+  // one stripe under stage timing, and with DMVR (its setup / cost buffers are the context's)
+  const int K = (c->stage_timing || dmvr) ? 1 : std::max(1, std::min(c->n_stripes, (n + PLAN_BLOCK - 1) / PLAN_BLOCK));
   const int per = (n + K - 1) / K;
   unsigned long long* status = c->d_status.p + c->pic_par;
   unsigned long long* next_status = c->d_status.p + (c->pic_par ^ 1);
@@ -1157,21 +1378,21 @@ static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, in
     // Plan-ahead: planning + setup of this picture on `aux`, gated only by the context stream's
     // position at the start of the previous call (its slot's previous user, two calls back, has
     // finished there), so they overlap the previous picture's interpolation.
-    if (per > c->slot[0].n_ensured || per > c->slot[1].n_ensured) {
+    if (!slot_fits(c->slot[0], per, dmvr) || !slot_fits(c->slot[1], per, dmvr)) {
       // growing frees buffers the other stream may still use, and zeroes on the context stream
       HIPCHK(c, hipStreamSynchronize(c->aux));
       HIPCHK(c, hipStreamSynchronize(c->stream));
-      for (int s = 0; s < 2; s++) RCCHK(ensure_slot_buffers(c, c->slot[s], per));
+      for (int s = 0; s < 2; s++) RCCHK(ensure_slot_buffers(c, c->slot[s], per, dmvr));
       HIPCHK(c, hipStreamSynchronize(c->stream));
     } else {
-      for (int s = 0; s < 2; s++) RCCHK(ensure_slot_buffers(c, c->slot[s], per));  // caps only
+      for (int s = 0; s < 2; s++) RCCHK(ensure_slot_buffers(c, c->slot[s], per, dmvr));  // caps only
     }
     HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_gate[c->gate_par], 0));
     c->gate_par ^= 1;
     HIPCHK(c, hipEventRecord(c->ev_gate[c->gate_par], c->stream));
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     RCCHK(launch_stripe(c, c->slot[c->ahead_par], c->aux, t, geo, d_in, n, 0, status, next_status, dy, sdy, dcb, dcr,
-                        sdc, c->stream));
+                        sdc, true, want_mvd));
     c->ahead_par ^= 1;
     HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     c->last_status = status;
@@ -1179,7 +1400,11 @@ static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, in
     c->status_pending = true;
     return MM_OK;
   }
-  for (int s = 0; s < std::min(K, 2); s++) RCCHK(ensure_slot_buffers(c, c->slot[s], per));
+  for (int s = 0; s < std::min(K, 2); s++) {
+    // growth of buffers a plan-ahead call on the auxiliary stream may still use
+    if (!slot_fits(c->slot[s], per, dmvr)) HIPCHK(c, hipStreamSynchronize(c->aux));
+    RCCHK(ensure_slot_buffers(c, c->slot[s], per, dmvr));
+  }
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
   if (K > 1) {
     HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
@@ -1189,7 +1414,7 @@ static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, in
     const int base = s * per, m = std::min(per, n - base);
     if (m <= 0) break;
     RCCHK(launch_stripe(c, c->slot[s & 1], (s & 1) ? c->aux : c->stream, t, geo, d_in + base, m, base, status,
-                        s == 0 ? next_status : nullptr, dy, sdy, dcb, dcr, sdc));
+                        s == 0 ? next_status : nullptr, dy, sdy, dcb, dcr, sdc, false, want_mvd));
   }
   if (K > 1) {
     HIPCHK(c, hipEventRecord(c->ev_join, c->aux));
@@ -1218,6 +1443,7 @@ int mm_set_stripes(mm_ctx* c, int stripes) {
 }
 
 // Synchronise and decode the deferred validation status of the last device-planned call.
+static int decode_status(mm_ctx* c, unsigned long long w, int* first_bad, const char* item);
 static int read_status(mm_ctx* c, int* first_bad) {
   if (first_bad) *first_bad = -1;
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1225,6 +1451,9 @@ static int read_status(mm_ctx* c, int* first_bad) {
   c->status_pending = false;
   unsigned long long w = 0;
   HIPCHK(c, hipMemcpy(&w, c->last_status, sizeof(w), hipMemcpyDeviceToHost));
+  return decode_status(c, w, first_bad, "PU");
+}
+static int decode_status(mm_ctx* c, unsigned long long w, int* first_bad, const char* item) {
   if (!w) return MM_OK;
   const unsigned long long v = ~w;
   const int code = (int)(v & 0xff), pu = (int)(v >> 8);
@@ -1233,7 +1462,7 @@ static int read_status(mm_ctx* c, int* first_bad) {
                                      "invalid BCW index, or the list covers more than the picture",
                                "HIP error", "reference POC not uploaded", "no epipole for (curPOC, refPOC)",
                                "invalid, CLASSIC or inactive motion model", "no device"};
-  return fail(c, code, "PU " + std::to_string(pu) + ": " + (code >= 0 && code <= 6 ? what[code] : "error"));
+  return fail(c, code, std::string(item) + " " + std::to_string(pu) + ": " + (code >= 0 && code <= 6 ? what[code] : "error"));
 }
 
 int mm_pred_device(mm_ctx* c, int cur_poc, const mm_pu_desc* d_pus, int n, int16_t* dy, ptrdiff_t sdy, int16_t* dcb,
@@ -1241,7 +1470,13 @@ int mm_pred_device(mm_ctx* c, int cur_poc, const mm_pu_desc* d_pus, int n, int16
   if (!c || n < 0 || (n > 0 && !d_pus) || !dy || (c->geo.chroma && (!dcb || !dcr))) return MM_ERR_ARG;
   if (n == 0) return MM_OK;
   HIPCHK(c, hipSetDevice(c->device));
-  return launch_device_plan(c, cur_poc, d_pus, n, dy, sdy, dcb, dcr, sdc, -1, 0, 3, true);
+  return launch_device_plan(c, cur_poc, d_pus, n, dy, sdy, dcb, dcr, sdc, -1, 0, 3, true, c->dmvr);
+}
+
+int mm_set_dmvr(mm_ctx* c, int on) {
+  if (!c) return MM_ERR_ARG;
+  c->dmvr = on != 0;
+  return MM_OK;
 }
 
 int mm_pred_status(mm_ctx* c, int* first_bad_pu) {
@@ -1353,64 +1588,101 @@ int mm_sad_window(mm_ctx* c, int cur_poc, const mm_me_block* blocks, int n, int 
   return MM_OK;
 }
 
+// MM-DMVR of a PU list: every PU is flagged MM_PUF_DMVR and the list runs the device-planned
+// picture path with DMVR on (search, decision, refined prediction); the deltas are read back.
 int mm_pred_dmvr(mm_ctx* c, int cur_poc, const mm_pu_desc* pus, int n, int16_t* dy, ptrdiff_t sdy, int16_t* dcb,
                  int16_t* dcr, ptrdiff_t sdc, int32_t* mvd_out) {
   if (!c || n < 0 || (n > 0 && !pus) || !dy || (c->geo.chroma && (!dcb || !dcr))) return MM_ERR_ARG;
   if (n == 0) return MM_OK;
   HIPCHK(c, hipSetDevice(c->device));
-  std::vector<std::pair<int, RefDev>> refs;
-  refs = ref_slots(c);
-  PicTables t;
-  std::string err;
-  int rc = build_pic_tables(seq_info(c->prm), c->epipoles, cur_poc, refs, &t, &err);
-  if (rc) return fail(c, rc, err);
-  t.pool = pool_of(c);
-  DmvrPlan plan;
-  rc = plan_dmvr(seq_info(c->prm), t, pus, n, &plan, &err);
-  if (rc) return fail(c, rc, err);
-  const int ns = (int)plan.sub.size(), nj = ns * N_OFF * 2, ne = (int)plan.n_elems;
-  RCCHK(upload(c, c->d_dmvr_sub, plan.sub));
-  RCCHK(upload(c, c->d_dmvr_off, plan.off));
-  RCCHK(upload(c, c->d_dmvr_chunk, plan.chunk));
-  HIPCHK(c, c->d_dmvr_setup.ensure(nj));
-  HIPCHK(c, c->d_dmvr_cost.ensure((size_t)ns * N_OFF));
-  HIPCHK(c, c->d_dmvr_pus.ensure(ns));
-  HIPCHK(c, c->d_dmvr_mvd.ensure(2 * (size_t)ns));
-  HIPCHK(c, hipMemsetAsync(c->d_dmvr_cost.p, 0, (size_t)ns * N_OFF * sizeof(uint32_t), c->stream));
-  hipLaunchKernelGGL(k_dmvr_setup, dim3((nj + 255) / 256), dim3(256), 0, c->stream, c->sc, c->d_dmvr_sub.p, nj, t,
-                     c->d_dmvr_setup.p);
-  hipLaunchKernelGGL(k_dmvr_cost, dim3(round_grid((ne + 255) / 256)), dim3(256), 0, c->stream, c->sc, c->geo,
-                     c->d_dmvr_sub.p, ns, c->d_dmvr_off.p, c->d_dmvr_chunk.p, ne, c->d_dmvr_setup.p, make_cache(c), t,
-                     c->d_dmvr_cost.p);
-  hipLaunchKernelGGL(k_dmvr_decide, dim3((ns + 255) / 256), dim3(256), 0, c->stream, c->d_dmvr_sub.p, ns,
-                     c->d_dmvr_cost.p, c->d_dmvr_pus.p, c->d_dmvr_mvd.p);
+  std::vector<mm_pu_desc> flagged(pus, pus + n);
+  long n_sub = 0;
+  for (auto& u : flagged) {
+    u.flags |= MM_PUF_DMVR;
+    if (u.w > 0 && u.h > 0) n_sub += (long)((u.w + 15) / 16) * ((u.h + 15) / 16);
+  }
+  RCCHK(mm_pred_prepare(c, cur_poc, flagged.data(), n));
+  c->prepared = false;  // the buffer holds this call's PUs, not a prepared picture
+  RCCHK(launch_device_plan(c, cur_poc, c->d_pu_in.p, n, dy, sdy, dcb, dcr, sdc, -1, 0, 3, false, true, true));
+  const int rc = read_status(c, nullptr);
+  if (rc) return rc;
+  // the deltas of the sub-PUs in placement order: PUs in list order (DMVR bucket placement keeps
+  // input order), sub-PUs in raster order
+  if (mvd_out && n_sub)
+    HIPCHK(c, hipMemcpy(mvd_out, c->d_dmvr_mvd.p, 2 * (size_t)n_sub * sizeof(int32_t), hipMemcpyDeviceToHost));
+  return MM_OK;
+}
+
+// Device copy of the context's epipole list, refreshed when the list changed since the last copy.
+static int sync_epi_table(mm_ctx* c) {
+  if (c->epipoles.version() == c->epi_version) return MM_OK;
+  std::vector<mmmvp::EpiDev> e;
+  epi_entries(c->epipoles, &e);
+  HIPCHK(c, hipEventSynchronize(c->ev_epi));  // the staging buffer may still feed the previous copy
+  if (e.size() > c->h_epi_cap) {
+    if (c->h_epi) (void)hipHostFree(c->h_epi);
+    c->h_epi = nullptr;
+    c->h_epi_cap = 0;
+    const size_t cap = std::max<size_t>(64, 2 * e.size());
+    HIPCHK(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_epi), cap * sizeof(mmmvp::EpiDev), hipHostMallocDefault));
+    c->h_epi_cap = cap;
+  }
+  if (e.size() > c->d_epi.cap || !c->d_epi.p) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // growth frees the buffer queued kernels read
+    HIPCHK(c, c->d_epi.ensure(std::max<size_t>(64, 2 * e.size())));
+  }
+  if (!e.empty()) {
+    std::copy(e.begin(), e.end(), c->h_epi);
+    HIPCHK(c, hipMemcpyAsync(c->d_epi.p, c->h_epi, e.size() * sizeof(mmmvp::EpiDev), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev_epi, c->stream));
+  }
+  c->epi_n = (int)e.size();
+  c->epi_version = c->epipoles.version();
+  return MM_OK;
+}
+
+static int read_mvp_status(mm_ctx* c, int* first_bad) {
+  if (first_bad) *first_bad = -1;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (!c->mvp_pending) return MM_OK;
+  c->mvp_pending = false;
+  unsigned long long w = 0;
+  HIPCHK(c, hipMemcpy(&w, c->d_mvp_status.p + (c->mvp_par ^ 1), sizeof(w), hipMemcpyDeviceToHost));
+  return decode_status(c, w, first_bad, "MVP query");
+}
+
+int mm_mvp_convert_device(mm_ctx* c, const mm_mvp_query* d_q, int n, int32_t* d_mv_out) {
+  if (!c || n < 0 || (n > 0 && (!d_q || !d_mv_out))) return MM_ERR_ARG;
+  if (n == 0) return MM_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  RCCHK(sync_epi_table(c));
+  const mmmvp::EpiTable et{c->d_epi.p, c->epi_n};
+  unsigned long long* st = c->d_mvp_status.p + c->mvp_par;
+  HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+  hipLaunchKernelGGL(k_mvp_dev, dim3((n + MVP_BLOCK - 1) / MVP_BLOCK), dim3(MVP_BLOCK), 0, c->stream, c->sc, d_q, n,
+                     c->prm.active_models, et, d_mv_out, st, c->d_mvp_status.p + (c->mvp_par ^ 1));
   HIPCHK(c, hipGetLastError());
-  // step 4: the refined sub-PUs are ordinary bi PUs for the device-planned prediction path
-  RCCHK(launch_device_plan(c, cur_poc, c->d_dmvr_pus.p, ns, dy, sdy, dcb, dcr, sdc));
-  if (mvd_out)
-    HIPCHK(c, hipMemcpyAsync(mvd_out, c->d_dmvr_mvd.p, 2 * (size_t)ns * sizeof(int32_t), hipMemcpyDeviceToHost,
-                             c->stream));
-  return read_status(c, nullptr);
+  HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+  c->mvp_par ^= 1;  // read_mvp_status reads the word of this call (mvp_par ^ 1 from now on)
+  c->mvp_pending = true;
+  return MM_OK;
+}
+
+int mm_mvp_status(mm_ctx* c, int* first_bad_query) {
+  if (!c) return MM_ERR_ARG;
+  return read_mvp_status(c, first_bad_query);
 }
 
 int mm_mvp_convert(mm_ctx* c, const mm_mvp_query* q, int n, int32_t* mv_out) {
   if (!c || n < 0 || (n > 0 && (!q || !mv_out))) return MM_ERR_ARG;
   if (n == 0) return MM_OK;
   HIPCHK(c, hipSetDevice(c->device));
-  std::vector<mmmvp::MvpQueryDev> qs;
-  std::vector<M3> ged;
-  std::string err;
-  int rc = plan_mvp(seq_info(c->prm), c->epipoles, q, n, &qs, &ged, &err);
-  if (rc) return fail(c, rc, err);
-  RCCHK(upload(c, c->d_mvp_q, qs));
-  RCCHK(upload(c, c->d_ged, ged));
+  HIPCHK(c, c->d_mvp_q.ensure(n));
   HIPCHK(c, c->d_mvp_out.ensure(2 * (size_t)n));
-  hipLaunchKernelGGL(k_mvp, dim3((n + 255) / 256), dim3(256), 0, c->stream, c->sc, c->d_mvp_q.p, n, c->d_ged.p,
-                     c->d_mvp_out.p);
-  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(c->d_mvp_q.p, q, (size_t)n * sizeof(mm_mvp_query), hipMemcpyHostToDevice, c->stream));
+  RCCHK(mm_mvp_convert_device(c, c->d_mvp_q.p, n, c->d_mvp_out.p));
   HIPCHK(c, hipMemcpyAsync(mv_out, c->d_mvp_out.p, 2 * (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  return MM_OK;
+  return read_mvp_status(c, nullptr);
 }
 
 int mm_set_stage_timing(mm_ctx* c, int on) {

@@ -76,8 +76,15 @@ MM_HD uint32_t me_sad_thread(int g, int bi, const SeqConst& sc, const Geometry& 
     py = cache.py[pl][ci];
     vip = cache.vip[pl][ci] != 0;
   }
+  const bool packet = packet_lane(e, b.n);
+  V3 pg;
+  const V3* pgp = nullptr;
+  if (!mpa && cache.trig_col) {
+    pg = grid_sphere(cache, (b.x >> 2) + col, (b.y >> 2) + row, packet);
+    pgp = &pg;
+  }
   int32_t fx, fy;
-  reproject_element(sc, s, gx, gy, packet_lane(e, b.n), mpa, px, py, vip, 0, &fx, &fy);
+  reproject_element(sc, s, gx, gy, packet, mpa, px, py, vip, 0, &fx, &fy, pgp);
   const int xPos = fx >> 4, yPos = fy >> 4, xFrac = fx & 15, yFrac = fy & 15;
   int16_t p[16];
   if (xPos < 0 || yPos < 0 || xPos >= geo.W - 4 || yPos >= geo.H - 4) {  // maxCUWidth = 0

@@ -82,11 +82,13 @@ MM_HD V3 sph_to_cart(float R, float th, float ph, Math m) {
 // ------------------------------------------------------------------------------------------
 // EquirectangularProjection (Projection.cpp:213-249 in SURVEY numbering; pixelOffset = 0)
 // ------------------------------------------------------------------------------------------
+MM_HD float erp_phi(float x, const SeqConst& s) { return ((-((x + 0.0f) / s.Wf)) * 2.0f) * PI_F; }
+MM_HD float erp_theta(float y, const SeqConst& s) { return ((y + 0.0f) / s.Hf) * PI_F; }
 MM_HD V3 erp_to_sphere(float x, float y, const SeqConst& s, Math m) {
-  float phi = ((-((x + 0.0f) / s.Wf)) * 2.0f) * PI_F;
-  float theta = ((y + 0.0f) / s.Hf) * PI_F;
-  return sph_to_cart(1.0f, theta, phi, m);
+  return sph_to_cart(1.0f, erp_theta(y, s), erp_phi(x, s), m);
 }
+// The same point from precomputed (sin, cos) of theta and phi: sph_to_cart(1, theta, phi)
+MM_HD V3 sph_from_trig(float st, float ct, float sp, float cp) { return {(1.0f * st) * cp, (1.0f * st) * sp, 1.0f * ct}; }
 
 MM_HD void erp_from_sphere(V3 p, const SeqConst& s, Math m, bool arr, float* ox, float* oy) {
   V3 sp = cart_to_sph(p, m, arr);
@@ -353,8 +355,11 @@ MM_HD void block_setup_f(BlockSetup* b, const SeqConst& s, int model, bool luma,
 // <Model>::modelMotion[Cached] of one element: the moved position as computed (before the NaN
 // fallback, offset removal and rounding).  CLASSIC (TranslationalMotionModel::modelMotion,
 // TranslationalMotionModel.cpp:8-13) adds the MV.
+// p_grid (optional): toSphere(gx, gy) of this element, taken from the separable per-column /
+// per-row trig table of the frame grid (mm_pipeline.h ErpTrig) -- the same values, computed once.
 MM_HD void model_motion_element(const SeqConst& s, const BlockSetup& b, float gx, float gy, bool packet,
-                                bool mpa_cached, float pers_x, float pers_y, bool pers_vip, float* omx, float* omy) {
+                                bool mpa_cached, float pers_x, float pers_y, bool pers_vip, float* omx, float* omy,
+                                const V3* p_grid = nullptr) {
   const Math m{packet};
   if (b.model == CLASSIC) {
     *omx = gx + b.mvx;
@@ -370,7 +375,7 @@ MM_HD void model_motion_element(const SeqConst& s, const BlockSetup& b, float gx
   // switch computes q and the shared tail projects it (one copy of the acosf/atan2f code).
   const bool mpa = b.model >= MPA_FRONT_BACK && b.model <= MPA_TOP_BOTTOM;
   V3 p = {0.0f, 0.0f, 0.0f};  // toSphere(grid) of TAN / 3DT / ROT / GED
-  if (!mpa) p = erp_to_sphere(gx, gy, s, m);
+  if (!mpa) p = p_grid ? *p_grid : erp_to_sphere(gx, gy, s, m);
   V3 q;
   switch (b.model) {
     case MPA_FRONT_BACK:
@@ -442,9 +447,9 @@ MM_HD void model_motion_element(const SeqConst& s, const BlockSetup& b, float gx
 
 MM_HD void reproject_element(const SeqConst& s, const BlockSetup& b, float gx, float gy, bool packet,
                              bool mpa_cached, float pers_x, float pers_y, bool pers_vip,
-                             int chroma_shift, int32_t* fx, int32_t* fy) {
+                             int chroma_shift, int32_t* fx, int32_t* fy, const V3* p_grid = nullptr) {
   float mx, my;
-  model_motion_element(s, b, gx, gy, packet, mpa_cached, pers_x, pers_y, pers_vip, &mx, &my);
+  model_motion_element(s, b, gx, gy, packet, mpa_cached, pers_x, pers_y, pers_vip, &mx, &my, p_grid);
   // NaN -> unmoved (MVReprojection.cpp:151-154), remove offset, rescale, round to fixed point
   if (isnanf_(mx) || isnanf_(my)) {
     mx = gx;

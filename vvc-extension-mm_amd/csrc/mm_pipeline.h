@@ -52,9 +52,10 @@ struct alignas(8) mm_int2 {
   int x, y;
 };
 // Per-luma-sub-block inputs of k_mc, written by the reprojection of a device-planned picture in
-// the order k_mc reads them (sub-block g of the class-sorted enumeration):
-//   meta[g]   = (ox | oy << 16, slot0 | slot1 << 4 | bcw << 8): output position of the luma 4x4
-//               sub-block, reference slot per list, BCW index -- written by the PU's primary job;
+// the order k_mc reads them (sub-block g of the band-sorted enumeration):
+//   meta[g]   = (ox | oy << 16, slot0 | slot1 << 4 | bcw << 8 | use0 << 12 | use1 << 13): output
+//               position of the luma 4x4 sub-block, reference slot per list, BCW index, the lists
+//               the sub-block uses -- written by the PU's primary job;
 //   pos[l][g] = (luma X, luma Y in 1/16 pel, chroma X, Y in 1/32 pel) of list l: the luma job
 //               writes .xy, the chroma job (or the aliasing MPA luma job) .zw.
 // A bi sub-block is 40 bytes, read with one 8-byte and two 16-byte loads.
@@ -63,6 +64,8 @@ struct McRec {
   mm_int4* pos[2];
 };
 #define MM_META_PRIMARY (1 << 16)
+#define MM_META_USE0 (1 << 12)
+#define MM_META_USE1 (1 << 13)
 
 // w1 = g_BcwWeights[bcw] (Rom.cpp:203 {-2, 3, 4, 5, 10}) as nibbles of w1 + 2; w0 = 8 - w1
 MM_HD int bcw_w1(int bcw) { return (int)((0xC7650u >> (4 * bcw)) & 15u) - 2; }
@@ -70,12 +73,51 @@ MM_HD int bcw_w1(int bcw) { return (int)((0xC7650u >> (4 * bcw)) & 15u) - 2; }
 // MVReprojection::fillCache's frame grid, MPA perspective coordinates per plane
 // (MotionPlaneAdaptiveMotionModel::fillCache), row-major [j][i] over the (W/4) x (H/4) grid
 // x = 4i + off, y = 4j + off.
+//
+// trig_col / trig_row (optional, may be null): EquirectangularProjection::toSphere on the same grid
+// is separable (Projection.cpp:213-228 -> Coordinate.cpp:57-59): phi depends only on the grid column
+// i, theta only on the grid row j, and sphericalToCartesian with R = 1 is
+// (sin th cos ph, sin th sin ph, cos th).  One (sin, cos) pair per column and per row, in both
+// flavours an element can need (Eigen packet psin/pcos, v = 1; glibc scalar sinf/cosf, v = 0), gives
+// every grid element's sphere point bit-identically -- the same functions of the same arguments,
+// computed once per sequence instead of twice per element (the north star's shared spherical trig).
+// Layout: trig_col[(v * cols + i) * 2 + {0: sin, 1: cos}] of phi, trig_row likewise of theta.
 struct MpaCache {
   const float* px[3];
   const float* py[3];
   const uint8_t* vip[3];
   int cols, rows;  // W/4, H/4
+  const float* trig_col;
+  const float* trig_row;
 };
+
+// One entry of the separable toSphere table (t over 2 * cols column entries, then 2 * rows rows)
+MM_HD void erp_trig_thread(int t, const SeqConst& sc, int cols, int rows, float* col, float* row) {
+  if (t < 2 * cols) {
+    const int v = t >= cols ? 1 : 0, i = t - v * cols;
+    const float ph = erp_phi(4.0f * (float)i + sc.off, sc);
+    const Math m{v};
+    col[2 * t] = m.sin(ph);
+    col[2 * t + 1] = m.cos(ph);
+    return;
+  }
+  t -= 2 * cols;
+  if (t >= 2 * rows) return;
+  const int v = t >= rows ? 1 : 0, j = t - v * rows;
+  const float th = erp_theta(4.0f * (float)j + sc.off, sc);
+  const Math m{v};
+  row[2 * t] = m.sin(th);
+  row[2 * t + 1] = m.cos(th);
+}
+
+// toSphere of frame-grid element (column gi, row gj) from the table
+MM_HD V3 grid_sphere(const MpaCache& c, int gi, int gj, bool packet) {
+  const int v = packet ? 1 : 0;
+  const float* pc = c.trig_col + 2 * (v * c.cols + gi);
+  const float* pr = c.trig_row + 2 * (v * c.rows + gj);
+  return sph_from_trig(pr[0], pr[1], pc[0], pc[1]);
+}
+MM_HD bool is_mpa_model(int m) { return m >= MPA_FRONT_BACK && m <= MPA_TOP_BOTTOM; }
 
 struct Geometry {
   int W, H, Wc, Hc;
@@ -173,8 +215,15 @@ MM_HD void reproj_thread_mc(int g, int ji, const SeqConst& sc, const JobDev* job
     py = cache.py[pl][ci];
     vip = cache.vip[pl][ci] != 0;
   }
+  const bool packet = packet_lane(eig, j.n);
+  V3 pg;
+  const V3* pgp = nullptr;
+  if (!is_mpa_model(j.model) && cache.trig_col) {
+    pg = grid_sphere(cache, (j.x >> 2) + col, (j.y >> 2) + row, packet);
+    pgp = &pg;
+  }
   int32_t fx, fy;
-  reproject_element(sc, setups[ji], gx, gy, packet_lane(eig, j.n), mpa_cached, px, py, vip, j.comp ? 1 : 0, &fx, &fy);
+  reproject_element(sc, setups[ji], gx, gy, packet, mpa_cached, px, py, vip, j.comp ? 1 : 0, &fx, &fy, pgp);
   // chroma 2x2 sub-block (row, col) belongs to luma 4x4 sub-block (row, col) of the same PU
   const int sb = j.sb_base + row * j.pu_cols + col;
   mm_int4* rec = &mc.pos[j.list][sb];
@@ -232,9 +281,15 @@ MM_HD void reproj_thread(int g, int ji, const SeqConst& sc, const JobDev* jobs, 
     py = cache.py[pl][ci];
     vip = cache.vip[pl][ci] != 0;
   }
+  const bool packet = packet_lane(local, j.n);
+  V3 pg;
+  const V3* pgp = nullptr;
+  if (!is_mpa_model(j.model) && cache.trig_col) {
+    pg = grid_sphere(cache, (j.x >> 2) + col, (j.y >> 2) + row, packet);
+    pgp = &pg;
+  }
   int32_t fx, fy;
-  reproject_element(sc, setups[ji], gx, gy, packet_lane(local, j.n), mpa_cached, px, py, vip, j.comp ? 1 : 0, &fx,
-                    &fy);
+  reproject_element(sc, setups[ji], gx, gy, packet, mpa_cached, px, py, vip, j.comp ? 1 : 0, &fx, &fy, pgp);
   out_xy[2 * (j.offset + local)] = fx;
   out_xy[2 * (j.offset + local) + 1] = fy;
 }
@@ -273,31 +328,36 @@ MM_HD int16_t weighted_avg(int p0, int p1, int w0, int w1, int bd) {
 }
 
 // One luma 4x4 sub-block and its two 4:2:0 chroma 2x2 sub-blocks from the McRec records (device-
-// planned pictures): for each used list, xPredInterBlkMM's per-sub-block dispatch
-// (InterPrediction.cpp:776-828), then xWeightedAverage (addAvg / addWeightedAvg for bi, the
-// rndRes uni prediction otherwise, InterPrediction.cpp:1584-1679).  cls = 0 bi, 1 uni L0, 2 uni
-// L1 (sb_class of g's PU bucket).  geo.hp (mm_pred_list): the 14-bit intermediate of the one list.
-// BI / HP are compile-time (mc_thread_rec dispatches on the wave-uniform class), so the bi path
-// carries no clipping and the uni path no runtime rounding-mode selects.
-template <bool BI, bool HP>
-MM_HD void mc_rec_impl(int g, int cls, const Geometry& geo, const Taps& taps, const McRec& mc, const RefDev* refs,
+// planned pictures): for each list the sub-block uses, xPredInterBlkMM's per-sub-block dispatch
+// (InterPrediction.cpp:776-828) at the 14-bit intermediate (bi = true), then xWeightedAverage
+// (InterPrediction.cpp:1584-1679): addAvg / addWeightedAvg of the two lists for bi, and for uni the
+// rndRes prediction -- which equals weighted_avg(p, *, 8, 0) of the list's 14-bit prediction p
+// exactly (both are floor((p + 2^(h-1) + 2^13) / 2^h) clipped, h = IF_INTERNAL_FRAC_BITS: the uni
+// V pass's offset is a multiple of 2^6, so its single shift equals the 14-bit shift followed by
+// this one; tests/test_filter_identity.py).  So bi and uni sub-blocks share one body and a wave may
+// hold both (k_mc's waves follow the picture's spatial order, not PU classes); a list no lane of
+// the wave uses is skipped as a whole.
+// HP (mm_pred_list hp = 1): every sub-block uses one list and keeps its 14-bit prediction.
+template <bool HP>
+MM_HD void mc_rec_impl(int g, const Geometry& geo, const Taps& taps, const McRec& mc, const RefDev* refs,
                        int16_t* dst_y, int dsy, int16_t* dst_cb, int16_t* dst_cr, int dsc) {
-  constexpr bool bi = BI;
-  constexpr bool hp = HP;  // keep the 14-bit intermediate (rndRes = !bi)
-  const int uni_list = cls == 2 ? 1 : 0;
-  const bool used[2] = {bi || uni_list == 0, bi || uni_list == 1};
   const mm_int2 meta = mc.meta[g];
+  const bool used[2] = {(meta.y & MM_META_USE0) != 0, (meta.y & MM_META_USE1) != 0};
   mm_int4 P[2];
 #pragma unroll
   for (int l = 0; l < 2; l++)
     if (used[l]) P[l] = mc.pos[l][g];
   const int ox = meta.x & 0xffff, oy = meta.x >> 16;
   const int slot[2] = {meta.y & 15, (meta.y >> 4) & 15};
-  const int w1 = bcw_w1((meta.y >> 8) & 7), w0 = 8 - w1;
+  const bool bi = used[0] && used[1];
+  // bi: (w0, w1) of the BCW index; uni: the list's prediction with weight 8 (see above)
+  const int w1b = bcw_w1((meta.y >> 8) & 7);
+  const int wa = bi ? 8 - w1b : 8, wb = bi ? w1b : 0;
   if (geo.store & 1) {
     int16_t pl[2][16];
 #pragma unroll
     for (int l = 0; l < 2; l++) {
+      for (int i = 0; i < 16; i++) pl[l][i] = 0;
       if (!used[l]) continue;
       const int32_t fx = P[l].x, fy = P[l].y;
       const int xPos = fx >> 4, yPos = fy >> 4, xFrac = fx & 15, yFrac = fy & 15;
@@ -307,24 +367,26 @@ MM_HD void mc_rec_impl(int g, int cls, const Geometry& geo, const Taps& taps, co
 #if defined(__HIP_DEVICE_COMPILE__)
       } else if (geo.padded || window_interior<8, 4, 4>(xPos, yPos, geo.W, geo.H)) {
         predict_subblock_pool<8, 4, 4>(taps.pool, r.off_y, 0, r.stride_y, xPos, yPos, taps.packed->lh[xFrac][(xPos - 3) & 1],
-                                       taps.packed->lv[yFrac], hp, geo.bd, pl[l]);
+                                       taps.packed->lv[yFrac], true, geo.bd, pl[l]);
 #else
       } else if (window_interior<8, 4, 4>(xPos, yPos, geo.W, geo.H)) {
-        predict_subblock_interior<8, 4, 4>(r.y, r.stride_y, xPos, yPos, taps.luma[xFrac], taps.luma[yFrac], hp,
+        predict_subblock_interior<8, 4, 4>(r.y, r.stride_y, xPos, yPos, taps.luma[xFrac], taps.luma[yFrac], true,
                                            geo.bd, pl[l]);
 #endif
       } else {
-        predict_subblock<8, 4, 4>(r.y, r.stride_y, geo.W, geo.H, xPos, yPos, taps.luma[xFrac], taps.luma[yFrac], hp,
+        predict_subblock<8, 4, 4>(r.y, r.stride_y, geo.W, geo.H, xPos, yPos, taps.luma[xFrac], taps.luma[yFrac], true,
                                   geo.bd, pl[l]);
       }
     }
+    const int pa = used[0] ? 0 : 1;  // uni L1: the list-1 prediction takes the first weight
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       int16_t o[4];
 #pragma unroll
       for (int c = 0; c < 4; c++) {
         const int i = r * 4 + c;
-        o[c] = bi ? weighted_avg(pl[0][i], pl[1][i], w0, w1, geo.bd) : pl[uni_list][i];
+        const int a = pa ? pl[1][i] : pl[0][i];
+        o[c] = HP ? (int16_t)a : weighted_avg(a, pl[1][i], wa, wb, geo.bd);
       }
       store_row<4>(dst_y + (long)(oy + r) * dsy + ox, o, geo.vec_store);
     }
@@ -333,6 +395,7 @@ MM_HD void mc_rec_impl(int g, int cls, const Geometry& geo, const Taps& taps, co
   int16_t pcb[2][4], pcr[2][4];
 #pragma unroll
   for (int l = 0; l < 2; l++) {
+    for (int i = 0; i < 4; i++) pcb[l][i] = pcr[l][i] = 0;
     if (!used[l]) continue;
     const int32_t fx = P[l].z, fy = P[l].w;
     const int xPos = fx >> 5, yPos = fy >> 5, xFrac = fx & 31, yFrac = fy & 31;
@@ -343,23 +406,24 @@ MM_HD void mc_rec_impl(int g, int cls, const Geometry& geo, const Taps& taps, co
     } else if (geo.padded || window_interior<4, 2, 2>(xPos, yPos, geo.Wc, geo.Hc)) {
       const uint32_t* ht = taps.packed->ch[xFrac][(xPos - 1) & 1];
       const uint32_t* vt = taps.packed->cv[yFrac];
-      predict_subblock_pool<4, 2, 2>(taps.pool, r.off_cb, 0, r.stride_c, xPos, yPos, ht, vt, hp, geo.bd, pcb[l]);
-      predict_subblock_pool<4, 2, 2>(taps.pool, r.off_cb, taps.pool.cr_delta, r.stride_c, xPos, yPos, ht, vt, hp, geo.bd,
-                                     pcr[l]);
+      predict_subblock_pool<4, 2, 2>(taps.pool, r.off_cb, 0, r.stride_c, xPos, yPos, ht, vt, true, geo.bd, pcb[l]);
+      predict_subblock_pool<4, 2, 2>(taps.pool, r.off_cb, taps.pool.cr_delta, r.stride_c, xPos, yPos, ht, vt, true,
+                                     geo.bd, pcr[l]);
 #else
     } else if (window_interior<4, 2, 2>(xPos, yPos, geo.Wc, geo.Hc)) {
-      predict_subblock_interior<4, 2, 2>(r.cb, r.stride_c, xPos, yPos, taps.chroma[xFrac], taps.chroma[yFrac], hp,
+      predict_subblock_interior<4, 2, 2>(r.cb, r.stride_c, xPos, yPos, taps.chroma[xFrac], taps.chroma[yFrac], true,
                                          geo.bd, pcb[l]);
-      predict_subblock_interior<4, 2, 2>(r.cr, r.stride_c, xPos, yPos, taps.chroma[xFrac], taps.chroma[yFrac], hp,
+      predict_subblock_interior<4, 2, 2>(r.cr, r.stride_c, xPos, yPos, taps.chroma[xFrac], taps.chroma[yFrac], true,
                                          geo.bd, pcr[l]);
 #endif
     } else {
       predict_subblock<4, 2, 2>(r.cb, r.stride_c, geo.Wc, geo.Hc, xPos, yPos, taps.chroma[xFrac], taps.chroma[yFrac],
-                                hp, geo.bd, pcb[l]);
+                                true, geo.bd, pcb[l]);
       predict_subblock<4, 2, 2>(r.cr, r.stride_c, geo.Wc, geo.Hc, xPos, yPos, taps.chroma[xFrac], taps.chroma[yFrac],
-                                hp, geo.bd, pcr[l]);
+                                true, geo.bd, pcr[l]);
     }
   }
+  const int pa = used[0] ? 0 : 1;
   const int cx = ox >> 1, cy = oy >> 1;
 #pragma unroll
   for (int r = 0; r < 2; r++) {
@@ -367,8 +431,9 @@ MM_HD void mc_rec_impl(int g, int cls, const Geometry& geo, const Taps& taps, co
 #pragma unroll
     for (int c = 0; c < 2; c++) {
       const int i = r * 2 + c;
-      ob[c] = bi ? weighted_avg(pcb[0][i], pcb[1][i], w0, w1, geo.bd) : pcb[uni_list][i];
-      orr[c] = bi ? weighted_avg(pcr[0][i], pcr[1][i], w0, w1, geo.bd) : pcr[uni_list][i];
+      const int ab = pa ? pcb[1][i] : pcb[0][i], ar = pa ? pcr[1][i] : pcr[0][i];
+      ob[c] = HP ? (int16_t)ab : weighted_avg(ab, pcb[1][i], wa, wb, geo.bd);
+      orr[c] = HP ? (int16_t)ar : weighted_avg(ar, pcr[1][i], wa, wb, geo.bd);
     }
     store_row<2>(dst_cb + (long)(cy + r) * dsc + cx, ob, geo.vec_store);
     store_row<2>(dst_cr + (long)(cy + r) * dsc + cx, orr, geo.vec_store);
@@ -378,14 +443,9 @@ MM_HD void mc_rec_impl(int g, int cls, const Geometry& geo, const Taps& taps, co
 // UNI_HP: mm_pred_list with hp = 1 (every sub-block is uni and keeps the 14-bit intermediate);
 // a separate kernel instance, so the picture path's register allocation does not carry it.
 template <bool UNI_HP = false>
-MM_HD void mc_thread_rec(int g, int cls, const Geometry& geo, const Taps& taps, const McRec& mc, const RefDev* refs,
+MM_HD void mc_thread_rec(int g, const Geometry& geo, const Taps& taps, const McRec& mc, const RefDev* refs,
                          int16_t* dst_y, int dsy, int16_t* dst_cb, int16_t* dst_cr, int dsc) {
-  if constexpr (UNI_HP)
-    mc_rec_impl<false, true>(g, cls, geo, taps, mc, refs, dst_y, dsy, dst_cb, dst_cr, dsc);
-  else if (cls == 0)
-    mc_rec_impl<true, true>(g, cls, geo, taps, mc, refs, dst_y, dsy, dst_cb, dst_cr, dsc);
-  else
-    mc_rec_impl<false, false>(g, cls, geo, taps, mc, refs, dst_y, dsy, dst_cb, dst_cr, dsc);
+  mc_rec_impl<UNI_HP>(g, geo, taps, mc, refs, dst_y, dsy, dst_cb, dst_cr, dsc);
 }
 
 }  // namespace mmpipe

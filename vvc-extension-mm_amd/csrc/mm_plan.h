@@ -137,9 +137,12 @@ class Planner {
       if (b.comp < 0 || b.comp > 2 || (b.comp > 0 && !seq_.chroma)) return fail(MM_ERR_ARG, "invalid component");
       const int cs = b.comp ? 1 : 0, sb = b.comp ? 2 : 4;
       const int Wc = seq_.W >> cs, Hc = seq_.H >> cs;
-      if (b.w <= 0 || b.h <= 0 || b.w % sb || b.h % sb || b.x < 0 || b.y < 0 || b.x % sb || b.y % sb ||
-          b.x + b.w > Wc || b.y + b.h > Hc)
-        return fail(MM_ERR_ARG, "block " + std::to_string(i) + " outside the picture or off the sub-block grid");
+      // JobDev stores block sizes in 8 bits and element counts in 16 bits: a block is at most one
+      // CTU (128 x 128 luma, VVC's MAX_CU_SIZE) in component units, as every VVC PU is
+      if (b.w <= 0 || b.h <= 0 || b.w > 128 || b.h > 128 || b.w % sb || b.h % sb || b.x < 0 || b.y < 0 ||
+          b.x % sb || b.y % sb || b.x + b.w > Wc || b.y + b.h > Hc)
+        return fail(MM_ERR_ARG, "block " + std::to_string(i) +
+                                    " outside the picture, off the sub-block grid or larger than 128x128");
       rc = add_job(b.x << cs, b.y << cs, b.w, b.h, b.comp ? 1 : 0, b.model, b.mv_hor, b.mv_ver, b.cur_poc, b.ref_poc);
       if (rc) return rc;
     }
@@ -292,142 +295,19 @@ inline int plan_me_window(const SeqInfo& s, const mmdev::PicTables& t, const mm_
   return MM_OK;
 }
 
-// ---- MM-DMVR (mm_pred_dmvr) -------------------------------------------------------------------
-// Sub-PUs of min(w,16) x min(h,16) in the reference's raster order (InterPrediction.cpp:2481-2484)
-// for PUs that satisfy the parts of PU::checkDMVRCondition the descriptors carry (bi, equal
-// models, w >= 8, h >= 8, w*h >= 128; UnitTools.cpp:1698-1726) -- the rest of the condition
-// (merge mode, equal POC distances, weights) is the caller's decision.
-struct DmvrPlan {
-  std::vector<mmdmvr::SubPuDev> sub;
-  std::vector<int> off, chunk;  // cost-element offsets per sub-PU, 64-element chunk starts
-  long n_elems = 0;
-};
-
-inline int plan_dmvr(const SeqInfo& s, const mmdev::PicTables& t, const mm_pu_desc* pus, int n, DmvrPlan* p,
-                     std::string* err) {
-  *p = DmvrPlan();
-  for (int i = 0; i < n; i++) {
-    const mm_pu_desc& u = pus[i];
-    if (u.w < 8 || u.h < 8 || u.w * u.h < 128 || u.w > 128 || u.h > 128 || (u.w & 3) || (u.h & 3) ||
-        (u.w > 16 && (u.w & 15)) || (u.h > 16 && (u.h & 15)) || (u.x & 3) ||
-        (u.y & 3) || u.x < 0 || u.y < 0 || u.x > s.W - u.w || u.y > s.H - u.h || u.ref_poc[0] < 0 || u.ref_poc[1] < 0 ||
-        u.model[0] != u.model[1] || u.bcw_idx != MM_BCW_DEFAULT) {
-      *err = "DMVR PU " + std::to_string(i) +
-             ": needs bi prediction, equal models, BCW_DEFAULT and w, h >= 8, w*h >= 128 (PU::checkDMVRCondition)";
-      return MM_ERR_ARG;
-    }
-    const int m = u.model[0];
-    if (m <= CLASSIC || m >= NUM_MODELS || !(t.active & (1u << m))) {
-      *err = "DMVR PU " + std::to_string(i) + ": invalid, CLASSIC or inactive motion model";
-      return MM_ERR_MODEL;
-    }
-    mmdmvr::SubPuDev base{};
-    for (int l = 0; l < 2; l++) {
-      int slot = -1;
-      for (int k = 0; k < t.n_slots; k++)
-        if (t.poc[k] == u.ref_poc[l]) slot = k;
-      if (slot < 0) {
-        *err = "DMVR PU " + std::to_string(i) + ": reference POC " + std::to_string(u.ref_poc[l]) + " not uploaded";
-        return MM_ERR_NOREF;
-      }
-      base.slot[l] = slot;
-      base.ref_poc[l] = u.ref_poc[l];
-      base.mv[l][0] = u.mv[l][0];
-      base.mv[l][1] = u.mv[l][1];
-      base.ged_idx[l] = -1;
-      if (m == GEODESIC_CAMPOSE) {
-        if (t.ged_cam[slot] < 0) {
-          *err = "DMVR PU " + std::to_string(i) + ": no epipole for (curPOC, refPOC)";
-          return MM_ERR_NOEPIPOLE;
-        }
-        base.ged_idx[l] = t.ged_cam[slot];
-      } else if (m >= GEODESIC_X && m <= GEODESIC_Z) {
-        base.ged_idx[l] = m - GEODESIC_X;
-      }
-    }
-    base.model = m;
-    const int dx = std::min(u.w, 16), dy = std::min(u.h, 16);
-    for (int y = u.y; y < u.y + u.h; y += dy)
-      for (int x = u.x; x < u.x + u.w; x += dx) {
-        mmdmvr::SubPuDev d = base;
-        d.x = x;
-        d.y = y;
-        d.w = dx;
-        d.h = dy;
-        d.n = (dx / 4) * (dy / 4);
-        d.rows = dy / 4;
-        d.elem_off = (int)p->n_elems;
-        p->off.push_back(d.elem_off);
-        p->n_elems += (long)mmdmvr::N_OFF * d.n;
-        p->sub.push_back(d);
-      }
-  }
-  if (p->n_elems >= (1L << 31)) {
-    *err = "DMVR list too large for one call";
-    return MM_ERR_ARG;
-  }
-  build_chunks(p->off, (int)p->n_elems, &p->chunk);
-  return MM_OK;
-}
-
-// ---- MM-MVP (mm_mvp_convert) -------------------------------------------------------------------
-// Validates the queries (models active; CLASSIC is always active) and resolves the GED rotations
-// of both sides: fixed epipoles for GEODESIC_X/Y/Z, EpipoleList::findEpipole for CAMPOSE.
-inline int plan_mvp(const SeqInfo& s, const EpipoleMap& epi, const mm_mvp_query* q, int n,
-                    std::vector<mmmvp::MvpQueryDev>* out, std::vector<M3>* ged, std::string* err) {
+// ---- MM-MVP (mm_mvp_convert[_device]) ------------------------------------------------------------
+// The available entries of an EpipoleList in key order: the device table the MVP kernel resolves
+// GEODESIC_CAMPOSE epipoles from (mmmvp::epi_find).
+inline void epi_entries(const EpipoleMap& epi, std::vector<mmmvp::EpiDev>* out) {
   out->clear();
-  ged->clear();
-  const V3 fixed[3] = {{1.0f, 0.0f, 0.0f}, {0.0f, 1.0f, 0.0f}, {0.0f, 0.0f, 1.0f}};
-  for (int i = 0; i < 3; i++) ged->push_back(ged_rotation(fixed[i]));
-  std::map<std::array<int32_t, 3>, int> cam;
-  auto resolve = [&](int model, int cur, int ref, int* idx, std::array<int32_t, 3>* e) -> int {
-    *idx = -1;
-    if (model >= GEODESIC_X && model <= GEODESIC_Z) *idx = model - GEODESIC_X;
-    if (model != GEODESIC_CAMPOSE) return MM_OK;
-    if (!find_epipole(epi, cur, ref, e)) return MM_ERR_NOEPIPOLE;
-    auto it = cam.find(*e);
-    if (it == cam.end()) {
-      V3 v = {fixed_to_float((*e)[0], 24), fixed_to_float((*e)[1], 24), fixed_to_float((*e)[2], 24)};
-      ged->push_back(ged_rotation(v));
-      it = cam.emplace(*e, (int)ged->size() - 1).first;
-    }
-    *idx = it->second;
-    return MM_OK;
-  };
-  for (int i = 0; i < n; i++) {
-    const mm_mvp_query& x = q[i];
-    for (int m : {x.model_orig, x.model_desired})
-      if (m < CLASSIC || m >= NUM_MODELS || !((s.prm.active_models | 1u) & (1u << m))) {
-        *err = "MVP query " + std::to_string(i) + ": invalid or inactive motion model";
-        return MM_ERR_MODEL;
-      }
-    if (x.shift_hor < 0 || x.shift_hor > 8 || x.shift_ver < 0 || x.shift_ver > 8 || x.cand_w <= 0 || x.cand_h <= 0 ||
-        x.cur_w <= 0 || x.cur_h <= 0) {
-      *err = "MVP query " + std::to_string(i) + ": invalid precision or block size";
-      return MM_ERR_ARG;
-    }
-    mmmvp::MvpQueryDev d;
-    d.q = x;
-    std::array<int32_t, 3> eo{}, ed{};
-    int rc = resolve(x.model_orig, x.cur_poc_orig, x.ref_poc_orig, &d.ged_orig, &eo);
-    if (!rc) rc = resolve(x.model_desired, x.cur_poc_desired, x.ref_poc_desired, &d.ged_desired, &ed);
-    // the early return compares the two CAMPOSE epipoles (MVReprojection.cpp:177-181); only
-    // evaluated there when both models are GEODESIC_CAMPOSE
-    d.same_epipole = 0;
-    if (x.model_orig == GEODESIC_CAMPOSE && x.model_desired == GEODESIC_CAMPOSE && !rc) d.same_epipole = eo == ed;
-    if (rc) {
-      // a missing epipole only matters when the conversion reaches the model (zero MVs and equal
-      // non-GED models return before)
-      const bool needed = !(x.mv_hor == 0 && x.mv_ver == 0);
-      if (needed) {
-        *err = "MVP query " + std::to_string(i) + ": no epipole for (curPOC, refPOC)";
-        return MM_ERR_NOEPIPOLE;
-      }
-      d.ged_orig = d.ged_desired = -1;
-    }
-    out->push_back(d);
+  for (const auto& kv : epi.entries()) {
+    if (!kv.second.available) continue;
+    mmmvp::EpiDev e;
+    e.cur = kv.first.first;
+    e.ref = kv.first.second;
+    for (int i = 0; i < 3; i++) e.q[i] = kv.second.q[i];
+    out->push_back(e);
   }
-  return MM_OK;
 }
 
 }  // namespace mmplan

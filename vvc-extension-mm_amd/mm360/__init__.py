@@ -53,7 +53,7 @@ EXPORTED_SYMBOLS = (
     "mm_set_stage_timing", "mm_last_stage_timing", "mm_upload_org", "mm_sad_window", "mm_pred_dmvr", "mm_mvp_convert",
     "mm_set_stripes", "mm_set_plan_ahead", "mm_pred_list", "mm_derive_effective_blocks", "mm_epipole_list_create",
     "mm_epipole_list_destroy", "mm_get_epipole_list", "mm_epipole_add", "mm_epipole_make_available", "mm_epipole_has",
-    "mm_epipole_find", "mm_epipole_derive_predictor", "mm_epipole_count",
+    "mm_epipole_find", "mm_epipole_derive_predictor", "mm_epipole_count", "mm_mvp_convert_device", "mm_mvp_status", "mm_set_dmvr",
 )
 
 BCW_DEFAULT = 2  # CommonDef.h:348-349; g_BcwWeights = {-2, 3, 4, 5, 10} (Rom.cpp:203)
@@ -81,7 +81,7 @@ BLOCK_DTYPE = np.dtype([("x", "<i4"), ("y", "<i4"), ("w", "<i4"), ("h", "<i4"), 
                         ("ref_poc", "<i4")])
 PU_DTYPE = np.dtype([("x", "<i4"), ("y", "<i4"), ("w", "<i4"), ("h", "<i4"), ("mv", "<i4", (2, 2)),
                      ("ref_poc", "<i4", (2,)), ("model", "<i4", (2,)), ("bcw_idx", "<i4"),
-                     ("reserved", "<i4", (3,))])
+                     ("flags", "<u4"), ("reserved", "<i4", (2,))])
 ME_BLOCK_DTYPE = np.dtype([("x", "<i4"), ("y", "<i4"), ("w", "<i4"), ("h", "<i4"), ("mv_hor", "<i4"),
                            ("mv_ver", "<i4"), ("model", "<i4"), ("ref_poc", "<i4"), ("sub_shift", "<i4")])
 MVP_QUERY_DTYPE = np.dtype([(n, "<i4") for n in (
@@ -97,6 +97,7 @@ assert PU_MOTION_DTYPE.itemsize == 80
 # MM_PU_* flags (include/mm360.h)
 PU_MERGE, PU_SUBPU, PU_CIIP, PU_SMVD, PU_MMVD, PU_MVREFINE = 0x1, 0x2, 0x4, 0x8, 0x10, 0x20
 PU_WEIGHTED, PU_LONGTERM, PU_REF_SCALED, PU_MMVD_ENC2 = 0x40, 0x80, 0x100, 0x200
+PUF_DMVR = 0x1  # mm_pu_desc.flags: MM_PUF_DMVR
 
 
 class ToolFlags(ctypes.Structure):
@@ -162,6 +163,9 @@ def load_library() -> ctypes.CDLL:
         "mm_set_stage_timing": (c_int, [vp, c_int]),
         "mm_upload_org": (c_int, [vp, c_int, vp, ctypes.c_ssize_t, c_int]),
         "mm_mvp_convert": (c_int, [vp, vp, c_int, vp]),
+        "mm_mvp_convert_device": (c_int, [vp, vp, c_int, vp]),
+        "mm_mvp_status": (c_int, [vp, POINTER(c_int)]),
+        "mm_set_dmvr": (c_int, [vp, c_int]),
         "mm_pred_dmvr": (c_int, [vp, c_int, vp, c_int, vp, ctypes.c_ssize_t, vp, vp, ctypes.c_ssize_t, vp]),
         "mm_sad_window": (c_int, [vp, c_int, vp, c_int, c_int, c_int, vp]),
         "mm_last_stage_timing": (c_int, [vp, POINTER(c_float)]),
@@ -270,6 +274,14 @@ def pus_to_device(pus: np.ndarray, device: int = 0):
     import torch
     pus = np.ascontiguousarray(pus, dtype=PU_DTYPE)
     words = pus.view(np.int32).reshape(len(pus), PU_DTYPE.itemsize // 4)
+    return torch.from_numpy(words.copy()).to(f"cuda:{device}")
+
+
+def queries_to_device(q: np.ndarray, device: int = 0):
+    """Copy an MVP_QUERY_DTYPE array into device memory (int32 CUDA tensor, 20 words per query)."""
+    import torch
+    q = np.ascontiguousarray(q, dtype=MVP_QUERY_DTYPE)
+    words = q.view(np.int32).reshape(len(q), MVP_QUERY_DTYPE.itemsize // 4)
     return torch.from_numpy(words.copy()).to(f"cuda:{device}")
 
 
@@ -395,6 +407,20 @@ class MMContext:
         self._check(self.lib.mm_mvp_convert(self.h, c_void_p(q.ctypes.data), len(q), c_void_p(out.ctypes.data)))
         return out[:len(q)]
 
+    def mvp_convert_device(self, d_queries, d_out):
+        """mm_mvp_convert_device: `d_queries` a CUDA tensor of MVP_QUERY_DTYPE records (e.g.
+        queries_to_device(q)), `d_out` an int32 CUDA tensor of 2 words per query.  Asynchronous on
+        the context stream; errors surface at mvp_status() / synchronize()."""
+        n = d_queries.numel() * d_queries.element_size() // MVP_QUERY_DTYPE.itemsize
+        import torch
+        assert d_out.numel() >= 2 * n and d_out.dtype == torch.int32
+        self._check(self.lib.mm_mvp_convert_device(self.h, c_void_p(_ptr(d_queries)), n, c_void_p(_ptr(d_out))))
+
+    def mvp_status(self):
+        """(code, first failing query) of the last mm_mvp_convert_device; raises MMError on failure."""
+        bad = c_int(-1)
+        self._check(self.lib.mm_mvp_status(self.h, ctypes.byref(bad)))
+
     def predict_dmvr(self, cur_poc: int, pus: np.ndarray, dst_y, dst_cb=None, dst_cr=None) -> np.ndarray:
         """MM-DMVR PUs (xProcessDMVRProjected): refined bi prediction into the device planes;
         returns the L0 MV delta (1/16 luma) of every <= 16x16 sub-PU, PU after PU, raster order."""
@@ -453,6 +479,11 @@ class MMContext:
         ms = c_float()
         self._check(self.lib.mm_last_timing(self.h, byref(ms)))
         return float(ms.value)
+
+    def set_dmvr(self, on: bool):
+        """mm_set_dmvr: the picture's DMVR enable -- MM_PUF_DMVR PUs of mm_pred_device lists run
+        the MM-DMVR search inside the launch sequence."""
+        self._check(self.lib.mm_set_dmvr(self.h, int(on)))
 
     def set_stage_timing(self, on: bool):
         self._check(self.lib.mm_set_stage_timing(self.h, int(on)))

@@ -101,10 +101,18 @@ def _split_ctu(rng, x0, y0, w, h, out):
             out += [(x0, y0, 8, 4), (x0, y0 + 4, 8, 4)]
 
 
-def pu_list(cfg: Config, frame: int = 0, uniform: bool = False, uniform_model: int = None,
-            ctu: int = 128) -> np.ndarray:
-    """Per-picture PU list (after the host's sub-PU split), PU_DTYPE."""
+def decoded_pus(cfg: Config, frame: int = 0, uniform: bool = False, uniform_model: int = None, ctu: int = 128,
+                dmvr_share: float = 0.0):
+    """The decoded PUs of a synthetic picture (PU_MOTION_DTYPE) and the picture's tool switches:
+    one record per leaf of the seeded CTU split, with its motion and the flags the decoder would
+    carry.  BDOF is on (RA cfg, cfg/encoder_randomaccess_vtm.cfg:139); DMVR is on only when
+    `dmvr_share` > 0, and then that share of the DMVR-eligible bi leaves (w, h >= 8, w * h >= 128)
+    is a merge PU with mvRefine and one model for both lists (PU::checkDMVRCondition requires
+    equal models, UnitTools.cpp:1715).  The DMVR decisions draw from their own seeded stream, so
+    the workload without DMVR does not change."""
+    from . import PU_MERGE, PU_MOTION_DTYPE, PU_MVREFINE, ToolFlags
     rng = np.random.default_rng(0x4D4D1000 + 977 * frame + cfg.width)
+    rng_d = np.random.default_rng(0x4D4D5000 + 977 * frame + cfg.width)
     models = cfg.models
     leaves: List[Tuple[int, int, int, int]] = []
     if uniform:
@@ -115,8 +123,11 @@ def pu_list(cfg: Config, frame: int = 0, uniform: bool = False, uniform_model: i
         for y0 in range(0, cfg.height, ctu):
             for x0 in range(0, cfg.width, ctu):
                 _split_ctu(rng, x0, y0, min(ctu, cfg.width - x0), min(ctu, cfg.height - y0), leaves)
-    rows = []
-    for (x, y, w, h) in leaves:
+    out = np.zeros(len(leaves), dtype=PU_MOTION_DTYPE)
+    out["pu"]["bcw_idx"] = 2  # BCW_DEFAULT
+    out["cur_poc"] = CUR_POC
+    out["sub_motion"] = -1
+    for i, (x, y, w, h) in enumerate(leaves):
         small = (w * h) < 64  # 8x4 / 4x8: uni only
         bi = (not small) and rng.random() < 0.6
         if uniform:
@@ -133,20 +144,39 @@ def pu_list(cfg: Config, frame: int = 0, uniform: bool = False, uniform_model: i
         else:
             lst = int(rng.integers(0, 2))
             refs = (REF_POCS[0], -1) if lst == 0 else (-1, REF_POCS[1])
-        if bi and (w > 16 or h > 16):
-            sw, sh = min(16, w), min(16, h)
-            for yy in range(y, y + h, sh):
-                for xx in range(x, x + w, sw):
-                    rows.append((xx, yy, sw, sh, mvs, refs, (m0, m1)))
-        else:
-            rows.append((x, y, w, h, mvs, refs, (m0, m1)))
-    out = new_pus(len(rows))
-    for i, (x, y, w, h, mvs, refs, ms) in enumerate(rows):
-        out[i]["x"], out[i]["y"], out[i]["w"], out[i]["h"] = x, y, w, h
-        out[i]["mv"] = np.array(mvs, dtype=np.int32)
-        out[i]["ref_poc"] = refs
-        out[i]["model"] = ms
-    return out
+        if dmvr_share > 0 and bi and w >= 8 and h >= 8 and w * h >= 128 and rng_d.random() < dmvr_share:
+            m1 = m0
+            out[i]["flags"] = PU_MERGE | PU_MVREFINE
+        u = out[i]["pu"]
+        u["x"], u["y"], u["w"], u["h"] = x, y, w, h
+        u["mv"] = np.array(mvs, dtype=np.int32)
+        u["ref_poc"] = refs
+        u["model"] = (m0, m1)
+    tools = ToolFlags(bdof=1, dmvr=1 if dmvr_share > 0 else 0, bcw=1, wp_bi=0)
+    return out, tools
+
+
+def pu_list(cfg: Config, frame: int = 0, uniform: bool = False, uniform_model: int = None,
+            ctu: int = 128, dmvr_share: float = 0.0) -> np.ndarray:
+    """Per-picture PU list, PU_DTYPE: the decoded PUs (decoded_pus) through the product's
+    effective-block derivation (mm_derive_effective_blocks = InterPrediction::motionCompensation's
+    control flow, InterPrediction.cpp:1681-1810): bi PUs wider or taller than 16 become 16x16
+    sub-PUs by the BDOF pre-check (xSubPuBio).  With a DMVR share, the DMVR PUs follow the rest,
+    flagged MM_PUF_DMVR (mm_pred_device runs their search; mm_set_dmvr must be on)."""
+    from . import PUF_DMVR, derive_effective_blocks
+    dec, tools = decoded_pus(cfg, frame, uniform, uniform_model, ctu, dmvr_share)
+    mc, dmvr = derive_effective_blocks(tools, dec)
+    if len(dmvr):
+        dmvr = dmvr.copy()
+        dmvr["flags"] |= PUF_DMVR
+        return np.concatenate([mc, dmvr])
+    return mc
+
+
+def dmvr_flagged(pus: np.ndarray) -> np.ndarray:
+    """Mask of the MM_PUF_DMVR PUs of a list."""
+    from . import PUF_DMVR
+    return (pus["flags"] & PUF_DMVR) != 0
 
 
 def luma_area(pus: np.ndarray) -> int:
