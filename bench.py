@@ -73,7 +73,9 @@ def host_info(threads):
     except OSError:
         pass
     libc = " ".join(platform.libc_ver())
-    return {"cpu_model": model, "nproc": os.cpu_count(), "threads_available": threads, "glibc": libc}
+    return {"cpu_model": model, "nproc": os.cpu_count(), "threads_available": threads, "glibc": libc,
+            "threads_note": "the all-threads leg uses one GPU's share of the GPU box's host (16 threads per "
+                            "GPU), not the whole machine"}
 
 
 def cpu_threads():
@@ -178,6 +180,7 @@ def cpu_baseline_and_check(args, cfg, params, pictures, gpu_out):
                      f"one host thread, {t_one:.1f} s; reference padding (extendPicBorder) {pad_s * 1e3:.0f} ms per "
                      f"picture done once outside the timing",
            "all_cores": {"value": round(area_all / t_all / 1e6, 3), "unit": "Mpixels/s", "threads": threads,
+                         "share": "per-GPU share of the host (16 threads per GPU on the GPU box)",
                          "sample": f"{len(pictures)} pictures, PU-parallel pthreads, {t_all:.2f} s"},
            "padding_ms_per_picture": round(pad_s * 1e3, 1)}
     cpu.update(info)
@@ -298,7 +301,14 @@ def mvp_per_picture(ctx, cfg, n_pus, reps=10):
 
 
 def bench_c4(args, cfg, params, rank, world, local, dist):
-    """C4: one C3 picture per step, CTU-row sharded over the ranks, one packed all-gather."""
+    """C4: one C3 picture per step, CTU-row sharded over the ranks, one packed all-gather per
+    picture, pictures in random-access decode order (mm360.gop): picture k is predicted only after
+    the all-gathers of all the pictures it references have landed (a stream wait on their RCCL
+    work), so a picture's all-gather overlaps only the prediction of pictures that do not reference
+    it.  Every step predicts the same PU list from the same resident reference planes (synthetic
+    data); the decode-order dependencies are enforced, the reference samples are not re-read from
+    the gathered pictures."""
+    from mm360 import gop as G
     (cur, pus, refs), = picture_set(cfg, 1)
     ctx = new_ctx(params, local, [(cur, pus, refs)])
     if args.plan_ahead:  # the stripe list is resident (mm_pred_prepare) before the timed region
@@ -306,31 +316,40 @@ def bench_c4(args, cfg, params, rank, world, local, dist):
     mine = P.shard_pus(pus, cfg.height, world, rank)
     ctx.prepare(cur, mine)
     lay = P.StripeLayout(cfg.width, cfg.height, world)
-    bufs = [torch.zeros(lay.total, dtype=torch.int16, device="cuda") for _ in range(2)]
+    n_bufs = 4
+    bufs = [torch.zeros(lay.total, dtype=torch.int16, device="cuda") for _ in range(n_bufs)]
     ptrs = [lay.dst_pointers(b.data_ptr(), rank) for b in bufs]
     area = W.luma_area(pus)
-    pending = [None, None]  # the all-gather still reading/writing each picture buffer
 
     def mc_only(s):
         ctx.run_raw(*ptrs[s % 2])
 
-    def with_allgather(s):
-        b = s % 2
-        if pending[b] is not None:  # picture s - 2's all-gather must finish before s overwrites
-            pending[b].wait()       # the buffer (a stream wait, not a host wait)
-        ctx.run_raw(*ptrs[b])
+    def gather(b):
         if args.dist_backend == "nccl":
-            pending[b] = P.allgather_packed(bufs[b], lay, async_op=True)
-        else:  # gloo rehearsal: host staging, synchronous
-            host = bufs[b].cpu()
-            P.allgather_packed(host, lay)
-            bufs[b].copy_(host)
+            return P.allgather_packed(bufs[b], lay, async_op=True)
+        host = bufs[b].cpu()  # gloo rehearsal: host staging, synchronous
+        P.allgather_packed(host, lay)
+        bufs[b].copy_(host)
+        return None
+
+    def loop_for(gop_name, ref_waits=True):
+        """A DependencyLoop whose warm-up steps are the tail of the GOP before the timed one, so
+        the timed steps start at a GOP boundary.  ref_waits False: the dependency-free upper bound
+        (every all-gather hidden behind the next picture, round 2's loop)."""
+        size = len(G.GOPS[gop_name])
+        start = (size - args.warmup % size) % size
+        return G.DependencyLoop(gop_name, n_bufs, lambda k, poc, rr, b: ctx.run_raw(*ptrs[b]), gather,
+                                lambda h: h.wait(), start=start, ref_waits=ref_waits)
 
     t_mc = timed(args.steps, args.warmup, mc_only, dist)
-    t_e2e = timed(args.steps, args.warmup, with_allgather, dist) if world > 1 else t_mc
-    for w in pending:
-        if w is not None:
-            w.wait()
+    results = {}
+    for name, gop_name, ref_waits in (("ra32", "ra32", True), ("ra8", "ra8", True), ("independent", "ra32", False)):
+        if world == 1:
+            results[name] = t_mc
+            continue
+        lp = loop_for(gop_name, ref_waits)
+        results[name] = timed(args.steps, args.warmup, lambda s: lp.step(), dist)
+    t_e2e = results["ra32"]
     torch.cuda.synchronize()
     ctx.synchronize()
     # stage timing of this rank's stripe
@@ -343,28 +362,34 @@ def bench_c4(args, cfg, params, rank, world, local, dist):
     st = np.mean(np.array(stages), axis=0)
     kernel_ms = float(st[3])
     achieved = W.algorithmic_bytes(mine) / (kernel_ms * 1e-3) / 1e9
-    # the last gathered picture (steps - 1) on this rank vs the oracle's full picture
+    # a gathered picture on this rank vs the oracle's full picture
     bit_exact = None
     if rank == 0 and not args.no_cpu_baseline:
         from oracle.oracle import Oracle
         orc = Oracle(params, [(cur, -1, W.GED_EPIPOLE_Q24)])
         want = orc.predict_padded(orc.padded_refs(refs), cur, pus, cfg.width, cfg.height, cpu_threads())
-        got = lay.unpack(bufs[(args.steps - 1) % 2].cpu().numpy())
+        got = lay.unpack(bufs[0].cpu().numpy())
         bit_exact = all(np.array_equal(g, w) for g, w in zip(got, want))
     if rank == 0:
         ag_bytes = (world - 1) * lay.seg * 2
+        per = lambda t: {"value": round(area * args.steps / t / 1e6, 2), "ms_per_step": round(t / args.steps * 1e3, 4)}
         print(json.dumps({
             "metric": METRIC, "value": round(area * args.steps / t_e2e / 1e6, 2), "unit": "Mpixels/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(t_e2e / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "f32+int16", "data": "synthetic (seeded ERP planes + PU list, SURVEY 8(d))",
             "config": {"workload": f"C4: {cfg.description}, CTU-row sharded across {world} GPU(s) with one packed "
-                                   f"RCCL all-gather per picture", "width": cfg.width, "height": cfg.height,
+                                   f"RCCL all-gather per picture, pictures in the reference's RA GOP-32 decode "
+                                   f"order (cfg/encoder_randomaccess_vtm.cfg), each predicted after its "
+                                   f"references' all-gathers", "width": cfg.width, "height": cfg.height,
                        "pus": int(len(pus)), "pus_rank0": int(len(mine)), "luma_area": int(area),
                        "stripe_ctu_rows": lay.rows // 128, "allgather_bytes_in_per_rank": int(ag_bytes),
+                       "gop": "ra32", "timed_pictures": "decode-order pictures 0..steps-1 of a GOP",
                        "plan_ahead": bool(args.plan_ahead), "parallelism": f"ctu-row stripes x{world}"},
-            "mc_only": {"value": round(area * args.steps / t_mc / 1e6, 2), "ms_per_step": round(t_mc / args.steps * 1e3, 4),
-                        "note": "same loop without the all-gather (references pre-replicated)"},
+            "ra_gop8": dict(per(results["ra8"]), note="same loop, dyadic hierarchical-B GOP-8 decode order"),
+            "independent": dict(per(results["independent"]),
+                                note="no reference waits: every all-gather hidden behind the next picture (upper bound)"),
+            "mc_only": dict(per(t_mc), note="same loop without the all-gather (references pre-replicated)"),
             "bit_exact": bit_exact,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "k_mc_dev (rank 0 stripe)",
@@ -382,8 +407,11 @@ def bench_c4_emulate(args, cfg, params):
     rank's CTU-row stripe (ranks run one after another here, so the max over ranks is the N-GPU
     step time of the MC part), then the predicted per-picture time of the N-GPU C4 loop, with the
     stripe all-gather (N-1)/N x 56.6 MB inbound per rank modelled at one xGMI link per direction
-    (ring, ~153 GB/s) and at all 7 links (direct, 7 x 153 GB/s), hidden behind the next picture's MC
-    (two picture buffers: max(mc, allgather)) or not (mc + allgather)."""
+    (ring, ~153 GB/s) and at all 7 links (direct, 7 x 153 GB/s): hidden behind the next picture's
+    MC regardless of dependencies (max(mc, allgather), the upper bound), or in random-access decode
+    order (mm360.gop.schedule: a picture waits for its references' all-gathers; the reference's
+    GOP-32 and a dyadic GOP-8)."""
+    from mm360 import gop as G
     (cur, pus, refs), = picture_set(cfg, 1)
     ctx = new_ctx(params, 0, [(cur, pus, refs)])
     if args.plan_ahead:
@@ -403,14 +431,18 @@ def bench_c4_emulate(args, cfg, params):
             worst = max(worst, t / args.steps)
         ag = (n - 1) / n * pic_bytes
         ring, mesh = ag / link, ag / (7 * link) if n > 1 else 0.0
-        out["n"][n] = {"mc_ms": round(worst * 1e3, 4),
+        mc = worst * 1e3
+        dep = {f"{g}_{k}": round(G.schedule(64, mc, a * 1e3, g)["ms_per_picture"], 4)
+               for g in ("ra32", "ra8") for k, a in (("ring", ring), ("mesh", mesh))}
+        out["n"][n] = {"mc_ms": round(mc, 4),
                        "allgather_ms": {"ring": round(ring * 1e3, 4), "mesh": round(mesh * 1e3, 4)},
                        "pred_ms_per_picture": {"hidden_ring": round(max(worst, ring) * 1e3, 4),
                                                "hidden_mesh": round(max(worst, mesh) * 1e3, 4),
-                                               "serial_ring": round((worst + ring) * 1e3, 4)},
+                                               "serial_ring": round((worst + ring) * 1e3, 4), **dep},
                        "pred_mpix_s": {"hidden_ring": round(area / max(worst, ring) / 1e6, 1),
                                        "hidden_mesh": round(area / max(worst, mesh) / 1e6, 1),
-                                       "mc_only": round(area / worst / 1e6, 1)}}
+                                       "mc_only": round(area / worst / 1e6, 1),
+                                       **{k: round(area / (v * 1e-3) / 1e6, 1) for k, v in dep.items()}}}
     print(json.dumps(out), flush=True)
     ctx.close()
 

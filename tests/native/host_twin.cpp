@@ -20,8 +20,8 @@ static const int8_t CHROMA_T[32][4] = MM_CHROMA_TAPS_INIT;
 struct Twin {
   SeqConst sc;
   Geometry geo;
-  std::vector<float> px[3], py[3];
-  std::vector<uint8_t> vip[3];
+  std::vector<float> px, py;  // the three MPA planes back to back (MpaCache)
+  std::vector<uint8_t> vip;
   std::vector<float> trig;  // separable toSphere table (MpaCache::trig_col / trig_row)
 };
 
@@ -39,25 +39,23 @@ static void make_twin(const mm_seq_params* p, Twin* t) {
   const int cols = p->width / 4, rows = p->height / 4, n = cols * rows;
   t->trig.assign((size_t)4 * (cols + rows), 0.0f);
   for (int i = 0; i < 2 * (cols + rows); i++) erp_trig_thread(i, t->sc, cols, rows, t->trig.data(), t->trig.data() + 4 * cols);
+  t->px.assign(3 * (size_t)n, 0.0f);
+  t->py.assign(3 * (size_t)n, 0.0f);
+  t->vip.assign(3 * (size_t)n, 0);
   for (int pl = 0; pl < 3; pl++) {
     if (!(p->active_models & (1u << (MPA_FRONT_BACK + pl)))) continue;
-    t->px[pl].resize(n);
-    t->py[pl].resize(n);
-    t->vip[pl].resize(n);
 #pragma omp parallel for schedule(static)
     for (int i = 0; i < n; i++)
-      mpa_cache_thread(i, t->sc, MPA_FRONT_BACK + pl, cols, rows, t->px[pl].data(), t->py[pl].data(),
-                       t->vip[pl].data());
+      mpa_cache_thread(i, t->sc, MPA_FRONT_BACK + pl, cols, rows, t->px.data() + (size_t)pl * n,
+                       t->py.data() + (size_t)pl * n, t->vip.data() + (size_t)pl * n);
   }
 }
 
 static MpaCache cache_of(const Twin& t) {
   MpaCache c{};
-  for (int pl = 0; pl < 3; pl++) {
-    c.px[pl] = t.px[pl].data();
-    c.py[pl] = t.py[pl].data();
-    c.vip[pl] = t.vip[pl].data();
-  }
+  c.px = t.px.data();
+  c.py = t.py.data();
+  c.vip = t.vip.data();
   c.cols = t.geo.W / 4;
   c.rows = t.geo.H / 4;
   c.trig_col = t.trig.data();
@@ -148,11 +146,16 @@ static int twin_pred_list(const Twin& t, const mmdev::PicTables& tab, const mm_p
 #pragma omp parallel for schedule(static)
     for (int j = 0; j < m.n_sub * N_OFF * 2; j++) dmvr_setup_thread(j, t.sc, subs.data(), tab.ged, dset.data());
     std::vector<uint32_t> costs((size_t)m.n_sub * N_OFF, 0);
+    std::vector<mm_int2> dpos(2 * (size_t)m.n_dmvr_elems + 2);
+#pragma omp parallel for schedule(static, 256)
+    for (long g = 0; g < m.n_dmvr_elems; g++)
+      dmvr_reproj_thread((int)g, find_item(sub_off.data(), sub_chunk.data(), (int)g, m.n_sub), t.sc, subs.data(),
+                         dset.data(), c, dpos.data());
 #pragma omp parallel for schedule(static, 256)
     for (long g = 0; g < m.n_dmvr_elems; g++) {
       int idx;
       const int si = find_item(sub_off.data(), sub_chunk.data(), (int)g, m.n_sub);
-      uint32_t v = dmvr_cost_thread((int)g, si, t.sc, t.geo, taps, subs.data(), dset.data(), c, tab.ref, &idx);
+      uint32_t v = dmvr_sad_thread((int)g, si, t.geo, taps, subs.data(), dpos.data(), tab.ref, &idx);
 #pragma omp atomic
       costs[idx] += v;
     }
@@ -163,13 +166,21 @@ static int twin_pred_list(const Twin& t, const mmdev::PicTables& tab, const mm_p
   std::vector<BlockSetup> setups(m.n_jobs);
 #pragma omp parallel for schedule(static)
   for (int i = 0; i < m.n_jobs; i++) setup_thread(i, t.sc, jobs.data(), tab.ged, setups.data());
-  std::vector<mm_int2> meta(std::max(m.n_sb, 1), mm_int2{});
-  std::vector<mm_int4> pos[2];
+  const size_t nsb = std::max(m.n_sb, 1);
+  std::vector<mm_int2> meta(nsb, mm_int2{});
+  std::vector<uint32_t> lpos[2], cpos[2];
+  std::vector<mm_int2> far[2][2];
   McRec mc;
   mc.meta = meta.data();
   for (int l = 0; l < 2; l++) {
-    pos[l].assign(std::max(m.n_sb, 1), mm_int4{});
-    mc.pos[l] = pos[l].data();
+    lpos[l].assign(nsb, 0u);
+    cpos[l].assign(nsb, 0u);
+    mc.lpos[l] = lpos[l].data();
+    mc.cpos[l] = cpos[l].data();
+    for (int q = 0; q < 2; q++) {
+      far[l][q].assign(nsb, mm_int2{});
+      mc.far[l][q] = far[l][q].data();
+    }
   }
 #pragma omp parallel for schedule(static, 256)
   for (int g = 0; g < m.n_elems; g++)

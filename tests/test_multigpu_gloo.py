@@ -14,6 +14,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import mm360
+from mm360 import gop as G
 from mm360 import parallel as P
 from mm360 import workload as W
 
@@ -109,3 +110,121 @@ def test_gloo_sharded_equals_full(tmp_path, cfg_name, world):
     assert sum(counts) == len(W.pu_list(cfg))
     n_ctu_rows = (cfg.height + 127) // 128
     assert all(c > 0 for c in counts) or n_ctu_rows < world  # C1 is a single CTU row
+
+
+GOP_CFG = W.Config("GOP", 512, 384, W.MPA3 + (mm360.GEODESIC_CAMPOSE, mm360.ROTATIONAL), 6,
+                   "512x384 ERP, three CTU rows (decode-order chain)")
+
+
+def _chain_pus(k, poc, refs):
+    """Picture k's PU list with its two workload references (0, 16) mapped onto the picture's
+    decode-order references: list 0 -> the nearest past one, list 1 -> the nearest future one
+    (the other side when one side is empty)."""
+    pus = W.pu_list(GOP_CFG, frame=k)
+    past = [r for r in refs if r < poc]
+    fut = [r for r in refs if r > poc]
+    r0 = max(past) if past else min(fut)
+    r1 = min(fut) if fut else max(past)
+    rp = pus["ref_poc"]
+    pus["ref_poc"] = np.where(rp == W.REF_POCS[0], r0, np.where(rp == W.REF_POCS[1], r1, -1))
+    return pus
+
+
+def _chain_worker(rank, world, port, n_pictures, out_dir):
+    """One rank of the C4 decode-order loop (mm360.gop.DependencyLoop) on CPU: every picture is
+    predicted FROM the gathered pictures it references, so a missing or early reference wait
+    would show up as a wrong picture."""
+    import sys
+    for p in (os.path.join(ROOT, "vvc-extension-mm_amd"), ROOT, os.path.join(ROOT, "tests", "native")):
+        sys.path.insert(0, p)
+    import twin
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = GOP_CFG
+    params = mm360.seq_params(cfg.width, cfg.height, cfg.models)
+    seq = G.decode_sequence(n_pictures, "ra8")
+    epi = [(poc, -1, W.GED_EPIPOLE_Q24) for poc, _, _ in seq]
+    lay = P.StripeLayout(cfg.width, cfg.height, world)
+    bufs = [np.full(lay.total, -5, dtype=np.int16) for _ in range(2)]
+    decoded = {0: W.ref_planes(cfg.width, cfg.height, 0)}
+    cur = {}
+
+    def predict(k, poc, refs, b):
+        mine = P.shard_pus(_chain_pus(k, poc, refs), cfg.height, world, rank)
+        planes = twin.predict(params, poc, mine, {r: decoded[r] for r in refs}, cfg.width, cfg.height, epi)
+        lay.pack(planes, rank, bufs[b])
+        cur["poc"] = poc
+
+    def gather(b):
+        t = torch.from_numpy(bufs[b])
+        P.allgather_packed(t, lay)
+        decoded[cur["poc"]] = lay.unpack(t.numpy())
+        return ("gathered", cur["poc"])
+
+    waits = []
+    loop = G.DependencyLoop("ra8", 2, predict, gather, waits.append)
+    for _ in range(n_pictures):
+        loop.step()
+    out = {f"poc{poc}_{c}": decoded[poc][i] for poc, _, _ in seq for i, c in enumerate(("y", "cb", "cr"))}
+    np.savez(os.path.join(out_dir, f"chain{rank}.npz"), **out)
+    with open(os.path.join(out_dir, f"trace{rank}.txt"), "w") as f:
+        for poc, waited in loop.trace:
+            f.write(f"{poc}:{','.join(map(str, waited))}\n")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_decode_sequences():
+    """The reference's RA GOP-32 (cfg/encoder_randomaccess_vtm.cfg:20-51) and the dyadic GOP-8:
+    every POC of a GOP decoded once, every reference decoded earlier (or before the sequence)."""
+    for name, size in (("ra32", 32), ("ra8", 8)):
+        seq = G.decode_sequence(3 * size, name)
+        assert sorted(p for p, _, _ in seq) == list(range(1, 3 * size + 1))
+        done = set()
+        for poc, tid, refs in seq:
+            assert poc not in refs and all(r in done or r <= 0 for r in refs), (name, poc, refs)
+            done.add(poc)
+        assert [p for p, _, _ in seq[:size]][:4] == [size, size // 2, size // 4, size // 8]
+        leaves = [p for p, t, _ in seq if t == max(tt for _, tt, _ in seq)]
+        assert all(p % 2 == 1 for p in leaves) and len(leaves) == len(seq) // 2
+    assert G.decode_sequence(1, "ra32", 22)[0] == (22, 4, [0, 16, 18, 20, 24, 32])
+
+
+def test_schedule_model():
+    """The dependency-aware model: with every all-gather shorter than the MC, each picture that
+    the next one references stalls the GPUs by one all-gather; half the pictures are referenced
+    leaves' parents in both GOPs.  Without all-gathers it is the MC time."""
+    for g in ("ra32", "ra8"):
+        assert G.schedule(64, 1.0, 0.0, g)["ms_per_picture"] == 1.0
+        r = G.schedule(64, 1.0, 0.3, g)
+        assert 1.0 < r["ms_per_picture"] < 1.3 and r["stall_ms_per_picture"] > 0
+        slow = G.schedule(64, 0.1, 1.0, g)  # all-gather bound
+        assert slow["ms_per_picture"] >= 1.0
+
+
+def test_gloo_decode_order_chain(tmp_path):
+    """C4 decode-order loop, world 2: each picture of an RA GOP-8 sequence is predicted from its
+    gathered references; every rank ends with exactly the unsharded chain, and each picture waited
+    for the all-gathers of all its references decoded in the sequence."""
+    n = 6
+    port = _free_port()
+    mp.spawn(_chain_worker, args=(2, port, n, str(tmp_path)), nprocs=2, join=True)
+    import twin
+    cfg = GOP_CFG
+    params = mm360.seq_params(cfg.width, cfg.height, cfg.models)
+    seq = G.decode_sequence(n, "ra8")
+    epi = [(poc, -1, W.GED_EPIPOLE_Q24) for poc, _, _ in seq]
+    decoded = {0: W.ref_planes(cfg.width, cfg.height, 0)}
+    for k, (poc, _, refs) in enumerate(seq):
+        decoded[poc] = twin.predict(params, poc, _chain_pus(k, poc, refs), {r: decoded[r] for r in refs},
+                                    cfg.width, cfg.height, epi)
+    for r in range(2):
+        z = np.load(os.path.join(tmp_path, f"chain{r}.npz"))
+        for poc, _, _ in seq:
+            for i, c in enumerate(("y", "cb", "cr")):
+                assert np.array_equal(z[f"poc{poc}_{c}"], decoded[poc][i]), (r, poc, c)
+        trace = open(os.path.join(tmp_path, f"trace{r}.txt")).read().split()
+        for (poc, _, refs), line in zip(seq, trace):
+            p, w = line.split(":")
+            assert int(p) == poc
+            assert sorted(int(x) for x in w.split(",") if x) == [x for x in refs if x > 0]

@@ -26,29 +26,25 @@ using mmdmvr::N_OFF;
 using mmdmvr::SubPuDev;
 
 constexpr int MAX_SLOTS = 16;  // reference pictures addressable by one picture (2 lists x 8)
-// PU buckets: N_PU_KEYS horizontal bins of the picture, by the PU's top row.  Inside a bin the PUs
-// keep the list's (decode) order, so the sub-block enumeration k_mc reads is spatial.  k_plan_place
-// cuts the bins into N_BANDS bands of about equal sub-block counts (PlanMeta::band), and k_mc runs
-// band r on the workgroups that share one XCD (mm_kernels.hip k_mc_dev): the reference windows of
-// neighbouring PUs -- which overlap by the MV spread plus the filter reach -- are fetched into that
-// XCD's L2 once, instead of once per XCD and per PU class.  k_mc handles bi and uni sub-blocks in
-// one body (the McRec meta word says which lists a sub-block uses), so no class buckets are needed.
-// The cut balances bands also for a stripe of the picture (mm360/parallel.py shards by CTU rows).
-constexpr int N_PU_KEYS = 64;
+// PU bucket: one.  PUs keep the list's (decode, raster CTU) order, quarter block by quarter block,
+// so the sub-block enumeration k_mc reads is spatial, and k_mc handles bi and uni sub-blocks in one
+// body (the McRec meta word says which lists a sub-block uses), so no class buckets are needed.
+// k_mc cuts the enumeration into N_BANDS equal bands, one per XCD (mm_kernels.hip k_mc_dev): each
+// band is a run of CTU rows, whose PUs' reference windows -- overlapping by the MV spread plus the
+// filter reach -- one XCD's L2 fetches once.  (Sorting by 64 picture-row bins instead measured the
+// same k_mc and a 3x slower k_plan_place: profiles/r03_ab_pu_keys.txt.)
+constexpr int N_PU_KEYS = 1;
 constexpr int N_BANDS = 8;
-MM_HD int pu_key(int y, int H) { return (int)(((long)y * N_PU_KEYS) / H); }
+MM_HD int pu_key(int y, int H) {
+  (void)y;
+  (void)H;
+  return 0;
+}
 
-// Band cut of the bins: band r = sub-blocks [band[r], band[r + 1]), bin boundaries at the nearest
-// bin start at or after r / N_BANDS of the sub-blocks (one thread; sb_base = the bins' starts).
+// band r = sub-blocks [band[r], band[r + 1])
 MM_HD void band_cut(const int* sb_base, int n_sb, int* band) {
-  int k = 0;
-  band[0] = 0;
-  for (int r = 1; r < N_BANDS; r++) {
-    const long target = (long)n_sb * r / N_BANDS;
-    while (k < N_PU_KEYS && sb_base[k] < target) k++;
-    band[r] = k < N_PU_KEYS ? sb_base[k] : n_sb;
-  }
-  band[N_BANDS] = n_sb;
+  (void)sb_base;
+  for (int r = 0; r <= N_BANDS; r++) band[r] = (int)((long)n_sb * r / N_BANDS);
 }
 constexpr int N_JOB_KEYS = 64;
 constexpr int DMVR_KEY = N_PU_KEYS + N_JOB_KEYS;  // one bucket of MM-DMVR sub-PUs after the PU and job keys

@@ -50,49 +50,62 @@ MM_HD void dmvr_setup_thread(int t, const SeqConst& sc, const SubPuDev* sp, cons
   block_setup(&out[t], sc, u.model, true, u.x, u.y, u.w, u.h, mvh, mvv, u.ged_idx[l] >= 0 ? &ged[u.ged_idx[l]] : nullptr);
 }
 
-// element = (sub-PU, offset, luma 4x4 sub-block): both lists' 14-bit predictions and this
-// sub-block's share of xDMVRCost (SAD over the even rows of the sub-PU, which are the even rows of
-// each 4x4 sub-block).  *cost_index = s * N_OFF + o.
-MM_HD uint32_t dmvr_cost_thread(int g, int si, const SeqConst& sc, const Geometry& geo, const Taps& taps,
-                                const SubPuDev* sp, const BlockSetup* setups, const MpaCache& cache,
-                                const RefDev* refs, int* cost_index) {
+// element = (sub-PU, offset, luma 4x4 sub-block) -> the reprojected luma positions of both lists
+// (1/16 pel): L0 at merge0 + offset, L1 at merge1 - offset (setups[(s * N_OFF + o) * 2 + l]).
+// The search runs as two kernels like the picture path -- this VALU-heavy reprojection (k_reproj's
+// footprint), then the window-load-heavy prediction + SAD (k_mc's) -- since one kernel doing both
+// needed 163-179 VGPRs (2 waves per SIMD) and ran at half the rate (profiles/r03_ab_dmvr_split.txt).
+MM_HD void dmvr_reproj_thread(int g, int si, const SeqConst& sc, const SubPuDev* sp, const BlockSetup* setups,
+                              const MpaCache& cache, mm_int2* pos) {
   const SubPuDev& u = sp[si];
   const int local = g - u.elem_off;
   const int o = local / u.n, e = local - o * u.n;
-  *cost_index = si * N_OFF + o;
   const int col = e / u.rows, row = e - col * u.rows;
   const float gx = (float)(u.x + 4 * col) + sc.off, gy = (float)(u.y + 4 * row) + sc.off;
   const bool mpa = u.model >= MPA_FRONT_BACK && u.model <= MPA_TOP_BOTTOM;
   float px = 0.0f, py = 0.0f;
   bool vip = false;
   if (mpa) {
-    const int ci = ((u.y >> 2) + row) * cache.cols + (u.x >> 2) + col;
-    const int pl = u.model - MPA_FRONT_BACK;
-    px = cache.px[pl][ci];
-    py = cache.py[pl][ci];
-    vip = cache.vip[pl][ci] != 0;
+    mpa_lookup(cache, u.model, (u.x >> 2) + col, (u.y >> 2) + row, &px, &py, &vip);
   }
   const bool packet = packet_lane(e, u.n);
-  V3 pg;
-  const V3* pgp = nullptr;
-  if (!mpa && cache.trig_col) {
-    pg = grid_sphere(cache, (u.x >> 2) + col, (u.y >> 2) + row, packet);
-    pgp = &pg;
-  }
-  int16_t p[2][16];
+  const GridSphere pg = grid_point(cache, u.model, (u.x >> 2) + col, (u.y >> 2) + row, packet);
 #pragma unroll
   for (int l = 0; l < 2; l++) {
     int32_t fx, fy;
-    reproject_element(sc, setups[(si * N_OFF + o) * 2 + l], gx, gy, packet, mpa, px, py, vip, 0, &fx, &fy, pgp);
+    reproject_element(sc, setups[(si * N_OFF + o) * 2 + l], gx, gy, packet, mpa, px, py, vip, 0, &fx, &fy, pg);
+    mm_int2 q;
+    q.x = fx;
+    q.y = fy;
+    pos[2 * (long)g + l] = q;
+  }
+}
+
+// element g's two 14-bit luma predictions from its positions and its share of xDMVRCost (SAD over
+// the even rows of the sub-PU, which are the even rows of each 4x4 sub-block).
+// *cost_index = s * N_OFF + o.
+MM_HD uint32_t dmvr_sad_thread(int g, int si, const Geometry& geo, const Taps& taps, const SubPuDev* sp,
+                               const mm_int2* pos, const RefDev* refs, int* cost_index) {
+  const SubPuDev& u = sp[si];
+  const int local = g - u.elem_off;
+  const int o = local / u.n;
+  *cost_index = si * N_OFF + o;
+  int16_t p[2][16];
+#pragma unroll
+  for (int l = 0; l < 2; l++) {
+    const mm_int2 q = pos[2 * (long)g + l];
+    const int32_t fx = q.x, fy = q.y;
     const int xPos = fx >> 4, yPos = fy >> 4, xFrac = fx & 15, yFrac = fy & 15;
     const RefDev r = refs[u.slot[l]];
     if (sb_out_of_range(xPos, yPos, geo.W, geo.H, geo.maxCUw, geo.maxCUh, 4, 4)) {
       for (int i = 0; i < 16; i++) p[l][i] = 0;
-    } else if (window_interior<8, 4, 4>(xPos, yPos, geo.W, geo.H)) {
 #if defined(__HIP_DEVICE_COMPILE__)
+    } else if (geo.padded || window_interior<8, 4, 4>(xPos, yPos, geo.W, geo.H)) {
+      // padded pool planes: every in-range window is readable without clamping (as in k_mc)
       predict_subblock_pool<8, 4, 4>(taps.pool, r.off_y, 0, r.stride_y, xPos, yPos, taps.packed->lh[xFrac][(xPos - 3) & 1],
                                      taps.packed->lv[yFrac], true, geo.bd, p[l]);
 #else
+    } else if (window_interior<8, 4, 4>(xPos, yPos, geo.W, geo.H)) {
       predict_subblock_interior<8, 4, 4>(r.y, r.stride_y, xPos, yPos, taps.luma[xFrac], taps.luma[yFrac], true, geo.bd,
                                          p[l]);
 #endif

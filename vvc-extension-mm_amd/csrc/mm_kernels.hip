@@ -263,6 +263,7 @@ __global__ void __launch_bounds__(PLACE_BLOCK) k_plan_place(const mm_pu_desc* __
       PlanMeta m = s_meta;
       if (!s_ok) {  // over capacity (overlapping PUs): nothing is predicted, the call fails
         m.n_pus = m.n_sb = m.n_jobs = m.n_elems = m.n_sub = m.n_dmvr_elems = 0;
+        for (int r = 0; r <= N_BANDS; r++) m.band[r] = 0;
         atomicMax(status, status_word(0, MM_ERR_ARG));
       }
       *meta = m;
@@ -373,7 +374,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
                                                 const PicTables t, int16_t* __restrict__ dst_y, int dsy,
                                                 int16_t* __restrict__ dst_cb, int16_t* __restrict__ dst_cr, int dsc) {
   const int band = blockIdx.x & 7, stride = (int)(gridDim.x >> 3) * 256;
-  const int b0 = meta->band[band], b1 = meta->band[band + 1];
+  const int n_sb = meta->n_sb;  // (second guard: a band never reaches past the plan's sub-blocks)
+  const int b0 = meta->band[band], b1 = min(meta->band[band + 1], n_sb);
   __shared__ PackedTaps s_taps;
   __shared__ RefDev s_ref[MAX_SLOTS];
   static_assert(sizeof(PackedTaps) % 16 == 0 && sizeof(PackedTaps) / 16 <= 256, "one 16-byte word per thread");
@@ -454,12 +456,29 @@ __global__ void __launch_bounds__(256) k_dmvr_setup_dev(SeqConst sc, const PlanM
   }
 }
 
-// thread per (sub-PU, offset, 4x4 sub-block); each wave's segments of equal cost index are summed
-// across lanes (shuffle scan) and added by their last lane
-__global__ void __launch_bounds__(256) k_dmvr_cost_dev(SeqConst sc, Geometry geo, const PlanMeta* __restrict__ meta,
-                                                       const SubPuDev* __restrict__ sp, const int* __restrict__ off,
-                                                       const int* __restrict__ chunk, const BlockSetup* __restrict__ setups,
-                                                       MpaCache cache, const PicTables t, uint32_t* __restrict__ costs) {
+// thread per (sub-PU, offset, 4x4 sub-block): both lists' reprojected luma positions
+__global__ void __launch_bounds__(256) k_dmvr_reproj_dev(SeqConst sc, const PlanMeta* __restrict__ meta,
+                                                         const SubPuDev* __restrict__ sp, const int* __restrict__ off,
+                                                         const int* __restrict__ chunk,
+                                                         const BlockSetup* __restrict__ setups, MpaCache cache,
+                                                         mm_int2* __restrict__ pos) {
+  const int n_elems = meta->n_dmvr_elems, n_sub = meta->n_sub;
+  const int lane = __lane_id();
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, n_waves = (gridDim.x * blockDim.x) >> 6;
+  for (int g0 = wave * 64; g0 < n_elems; g0 += n_waves * 64) {
+    const int g = g0 + lane;
+    const int si = wave_find_item(off, chunk, g, n_sub);
+    if (g < n_elems) dmvr_reproj_thread(g, si, sc, sp, setups, cache, pos);
+  }
+}
+
+// thread per (sub-PU, offset, 4x4 sub-block): the two luma predictions and the sub-block's SAD share;
+// each wave's segments of equal cost index are summed across lanes (shuffle scan) and added by their
+// last lane
+__global__ void __launch_bounds__(256) k_dmvr_sad_dev(Geometry geo, const PlanMeta* __restrict__ meta,
+                                                      const SubPuDev* __restrict__ sp, const int* __restrict__ off,
+                                                      const int* __restrict__ chunk, const mm_int2* __restrict__ pos,
+                                                      const PicTables t, uint32_t* __restrict__ costs) {
   const int n_elems = meta->n_dmvr_elems, n_sub = meta->n_sub;
   const int lane = __lane_id();
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, n_waves = (gridDim.x * blockDim.x) >> 6;
@@ -470,7 +489,7 @@ __global__ void __launch_bounds__(256) k_dmvr_cost_dev(SeqConst sc, Geometry geo
     const bool active = g < n_elems;
     int idx = -1 - lane;
     uint32_t v = 0;
-    if (active) v = dmvr_cost_thread(g, si, sc, geo, taps, sp, setups, cache, t.ref, &idx);
+    if (active) v = dmvr_sad_thread(g, si, geo, taps, sp, pos, t.ref, &idx);
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
       const uint32_t vu = __shfl_up(v, d);
@@ -661,7 +680,8 @@ struct PlanSlot {
   DevBuf<unsigned long long> blkq;  // per-quarter bucket counts
   DevBuf<PlanMeta> meta;
   DevBuf<mm_int2> mc_meta;
-  DevBuf<mm_int4> mc_pos[2];
+  DevBuf<uint32_t> mc_lpos[2], mc_cpos[2];
+  DevBuf<mm_int2> mc_far[2][2];
   DevBuf<SubPuDev> dmvr_sub;  // MM-DMVR sub-PU records (k_plan_place) and their element offsets / chunks
   DevBuf<int> dmvr_off, dmvr_chunk;
   int n_ensured = 0;  // largest stripe size the buffers were sized for (they only grow)
@@ -679,7 +699,11 @@ struct PlanSlot {
     blkq.release();
     meta.release();
     mc_meta.release();
-    for (int l = 0; l < 2; l++) mc_pos[l].release();
+    for (int l = 0; l < 2; l++) {
+      mc_lpos[l].release();
+      mc_cpos[l].release();
+      for (int k = 0; k < 2; k++) mc_far[l][k].release();
+    }
   }
 };
 
@@ -712,9 +736,9 @@ struct mm_ctx {
   EpipoleMap epipoles;                            // the context's EpipoleList (mm_epipole.h)
   mm_epipole_list epi_handle{&epipoles, false};   // its C-ABI handle (mm_get_epipole_list)
   float* trig = nullptr;  // separable toSphere table of the frame grid (MpaCache::trig_col / trig_row)
-  float* mpa_px[3] = {nullptr, nullptr, nullptr};
-  float* mpa_py[3] = {nullptr, nullptr, nullptr};
-  uint8_t* mpa_vip[3] = {nullptr, nullptr, nullptr};
+  float* mpa_px = nullptr;  // the three MPA planes back to back (MpaCache)
+  float* mpa_py = nullptr;
+  uint8_t* mpa_vip = nullptr;
   Plan plan;  // host plan of the parity API mm_reproject
   DevBuf<JobDev> d_jobs;
   DevBuf<int> d_job_off, d_job_chunk, d_pu_off, d_pu_chunk;
@@ -751,6 +775,7 @@ struct mm_ctx {
   bool dmvr = false;
   DevBuf<int> d_dmvr_mvd;
   DevBuf<uint32_t> d_dmvr_cost;
+  DevBuf<mm_int2> d_dmvr_pos;  // both lists' reprojected positions per cost element
   DevBuf<BlockSetup> d_dmvr_setup;
   // MM-MVP: the device copy of the epipole list (refreshed when its version moves, staged through a
   // pinned buffer on the context stream), the host-buffer API's query / result buffers and the
@@ -798,11 +823,9 @@ static int upload(mm_ctx* c, DevBuf<T>& d, const std::vector<T>& h) {
 
 static MpaCache make_cache(mm_ctx* c) {
   MpaCache mc{};
-  for (int pl = 0; pl < 3; pl++) {
-    mc.px[pl] = c->mpa_px[pl];
-    mc.py[pl] = c->mpa_py[pl];
-    mc.vip[pl] = c->mpa_vip[pl];
-  }
+  mc.px = c->mpa_px;
+  mc.py = c->mpa_py;
+  mc.vip = c->mpa_vip;
   mc.cols = c->geo.W / 4;
   mc.rows = c->geo.H / 4;
   mc.trig_col = c->trig;
@@ -909,15 +932,17 @@ int mm_create(const mm_seq_params* p, int device, mm_ctx** out_ctx) {
   }
   // MPA frame caches (MVReprojection::init -> MotionPlaneAdaptiveMotionModel::fillCache)
   const int cols = p->width / 4, rows = p->height / 4, n = cols * rows;
+  const unsigned mpa_bits = p->active_models & (7u << MPA_FRONT_BACK);
+  if (mpa_bits && (hipMalloc(&c->mpa_px, 3 * (size_t)n * sizeof(float)) != hipSuccess ||
+                   hipMalloc(&c->mpa_py, 3 * (size_t)n * sizeof(float)) != hipSuccess ||
+                   hipMalloc(&c->mpa_vip, 3 * (size_t)n) != hipSuccess)) {
+    mm_destroy(c);
+    return MM_ERR_HIP;
+  }
   for (int pl = 0; pl < 3; pl++) {
     if (!(p->active_models & (1u << (MPA_FRONT_BACK + pl)))) continue;
-    if (hipMalloc(&c->mpa_px[pl], n * sizeof(float)) != hipSuccess ||
-        hipMalloc(&c->mpa_py[pl], n * sizeof(float)) != hipSuccess || hipMalloc(&c->mpa_vip[pl], n) != hipSuccess) {
-      mm_destroy(c);
-      return MM_ERR_HIP;
-    }
     hipLaunchKernelGGL(k_mpa_cache, dim3((n + 255) / 256), dim3(256), 0, c->stream, c->sc, MPA_FRONT_BACK + pl, cols,
-                       rows, c->mpa_px[pl], c->mpa_py[pl], c->mpa_vip[pl]);
+                       rows, c->mpa_px + (size_t)pl * n, c->mpa_py + (size_t)pl * n, c->mpa_vip + (size_t)pl * n);
   }
   // separable toSphere table (MpaCache::trig_col / trig_row): 2 flavours x (cols + rows) pairs
   if (hipMalloc(&c->trig, (size_t)4 * (cols + rows) * sizeof(float)) != hipSuccess) {
@@ -943,11 +968,9 @@ int mm_destroy(mm_ctx* c) {
   (void)hipStreamSynchronize(c->stream);
   if (c->pool) (void)hipFree(c->pool);
   if (c->trig) (void)hipFree(c->trig);
-  for (int pl = 0; pl < 3; pl++) {
-    if (c->mpa_px[pl]) (void)hipFree(c->mpa_px[pl]);
-    if (c->mpa_py[pl]) (void)hipFree(c->mpa_py[pl]);
-    if (c->mpa_vip[pl]) (void)hipFree(c->mpa_vip[pl]);
-  }
+  if (c->mpa_px) (void)hipFree(c->mpa_px);
+  if (c->mpa_py) (void)hipFree(c->mpa_py);
+  if (c->mpa_vip) (void)hipFree(c->mpa_vip);
   c->d_jobs.release();
   c->d_job_off.release();
   c->d_job_chunk.release();
@@ -963,6 +986,7 @@ int mm_destroy(mm_ctx* c) {
   c->d_me_blocks.release();
   c->d_dmvr_mvd.release();
   c->d_dmvr_cost.release();
+  c->d_dmvr_pos.release();
   c->d_dmvr_setup.release();
   c->d_mvp_q.release();
   c->d_mvp_out.release();
@@ -1252,6 +1276,7 @@ static int ensure_slot_buffers(mm_ctx* c, PlanSlot& S, int n, bool dmvr) {
     HIPCHK(c, S.dmvr_chunk.ensure((size_t)k.dmvr_elems / 64 + 1));
     HIPCHK(c, c->d_dmvr_setup.ensure((size_t)k.subs * N_OFF * 2));
     HIPCHK(c, c->d_dmvr_cost.ensure((size_t)k.subs * N_OFF));
+    HIPCHK(c, c->d_dmvr_pos.ensure(2 * (size_t)k.dmvr_elems));
     HIPCHK(c, c->d_dmvr_mvd.ensure(2 * (size_t)k.subs));
     S.dmvr_ensured = true;
   }
@@ -1272,8 +1297,14 @@ static int ensure_slot_buffers(mm_ctx* c, PlanSlot& S, int n, bool dmvr) {
   HIPCHK(c, S.mc_meta.ensure(k.sb, &fresh));
   if (fresh) HIPCHK(c, hipMemsetAsync(S.mc_meta.p, 0, S.mc_meta.cap * sizeof(mm_int2), c->stream));
   for (int l = 0; l < 2; l++) {
-    HIPCHK(c, S.mc_pos[l].ensure(k.sb, &fresh));
-    if (fresh) HIPCHK(c, hipMemsetAsync(S.mc_pos[l].p, 0, S.mc_pos[l].cap * sizeof(mm_int4), c->stream));
+    HIPCHK(c, S.mc_lpos[l].ensure(k.sb, &fresh));
+    if (fresh) HIPCHK(c, hipMemsetAsync(S.mc_lpos[l].p, 0, S.mc_lpos[l].cap * sizeof(uint32_t), c->stream));
+    HIPCHK(c, S.mc_cpos[l].ensure(k.sb, &fresh));
+    if (fresh) HIPCHK(c, hipMemsetAsync(S.mc_cpos[l].p, 0, S.mc_cpos[l].cap * sizeof(uint32_t), c->stream));
+    for (int q = 0; q < 2; q++) {  // touched only by the sub-blocks whose positions are far
+      HIPCHK(c, S.mc_far[l][q].ensure(k.sb, &fresh));
+      if (fresh) HIPCHK(c, hipMemsetAsync(S.mc_far[l][q].p, 0, S.mc_far[l][q].cap * sizeof(mm_int2), c->stream));
+    }
   }
   S.n_ensured = std::max(S.n_ensured, n);
   return MM_OK;
@@ -1316,8 +1347,10 @@ static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables
     const int gc = (int)std::min<long>(DMVR_GRID, ((long)k.dmvr_elems + 255) / 256 + 1);
     hipLaunchKernelGGL(k_dmvr_setup_dev, dim3(gd), dim3(256), 0, st, c->sc, S.meta.p, S.dmvr_sub.p, t, c->d_dmvr_setup.p,
                        c->d_dmvr_cost.p);
-    hipLaunchKernelGGL(k_dmvr_cost_dev, dim3(gc), dim3(256), 0, st, c->sc, geo, S.meta.p, S.dmvr_sub.p, S.dmvr_off.p,
-                       S.dmvr_chunk.p, c->d_dmvr_setup.p, make_cache(c), t, c->d_dmvr_cost.p);
+    hipLaunchKernelGGL(k_dmvr_reproj_dev, dim3(gc), dim3(256), 0, st, c->sc, S.meta.p, S.dmvr_sub.p, S.dmvr_off.p,
+                       S.dmvr_chunk.p, c->d_dmvr_setup.p, make_cache(c), c->d_dmvr_pos.p);
+    hipLaunchKernelGGL(k_dmvr_sad_dev, dim3(gc), dim3(256), 0, st, geo, S.meta.p, S.dmvr_sub.p, S.dmvr_off.p,
+                       S.dmvr_chunk.p, c->d_dmvr_pos.p, t, c->d_dmvr_cost.p);
     hipLaunchKernelGGL(k_dmvr_decide_dev, dim3(std::max(1, std::min(DMVR_GRID, (k.subs + 255) / 256))), dim3(256), 0, st,
                        S.meta.p, S.dmvr_sub.p, c->d_dmvr_cost.p, S.jobs.p, want_mvd ? c->d_dmvr_mvd.p : nullptr);
   }
@@ -1330,7 +1363,11 @@ static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[1], st));
   McRec mc;
   mc.meta = S.mc_meta.p;
-  for (int l = 0; l < 2; l++) mc.pos[l] = S.mc_pos[l].p;
+  for (int l = 0; l < 2; l++) {
+    mc.lpos[l] = S.mc_lpos[l].p;
+    mc.cpos[l] = S.mc_cpos[l].p;
+    for (int q = 0; q < 2; q++) mc.far[l][q] = S.mc_far[l][q].p;
+  }
   hipLaunchKernelGGL(k_reproj_dev, dim3(gr), dim3(256), 0, st, c->sc, S.meta.p, S.jobs.p, S.job_off.p, S.job_chunk.p,
                      S.setup.p, make_cache(c), mc);
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[2], st));

@@ -70,32 +70,25 @@ MM_HD uint32_t me_sad_thread(int g, int bi, const SeqConst& sc, const Geometry& 
   float px = 0.0f, py = 0.0f;
   bool vip = false;
   if (mpa) {
-    const int ci = ((b.y >> 2) + row) * cache.cols + (b.x >> 2) + col;
-    const int pl = b.model - MPA_FRONT_BACK;
-    px = cache.px[pl][ci];
-    py = cache.py[pl][ci];
-    vip = cache.vip[pl][ci] != 0;
+    mpa_lookup(cache, b.model, (b.x >> 2) + col, (b.y >> 2) + row, &px, &py, &vip);
   }
   const bool packet = packet_lane(e, b.n);
-  V3 pg;
-  const V3* pgp = nullptr;
-  if (!mpa && cache.trig_col) {
-    pg = grid_sphere(cache, (b.x >> 2) + col, (b.y >> 2) + row, packet);
-    pgp = &pg;
-  }
+  const GridSphere pg = grid_point(cache, b.model, (b.x >> 2) + col, (b.y >> 2) + row, packet);
   int32_t fx, fy;
-  reproject_element(sc, s, gx, gy, packet, mpa, px, py, vip, 0, &fx, &fy, pgp);
+  reproject_element(sc, s, gx, gy, packet, mpa, px, py, vip, 0, &fx, &fy, pg);
   const int xPos = fx >> 4, yPos = fy >> 4, xFrac = fx & 15, yFrac = fy & 15;
   int16_t p[16];
   if (xPos < 0 || yPos < 0 || xPos >= geo.W - 4 || yPos >= geo.H - 4) {  // maxCUWidth = 0
     for (int i = 0; i < 16; i++) p[i] = 0;
   } else {
     const RefDev r = refs[b.slot];
-    if (window_interior<8, 4, 4>(xPos, yPos, geo.W, geo.H)) {
 #if defined(__HIP_DEVICE_COMPILE__)
+    if (geo.padded || window_interior<8, 4, 4>(xPos, yPos, geo.W, geo.H)) {
+      // padded pool planes: every in-range window is readable without clamping (as in k_mc)
       predict_subblock_pool<8, 4, 4>(taps.pool, r.off_y, 0, r.stride_y, xPos, yPos, taps.packed->lh[xFrac][(xPos - 3) & 1],
                                      taps.packed->lv[yFrac], false, geo.bd, p);
 #else
+    if (window_interior<8, 4, 4>(xPos, yPos, geo.W, geo.H)) {
       predict_subblock_interior<8, 4, 4>(r.y, r.stride_y, xPos, yPos, taps.luma[xFrac], taps.luma[yFrac], false, geo.bd,
                                          p);
 #endif

@@ -355,11 +355,22 @@ MM_HD void block_setup_f(BlockSetup* b, const SeqConst& s, int model, bool luma,
 // <Model>::modelMotion[Cached] of one element: the moved position as computed (before the NaN
 // fallback, offset removal and rounding).  CLASSIC (TranslationalMotionModel::modelMotion,
 // TranslationalMotionModel.cpp:8-13) adds the MV.
-// p_grid (optional): toSphere(gx, gy) of this element, taken from the separable per-column /
-// per-row trig table of the frame grid (mm_pipeline.h ErpTrig) -- the same values, computed once.
+// grid (optional, .valid): toSphere(gx, gy) of this element, taken from the separable per-column /
+// per-row trig table of the frame grid (mm_pipeline.h MpaCache) -- the same values, computed once.
+// Passed by value: a pointer to a caller's local would keep that local in scratch memory.
+struct GridSphere {
+  V3 p;
+  bool valid;
+};
+MM_HD GridSphere no_grid() {
+  GridSphere g;
+  g.p = {0.0f, 0.0f, 0.0f};
+  g.valid = false;
+  return g;
+}
 MM_HD void model_motion_element(const SeqConst& s, const BlockSetup& b, float gx, float gy, bool packet,
                                 bool mpa_cached, float pers_x, float pers_y, bool pers_vip, float* omx, float* omy,
-                                const V3* p_grid = nullptr) {
+                                GridSphere grid = no_grid()) {
   const Math m{packet};
   if (b.model == CLASSIC) {
     *omx = gx + b.mvx;
@@ -375,7 +386,7 @@ MM_HD void model_motion_element(const SeqConst& s, const BlockSetup& b, float gx
   // switch computes q and the shared tail projects it (one copy of the acosf/atan2f code).
   const bool mpa = b.model >= MPA_FRONT_BACK && b.model <= MPA_TOP_BOTTOM;
   V3 p = {0.0f, 0.0f, 0.0f};  // toSphere(grid) of TAN / 3DT / ROT / GED
-  if (!mpa) p = p_grid ? *p_grid : erp_to_sphere(gx, gy, s, m);
+  if (!mpa) p = grid.valid ? grid.p : erp_to_sphere(gx, gy, s, m);
   V3 q;
   switch (b.model) {
     case MPA_FRONT_BACK:
@@ -447,9 +458,9 @@ MM_HD void model_motion_element(const SeqConst& s, const BlockSetup& b, float gx
 
 MM_HD void reproject_element(const SeqConst& s, const BlockSetup& b, float gx, float gy, bool packet,
                              bool mpa_cached, float pers_x, float pers_y, bool pers_vip,
-                             int chroma_shift, int32_t* fx, int32_t* fy, const V3* p_grid = nullptr) {
+                             int chroma_shift, int32_t* fx, int32_t* fy, GridSphere grid = no_grid()) {
   float mx, my;
-  model_motion_element(s, b, gx, gy, packet, mpa_cached, pers_x, pers_y, pers_vip, &mx, &my, p_grid);
+  model_motion_element(s, b, gx, gy, packet, mpa_cached, pers_x, pers_y, pers_vip, &mx, &my, grid);
   // NaN -> unmoved (MVReprojection.cpp:151-154), remove offset, rescale, round to fixed point
   if (isnanf_(mx) || isnanf_(my)) {
     mx = gx;

@@ -52,17 +52,32 @@ struct alignas(8) mm_int2 {
   int x, y;
 };
 // Per-luma-sub-block inputs of k_mc, written by the reprojection of a device-planned picture in
-// the order k_mc reads them (sub-block g of the band-sorted enumeration):
-//   meta[g]   = (ox | oy << 16, slot0 | slot1 << 4 | bcw << 8 | use0 << 12 | use1 << 13): output
-//               position of the luma 4x4 sub-block, reference slot per list, BCW index, the lists
-//               the sub-block uses -- written by the PU's primary job;
-//   pos[l][g] = (luma X, luma Y in 1/16 pel, chroma X, Y in 1/32 pel) of list l: the luma job
-//               writes .xy, the chroma job (or the aliasing MPA luma job) .zw.
-// A bi sub-block is 40 bytes, read with one 8-byte and two 16-byte loads.
+// the order k_mc reads them (sub-block g of the enumeration):
+//   meta[g]    = (ox | oy << 16, slot0 | slot1 << 4 | bcw << 8 | use0 << 12 | use1 << 13): output
+//                position of the luma 4x4 sub-block, reference slot per list, BCW index, the lists
+//                the sub-block uses -- written by the PU's primary job;
+//   lpos[l][g] = the list-l luma position in 1/16 pel relative to the sub-block origin
+//                (16 ox, 16 oy), as two int16 (x lo, y hi) -- written by the luma job;
+//   cpos[l][g] = the 4:2:0 chroma position in 1/32 pel relative to (32 (ox / 2), 32 (oy / 2)),
+//                likewise -- written by the chroma job, or by the aliasing MPA luma job.
+// A relative position that does not fit 16 bits (a wrap across the ERP seam, motion of more than
+// 2047 samples) is stored as MM_POS_FAR and its absolute (x, y) in far[l][comp][g], which only those
+// sub-blocks touch.  So a bi sub-block is 24 bytes (8 + 4 x 4), each array written by one job kind
+// in whole lines, against 40 bytes of interleaved luma / chroma halves before (round 2).
 struct McRec {
   mm_int2* meta;
-  mm_int4* pos[2];
+  uint32_t* lpos[2];
+  uint32_t* cpos[2];
+  mm_int2* far[2][2];  // [list][comp]
 };
+#define MM_POS_FAR 0x8000u  // low half of a relative position word: look up far[][][]
+
+// A position relative to base as one word, or MM_POS_FAR
+MM_HD uint32_t pack_rel(int32_t fx, int32_t fy, int32_t bx, int32_t by) {
+  const long dx = (long)fx - bx, dy = (long)fy - by;
+  if (dx < -32767 || dx > 32767 || dy < -32768 || dy > 32767) return MM_POS_FAR;
+  return ((uint32_t)(uint16_t)(int16_t)dx) | ((uint32_t)(uint16_t)(int16_t)dy << 16);
+}
 #define MM_META_PRIMARY (1 << 16)
 #define MM_META_USE0 (1 << 12)
 #define MM_META_USE1 (1 << 13)
@@ -82,10 +97,13 @@ MM_HD int bcw_w1(int bcw) { return (int)((0xC7650u >> (4 * bcw)) & 15u) - 2; }
 // every grid element's sphere point bit-identically -- the same functions of the same arguments,
 // computed once per sequence instead of twice per element (the north star's shared spherical trig).
 // Layout: trig_col[(v * cols + i) * 2 + {0: sin, 1: cos}] of phi, trig_row likewise of theta.
+// px / py / vip hold the three MPA planes back to back (plane pl at pl * cols * rows): the plane is
+// picked by address arithmetic, never by indexing a pointer array with a per-lane model (which
+// would copy the kernel-argument struct to scratch memory).
 struct MpaCache {
-  const float* px[3];
-  const float* py[3];
-  const uint8_t* vip[3];
+  const float* px;
+  const float* py;
+  const uint8_t* vip;
   int cols, rows;  // W/4, H/4
   const float* trig_col;
   const float* trig_row;
@@ -118,6 +136,22 @@ MM_HD V3 grid_sphere(const MpaCache& c, int gi, int gj, bool packet) {
   return sph_from_trig(pr[0], pr[1], pc[0], pc[1]);
 }
 MM_HD bool is_mpa_model(int m) { return m >= MPA_FRONT_BACK && m <= MPA_TOP_BOTTOM; }
+
+// The frame-cache entry of an MPA model at grid (gi, gj)
+MM_HD void mpa_lookup(const MpaCache& c, int model, int gi, int gj, float* px, float* py, bool* vip) {
+  const long k = (long)(model - MPA_FRONT_BACK) * c.cols * c.rows + (long)gj * c.cols + gi;
+  *px = c.px[k];
+  *py = c.py[k];
+  *vip = c.vip[k] != 0;
+}
+// toSphere of a non-MPA element from the trig table, when the table exists
+MM_HD GridSphere grid_point(const MpaCache& c, int model, int gi, int gj, bool packet) {
+  if (is_mpa_model(model) || !c.trig_col) return no_grid();
+  GridSphere g;
+  g.p = grid_sphere(c, gi, gj, packet);
+  g.valid = true;
+  return g;
+}
 
 struct Geometry {
   int W, H, Wc, Hc;
@@ -209,47 +243,42 @@ MM_HD void reproj_thread_mc(int g, int ji, const SeqConst& sc, const JobDev* job
   float px = 0.0f, py = 0.0f;
   bool vip = false;
   if (mpa_cached) {
-    const int ci = ((j.y >> 2) + row) * cache.cols + (j.x >> 2) + col;
-    const int pl = j.model - MPA_FRONT_BACK;
-    px = cache.px[pl][ci];
-    py = cache.py[pl][ci];
-    vip = cache.vip[pl][ci] != 0;
+    mpa_lookup(cache, j.model, (j.x >> 2) + col, (j.y >> 2) + row, &px, &py, &vip);
   }
   const bool packet = packet_lane(eig, j.n);
-  V3 pg;
-  const V3* pgp = nullptr;
-  if (!is_mpa_model(j.model) && cache.trig_col) {
-    pg = grid_sphere(cache, (j.x >> 2) + col, (j.y >> 2) + row, packet);
-    pgp = &pg;
-  }
+  const GridSphere pg = grid_point(cache, j.model, (j.x >> 2) + col, (j.y >> 2) + row, packet);
   int32_t fx, fy;
-  reproject_element(sc, setups[ji], gx, gy, packet, mpa_cached, px, py, vip, j.comp ? 1 : 0, &fx, &fy, pgp);
+  reproject_element(sc, setups[ji], gx, gy, packet, mpa_cached, px, py, vip, j.comp ? 1 : 0, &fx, &fy, pg);
   // chroma 2x2 sub-block (row, col) belongs to luma 4x4 sub-block (row, col) of the same PU
   const int sb = j.sb_base + row * j.pu_cols + col;
-  mm_int4* rec = &mc.pos[j.list][sb];
+  const int ox = j.x + 4 * col, oy = j.y + 4 * row;  // luma sub-block origin; 32 (ox / 2) == 16 ox
+  const uint32_t rel = pack_rel(fx, fy, 16 * ox, 16 * oy);
+  mm_int2 xy;
+  xy.x = fx;
+  xy.y = fy;
+  // the list's arrays by selects: indexing the kernel-argument arrays with j.list would copy the
+  // whole McRec into a per-lane private array (promoted to 72 B of LDS per lane)
+  const bool l1 = j.list != 0;
+  uint32_t* const lpos = l1 ? mc.lpos[1] : mc.lpos[0];
+  uint32_t* const cpos = l1 ? mc.cpos[1] : mc.cpos[0];
+  mm_int2* const lfar = l1 ? mc.far[1][0] : mc.far[0][0];
+  mm_int2* const cfar = l1 ? mc.far[1][1] : mc.far[0][1];
   if (j.comp == 0) {
-    if (j.alias) {
-      mm_int4 r;
-      r.x = r.z = fx;
-      r.y = r.w = fy;
-      *rec = r;
-    } else {
-      mm_int2 xy;
-      xy.x = fx;
-      xy.y = fy;
-      reinterpret_cast<mm_int2*>(rec)[0] = xy;
+    lpos[sb] = rel;
+    if (rel == MM_POS_FAR) lfar[sb] = xy;
+    if (j.alias) {  // MPA chroma == luma (mm_devplan.h mpa_chroma_aliases)
+      cpos[sb] = rel;
+      if (rel == MM_POS_FAR) cfar[sb] = xy;
     }
     if (j.meta_hi & MM_META_PRIMARY) {
       mm_int2 m;
-      m.x = ((j.y + 4 * row) << 16) | (j.x + 4 * col);
+      m.x = (oy << 16) | ox;
       m.y = j.meta_hi & 0xffff;
       mc.meta[sb] = m;
     }
   } else {
-    mm_int2 xy;
-    xy.x = fx;
-    xy.y = fy;
-    reinterpret_cast<mm_int2*>(rec)[1] = xy;
+    cpos[sb] = rel;
+    if (rel == MM_POS_FAR) cfar[sb] = xy;
   }
 }
 
@@ -275,21 +304,12 @@ MM_HD void reproj_thread(int g, int ji, const SeqConst& sc, const JobDev* jobs, 
   float px = 0.0f, py = 0.0f;
   bool vip = false;
   if (mpa_cached) {
-    const int ci = ((j.y >> 2) + row) * cache.cols + (j.x >> 2) + col;
-    const int pl = j.model - MPA_FRONT_BACK;
-    px = cache.px[pl][ci];
-    py = cache.py[pl][ci];
-    vip = cache.vip[pl][ci] != 0;
+    mpa_lookup(cache, j.model, (j.x >> 2) + col, (j.y >> 2) + row, &px, &py, &vip);
   }
   const bool packet = packet_lane(local, j.n);
-  V3 pg;
-  const V3* pgp = nullptr;
-  if (!is_mpa_model(j.model) && cache.trig_col) {
-    pg = grid_sphere(cache, (j.x >> 2) + col, (j.y >> 2) + row, packet);
-    pgp = &pg;
-  }
+  const GridSphere pg = grid_point(cache, j.model, (j.x >> 2) + col, (j.y >> 2) + row, packet);
   int32_t fx, fy;
-  reproject_element(sc, setups[ji], gx, gy, packet, mpa_cached, px, py, vip, j.comp ? 1 : 0, &fx, &fy, pgp);
+  reproject_element(sc, setups[ji], gx, gy, packet, mpa_cached, px, py, vip, j.comp ? 1 : 0, &fx, &fy, pg);
   out_xy[2 * (j.offset + local)] = fx;
   out_xy[2 * (j.offset + local) + 1] = fy;
 }
@@ -343,11 +363,27 @@ MM_HD void mc_rec_impl(int g, const Geometry& geo, const Taps& taps, const McRec
                        int16_t* dst_y, int dsy, int16_t* dst_cb, int16_t* dst_cr, int dsc) {
   const mm_int2 meta = mc.meta[g];
   const bool used[2] = {(meta.y & MM_META_USE0) != 0, (meta.y & MM_META_USE1) != 0};
-  mm_int4 P[2];
-#pragma unroll
-  for (int l = 0; l < 2; l++)
-    if (used[l]) P[l] = mc.pos[l][g];
   const int ox = meta.x & 0xffff, oy = meta.x >> 16;
+  mm_int4 P[2];  // (luma x, y in 1/16 pel, chroma x, y in 1/32 pel) per list
+#pragma unroll
+  for (int l = 0; l < 2; l++) {
+    if (!used[l]) continue;
+    const uint32_t lp = mc.lpos[l][g], cp = mc.cpos[l][g];
+    P[l].x = 16 * ox + (int16_t)(lp & 0xffffu);
+    P[l].y = 16 * oy + (int16_t)(lp >> 16);
+    P[l].z = 16 * ox + (int16_t)(cp & 0xffffu);
+    P[l].w = 16 * oy + (int16_t)(cp >> 16);
+    if (lp == MM_POS_FAR) {
+      const mm_int2 f = mc.far[l][0][g];
+      P[l].x = f.x;
+      P[l].y = f.y;
+    }
+    if (cp == MM_POS_FAR) {
+      const mm_int2 f = mc.far[l][1][g];
+      P[l].z = f.x;
+      P[l].w = f.y;
+    }
+  }
   const int slot[2] = {meta.y & 15, (meta.y >> 4) & 15};
   const bool bi = used[0] && used[1];
   // bi: (w0, w1) of the BCW index; uni: the list's prediction with weight 8 (see above)
