@@ -198,6 +198,7 @@ def bench_pictures(args, cfg, params, rank, world, local, dist):
         ctx.set_stripes(args.stripes)
     if args.plan_ahead:
         ctx.set_plan_ahead(True)
+    ctx.set_call_timing(False)  # a decoder loop reads no per-call times (stage timing below is separate)
     d_pus = [mm360.pus_to_device(p) for _, p, _ in pictures]
     outs = [planes(cfg) for _ in pictures]
     area = [W.luma_area(p) for _, p, _ in pictures]
@@ -229,7 +230,8 @@ def bench_pictures(args, cfg, params, rank, world, local, dist):
     alg_step = float(np.mean([alg[s % P_] for s in range(args.kernel_steps)]))
     achieved = alg_step / (kernel_ms * 1e-3) / 1e9
     got = [tuple(t.cpu().numpy() for t in o) for o in outs]
-    mvp = mvp_per_picture(ctx, cfg, int(np.mean([len(p) for _, p, _ in pictures]))) if args.config == "C3" else None
+    mvp = (mvp_per_picture(ctx, cfg, int(np.mean([len(p) for _, p, _ in pictures])))
+           if args.config == "C3" and not args.no_mvp else None)
 
     cpu, bit_exact, mism = None, None, None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -313,6 +315,7 @@ def bench_c4(args, cfg, params, rank, world, local, dist):
     ctx = new_ctx(params, local, [(cur, pus, refs)])
     if args.plan_ahead:  # the stripe list is resident (mm_pred_prepare) before the timed region
         ctx.set_plan_ahead(True)
+    ctx.set_call_timing(False)
     mine = P.shard_pus(pus, cfg.height, world, rank)
     ctx.prepare(cur, mine)
     lay = P.StripeLayout(cfg.width, cfg.height, world)
@@ -522,6 +525,7 @@ def main():
     ap.add_argument("--config", default=None, help="C3 (default at 1 GPU), C4 (default at N > 1), C2, C5")
     ap.add_argument("--pictures", type=int, default=4, help="C3: distinct pictures (each with its own references)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-mvp", action="store_true", help="C3: skip the MM-MVP figure beside the line")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="length of the one-thread CPU baseline sample")
     ap.add_argument("--kernel-steps", type=int, default=8, help="extra steps timed per launch with HIP events")
     ap.add_argument("--lib", default=None, help="alternative build of libmm360.so (A/B experiments)")

@@ -321,9 +321,16 @@ int mm_upload_org(mm_ctx* ctx, int poc, const int16_t* y, ptrdiff_t stride_y, in
 int mm_sad_window(mm_ctx* ctx, int cur_poc, const mm_me_block* blocks, int n, int range, int step,
                   uint32_t* sads);
 
-/* Device time of the last mm_pred_device / mm_pred_run / mm_sad_window launch sequence (HIP events on the
- * context stream around all of its launches), milliseconds. */
+/* Device time of the last mm_pred_device / mm_pred_run / mm_sad_window / mm_mvp_convert_device
+ * launch sequence (HIP events on the context stream around all of its launches), milliseconds.
+ * MM_ERR_ARG if that sequence was a picture call made with call timing off. */
 int mm_last_timing(mm_ctx* ctx, float* ms_total);
+
+/* Call timing of the picture calls (mm_pred*, default on): the two events mm_last_timing reads.
+ * Every event recorded on the context stream costs it ~4 us of a picture's ~0.2 ms, so a decoder
+ * loop that does not read the time switches them off.  (No reference counterpart; the reference's
+ * INTERPRED_PROFILING timers are compiled out by default.) */
+int mm_set_call_timing(mm_ctx* ctx, int on);
 
 /* Per-stage device time of the last launch sequence, recorded only while stage timing is on
  * (extra events between the launches): ms[0] planning (memset + k_plan_count + k_plan_place),

@@ -206,6 +206,12 @@ def test_pred_deterministic_and_split_api():
             ctx.run(dy, dcb, dcr)
         ctx.synchronize()
         assert ctx.last_timing_ms() > 0
+        ctx.set_call_timing(False)  # no events around the call: nothing to read
+        ctx.run(dy, dcb, dcr)
+        ctx.synchronize()
+        with pytest.raises(mm360.MMError):
+            ctx.last_timing_ms()
+        ctx.set_call_timing(True)
     for x, t in zip(a, (dy, dcb, dcr)):
         assert np.array_equal(x, t.cpu().numpy())
 

@@ -793,6 +793,10 @@ struct mm_ctx {
   bool mvp_pending = false;
   DevBuf<int> d_me_off, d_me_chunk;
   bool stage_timing = false;
+  // mm_set_call_timing: ev0 / ev1 around every picture call (on by default); `timed`: the last
+  // launch sequence recorded them
+  bool call_timing = true;
+  bool timed = false;
   hipEvent_t ev_stage[3] = {nullptr, nullptr, nullptr};  // after planning, setup, reprojection
 };
 
@@ -916,15 +920,22 @@ int mm_create(const mm_seq_params* p, int device, mm_ctx** out_ctx) {
   c->geo.hp = 0;
   c->geo.store = 3;
   c->geo.padded = 1;
-  if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-      hipEventCreate(&c->ev_stage[0]) != hipSuccess || hipEventCreate(&c->ev_stage[1]) != hipSuccess ||
-      hipEventCreate(&c->ev_stage[2]) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_gate[0], hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_gate[1], hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_plan, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_epi, hipEventDisableTiming) != hipSuccess ||
+  // Every event the library records is a device-scope release: it orders work between the
+  // context and auxiliary streams and times it, and never publishes device memory to the host
+  // (status words and results reach the host through copies).  The default system-scope release
+  // writes back the L2 after each picture's 57 MB of output: ~5 us per event, ~17 us per picture
+  // with the three events a call records (profiles/r03_ab_event_scope.txt).
+  constexpr unsigned TIMED = hipEventReleaseToDevice, SYNC = hipEventDisableTiming | hipEventReleaseToDevice;
+  if (hipEventCreateWithFlags(&c->ev0, TIMED) != hipSuccess || hipEventCreateWithFlags(&c->ev1, TIMED) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_stage[0], TIMED) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_stage[1], TIMED) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_stage[2], TIMED) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_fork, SYNC) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_join, SYNC) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_gate[0], SYNC) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_gate[1], SYNC) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_plan, SYNC) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_epi, SYNC) != hipSuccess ||
       hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
       hipEventRecord(c->ev_gate[0], c->stream) != hipSuccess) {
     mm_destroy(c);
@@ -1427,11 +1438,12 @@ static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, in
     HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_gate[c->gate_par], 0));
     c->gate_par ^= 1;
     HIPCHK(c, hipEventRecord(c->ev_gate[c->gate_par], c->stream));
-    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    c->timed = c->call_timing;
+    if (c->timed) HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     RCCHK(launch_stripe(c, c->slot[c->ahead_par], c->aux, t, geo, d_in, n, 0, status, next_status, dy, sdy, dcb, dcr,
                         sdc, true, want_mvd));
     c->ahead_par ^= 1;
-    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    if (c->timed) HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     c->last_status = status;
     c->pic_par ^= 1;
     c->status_pending = true;
@@ -1442,7 +1454,9 @@ static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, in
     if (!slot_fits(c->slot[s], per, dmvr)) HIPCHK(c, hipStreamSynchronize(c->aux));
     RCCHK(ensure_slot_buffers(c, c->slot[s], per, dmvr));
   }
-  HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+  // each event a call records costs the context stream ~4 us (profiles/r03_ab_event_scope.txt)
+  c->timed = c->call_timing || c->stage_timing;
+  if (c->timed) HIPCHK(c, hipEventRecord(c->ev0, c->stream));
   if (K > 1) {
     HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
     HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_fork, 0));
@@ -1457,10 +1471,13 @@ static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, in
     HIPCHK(c, hipEventRecord(c->ev_join, c->aux));
     HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_join, 0));
   }
-  HIPCHK(c, hipEventRecord(c->ev1, c->stream));
-  // a following plan-ahead call starts its planning only after this whole call (both slots used)
-  c->gate_par ^= 1;
-  HIPCHK(c, hipEventRecord(c->ev_gate[c->gate_par], c->stream));
+  if (c->timed) HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+  // a following plan-ahead call starts its planning only after this whole call (both slots used);
+  // while plan-ahead is off, mm_set_plan_ahead records the gates when it is switched on
+  if (c->plan_ahead) {
+    c->gate_par ^= 1;
+    HIPCHK(c, hipEventRecord(c->ev_gate[c->gate_par], c->stream));
+  }
   c->last_status = status;
   c->pic_par ^= 1;
   c->status_pending = true;
@@ -1469,7 +1486,18 @@ static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, in
 
 int mm_set_plan_ahead(mm_ctx* c, int on) {
   if (!c) return MM_ERR_ARG;
+  if (on && !c->plan_ahead) {  // calls made while it was off recorded no gate: gate on the current position
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipEventRecord(c->ev_gate[0], c->stream));
+    HIPCHK(c, hipEventRecord(c->ev_gate[1], c->stream));
+  }
   c->plan_ahead = on != 0;
+  return MM_OK;
+}
+
+int mm_set_call_timing(mm_ctx* c, int on) {
+  if (!c) return MM_ERR_ARG;
+  c->call_timing = on != 0;
   return MM_OK;
 }
 
@@ -1563,6 +1591,7 @@ int mm_pred_list(mm_ctx* c, int cur_poc, const mm_pu_desc* pus, int n, int list,
 
 int mm_last_timing(mm_ctx* c, float* ms) {
   if (!c || !ms) return MM_ERR_ARG;
+  if (!c->timed) return fail(c, MM_ERR_ARG, "the last launch sequence was not timed (mm_set_call_timing)");
   HIPCHK(c, hipEventSynchronize(c->ev1));
   HIPCHK(c, hipEventElapsedTime(ms, c->ev0, c->ev1));
   return MM_OK;
@@ -1603,6 +1632,7 @@ int mm_sad_window(mm_ctx* c, int cur_poc, const mm_me_block* blocks, int n, int 
   std::vector<MeBatch> batches;
   rc = plan_me_window(seq_info(c->prm), t, blocks, n, w, &batches, &err);
   if (rc) return fail(c, rc, err);
+  c->timed = true;
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
   HIPCHK(c, hipMemsetAsync(sads, 0, (size_t)n * w.C * sizeof(uint32_t), c->stream));
   for (const MeBatch& bt : batches) {
@@ -1695,6 +1725,7 @@ int mm_mvp_convert_device(mm_ctx* c, const mm_mvp_query* d_q, int n, int32_t* d_
   RCCHK(sync_epi_table(c));
   const mmmvp::EpiTable et{c->d_epi.p, c->epi_n};
   unsigned long long* st = c->d_mvp_status.p + c->mvp_par;
+  c->timed = true;
   HIPCHK(c, hipEventRecord(c->ev0, c->stream));
   hipLaunchKernelGGL(k_mvp_dev, dim3((n + MVP_BLOCK - 1) / MVP_BLOCK), dim3(MVP_BLOCK), 0, c->stream, c->sc, d_q, n,
                      c->prm.active_models, et, d_mv_out, st, c->d_mvp_status.p + (c->mvp_par ^ 1));

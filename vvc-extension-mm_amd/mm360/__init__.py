@@ -49,7 +49,7 @@ ERROR_NAMES = {
 EXPORTED_SYMBOLS = (
     "mm_create", "mm_destroy", "mm_set_stream", "mm_synchronize", "mm_last_error", "mm_get_version",
     "mm_set_epipole", "mm_upload_ref", "mm_release_ref", "mm_reproject", "mm_pred",
-    "mm_pred_device", "mm_pred_status", "mm_pred_prepare", "mm_pred_run", "mm_filter", "mm_last_timing",
+    "mm_pred_device", "mm_pred_status", "mm_pred_prepare", "mm_pred_run", "mm_filter", "mm_last_timing", "mm_set_call_timing",
     "mm_set_stage_timing", "mm_last_stage_timing", "mm_upload_org", "mm_sad_window", "mm_pred_dmvr", "mm_mvp_convert",
     "mm_set_stripes", "mm_set_plan_ahead", "mm_pred_list", "mm_derive_effective_blocks", "mm_epipole_list_create",
     "mm_epipole_list_destroy", "mm_get_epipole_list", "mm_epipole_add", "mm_epipole_make_available", "mm_epipole_has",
@@ -160,6 +160,7 @@ def load_library() -> ctypes.CDLL:
         "mm_filter": (c_int, [vp, c_int, c_int, vp, ctypes.c_ssize_t, vp, ctypes.c_ssize_t, c_int, c_int,
                               c_int, c_int, c_int]),
         "mm_last_timing": (c_int, [vp, POINTER(c_float)]),
+        "mm_set_call_timing": (c_int, [vp, c_int]),
         "mm_set_stage_timing": (c_int, [vp, c_int]),
         "mm_upload_org": (c_int, [vp, c_int, vp, ctypes.c_ssize_t, c_int]),
         "mm_mvp_convert": (c_int, [vp, vp, c_int, vp]),
@@ -474,6 +475,10 @@ class MMContext:
         n = d_pus.numel() * d_pus.element_size() // PU_DTYPE.itemsize
         self._check(self.lib.mm_pred_device(self.h, cur_poc, c_void_p(_ptr(d_pus)), n, c_void_p(ptr_y), stride_y,
                                             c_void_p(ptr_cb), c_void_p(ptr_cr), stride_c))
+
+    def set_call_timing(self, on: bool) -> None:
+        """mm_set_call_timing: the events around every picture call (on by default)."""
+        self._check(self.lib.mm_set_call_timing(self.h, 1 if on else 0))
 
     def last_timing_ms(self) -> float:
         ms = c_float()
