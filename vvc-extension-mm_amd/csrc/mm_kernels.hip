@@ -390,10 +390,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   const Taps taps{c_luma_taps, c_chroma_taps, &s_taps, t.pool};
   // s_ref: each lane looks its slots' pool offsets up in LDS; indexing the kernel-argument copy
   // per lane was a dependent global load between the record loads and the window loads
-  for (int g = first + (int)threadIdx.x; g - (int)threadIdx.x < b1; g += stride)
-    if (g < b1) mc_thread_rec<UNI_HP>(g, geo, taps, mc, s_ref, dst_y, dsy, dst_cb, dst_cr, dsc);
+  // software-pipelined records: the next iteration's 24 bytes are in flight while this one predicts
+  int g = first + (int)threadIdx.x;
+  McIn cur = mc_rec_load(mc, min(g, b1 - 1));
+  for (; g - (int)threadIdx.x < b1; g += stride) {
+    const int gn = g + stride;
+    McIn nxt;
+    if (gn - (int)threadIdx.x < b1) nxt = mc_rec_load(mc, min(gn, b1 - 1));
+    if (g < b1) mc_thread_in<UNI_HP>(g, cur, geo, taps, mc, s_ref, dst_y, dsy, dst_cb, dst_cr, dsc);
+    cur = nxt;
+  }
 }
 constexpr int MC_BLOCKS_PER_XCD = 128;  // 32 CUs x 4 workgroups (16 waves per CU at 4 per SIMD)
+// plan-ahead gate: the next picture's planning may start once this picture's reprojection is done
+// (true: it overlaps k_mc) or once the previous picture is done (false: it overlaps k_reproj)
+constexpr bool GATE_AFTER_REPROJ = false;
 
 // --------------------------------------------------------------------------------------------
 // Encoder candidate windows (mm_sad_window, mm_me.h)
@@ -1381,6 +1392,7 @@ static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables
   }
   hipLaunchKernelGGL(k_reproj_dev, dim3(gr), dim3(256), 0, st, c->sc, S.meta.p, S.jobs.p, S.job_off.p, S.job_chunk.p,
                      S.setup.p, make_cache(c), mc);
+  if (plan_ahead && GATE_AFTER_REPROJ) HIPCHK(c, hipEventRecord(c->ev_gate[c->gate_par], st));
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[2], st));
   if (geo.hp)
     hipLaunchKernelGGL(k_mc_dev<true>, dim3(gm), dim3(256), 0, st, geo, S.meta.p, mc, t, dy, (int)sdy, dcb, dcr, (int)sdc);
@@ -1437,7 +1449,7 @@ static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, in
     }
     HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_gate[c->gate_par], 0));
     c->gate_par ^= 1;
-    HIPCHK(c, hipEventRecord(c->ev_gate[c->gate_par], c->stream));
+    if (!GATE_AFTER_REPROJ) HIPCHK(c, hipEventRecord(c->ev_gate[c->gate_par], c->stream));
     c->timed = c->call_timing;
     if (c->timed) HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     RCCHK(launch_stripe(c, c->slot[c->ahead_par], c->aux, t, geo, d_in, n, 0, status, next_status, dy, sdy, dcb, dcr,

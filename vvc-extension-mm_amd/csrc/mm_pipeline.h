@@ -358,17 +358,36 @@ MM_HD int16_t weighted_avg(int p0, int p1, int w0, int w1, int bd) {
 // hold both (k_mc's waves follow the picture's spatial order, not PU classes); a list no lane of
 // the wave uses is skipped as a whole.
 // HP (mm_pred_list hp = 1): every sub-block uses one list and keeps its 14-bit prediction.
+// The 24 bytes of one sub-block's record, loaded by mc_rec_load (the positions of both lists
+// unconditionally: the arrays are zeroed at allocation, and a wave of the class-agnostic
+// enumeration mixes bi and uni sub-blocks, so it loads both lists anyway).  k_mc_dev loads the next
+// iteration's record before predicting the current one.
+struct McIn {
+  mm_int2 meta;
+  uint32_t lp[2], cp[2];
+};
+MM_HD McIn mc_rec_load(const McRec& mc, int g) {
+  McIn r;
+  r.meta = mc.meta[g];
+#pragma unroll
+  for (int l = 0; l < 2; l++) {
+    r.lp[l] = mc.lpos[l][g];
+    r.cp[l] = mc.cpos[l][g];
+  }
+  return r;
+}
+
 template <bool HP>
-MM_HD void mc_rec_impl(int g, const Geometry& geo, const Taps& taps, const McRec& mc, const RefDev* refs,
-                       int16_t* dst_y, int dsy, int16_t* dst_cb, int16_t* dst_cr, int dsc) {
-  const mm_int2 meta = mc.meta[g];
+MM_HD void mc_rec_impl(int g, const McIn& in, const Geometry& geo, const Taps& taps, const McRec& mc,
+                       const RefDev* refs, int16_t* dst_y, int dsy, int16_t* dst_cb, int16_t* dst_cr, int dsc) {
+  const mm_int2 meta = in.meta;
   const bool used[2] = {(meta.y & MM_META_USE0) != 0, (meta.y & MM_META_USE1) != 0};
   const int ox = meta.x & 0xffff, oy = meta.x >> 16;
   mm_int4 P[2];  // (luma x, y in 1/16 pel, chroma x, y in 1/32 pel) per list
 #pragma unroll
   for (int l = 0; l < 2; l++) {
     if (!used[l]) continue;
-    const uint32_t lp = mc.lpos[l][g], cp = mc.cpos[l][g];
+    const uint32_t lp = in.lp[l], cp = in.cp[l];
     P[l].x = 16 * ox + (int16_t)(lp & 0xffffu);
     P[l].y = 16 * oy + (int16_t)(lp >> 16);
     P[l].z = 16 * ox + (int16_t)(cp & 0xffffu);
@@ -481,7 +500,12 @@ MM_HD void mc_rec_impl(int g, const Geometry& geo, const Taps& taps, const McRec
 template <bool UNI_HP = false>
 MM_HD void mc_thread_rec(int g, const Geometry& geo, const Taps& taps, const McRec& mc, const RefDev* refs,
                          int16_t* dst_y, int dsy, int16_t* dst_cb, int16_t* dst_cr, int dsc) {
-  mc_rec_impl<UNI_HP>(g, geo, taps, mc, refs, dst_y, dsy, dst_cb, dst_cr, dsc);
+  mc_rec_impl<UNI_HP>(g, mc_rec_load(mc, g), geo, taps, mc, refs, dst_y, dsy, dst_cb, dst_cr, dsc);
+}
+template <bool UNI_HP = false>
+MM_HD void mc_thread_in(int g, const McIn& in, const Geometry& geo, const Taps& taps, const McRec& mc,
+                        const RefDev* refs, int16_t* dst_y, int dsy, int16_t* dst_cb, int16_t* dst_cr, int dsc) {
+  mc_rec_impl<UNI_HP>(g, in, geo, taps, mc, refs, dst_y, dsy, dst_cb, dst_cr, dsc);
 }
 
 }  // namespace mmpipe
