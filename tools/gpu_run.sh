@@ -27,6 +27,7 @@ for step in "$@"; do
     prof_c5) run prof_c5 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c5 -o run --output-format csv -- python3 bench.py --config C5 --steps 5 --warmup 2 --no-cpu-baseline ;;
     c4_emulate) run c4_emulate 600 python bench.py --config C4 --c4-emulate ;;
     c4_gloo2) run c4_gloo2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --dist-backend gloo --steps 6 --warmup 2 ;;
+    per_model) run per_model 900 bash tools/per_model.sh ;;
     ubench) run ubench 300 bash -c "tools/ubench/load_check && tools/ubench/valu_rate2" ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 12 --warmup 4 --no-cpu-baseline ;;
     pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 ;;

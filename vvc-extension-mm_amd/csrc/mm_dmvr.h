@@ -11,7 +11,7 @@
 //   3. parabolic sub-pel refinement from the 5 costs around the best offset unless it lies on the
 //      window border (xDMVRSubPixelErrorSurface :2157-2175, xSubPelErrorSrfc :1996-2048);
 //   4. the sub-PU is predicted as a bi PU at merge0 + mvd / merge1 - mvd (all components, addAvg).
-// Steps 1-3 run here (k_dmvr_setup, k_dmvr_cost, k_dmvr_decide) inside the picture's device-planned
+// Steps 1-3 run here (k_dmvr_setup_dev, k_dmvr_reproj_dev + k_dmvr_sad_dev, k_dmvr_decide_dev) inside the picture's device-planned
 // launch sequence: the planner (mm_devplan.h) places every sub-PU of an MM_PUF_DMVR PU as a bi PU
 // with its reprojection jobs and a SubPuDev record pointing at them, the search runs on the
 // records, and k_dmvr_decide writes the refined MVs into those jobs before k_setup reads them --
