@@ -51,10 +51,10 @@ RED_DEVICE = ["cuda"]  # where the timing reductions run: "cpu" under the gloo r
 
 def measured_traffic(args, config):
     """HBM bytes per k_mc_dev launch from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes
-    (profiles/r02_traffic.json, tools/traffic_json.py), only when that profile was taken with
+    (profiles/r03_traffic.json, tools/traffic_json.py), only when that profile was taken with
     this very library (sha256) and the same workload; else None."""
     import hashlib
-    path = os.path.join(ROOT, "profiles", "r02_traffic.json")
+    path = os.path.join(ROOT, "profiles", "r03_traffic.json")
     if config != "C3" or args.uniform_model is not None or args.coherent_mv or not os.path.exists(path):
         return None
     d = json.load(open(path))

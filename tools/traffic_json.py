@@ -12,7 +12,7 @@ import json
 import sys
 
 ROOT = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
-OUT = sys.argv[2] if len(sys.argv) > 2 else "profiles/r02_traffic.json"
+OUT = sys.argv[2] if len(sys.argv) > 2 else "profiles/r03_traffic.json"
 PICTURES = 4  # bench.py --pictures default, used by the pmc passes of tools/gpu_run.sh
 KERNEL = "k_mc_dev"
 
