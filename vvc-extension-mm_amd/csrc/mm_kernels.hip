@@ -53,6 +53,10 @@ __global__ void k_erp_trig(SeqConst sc, int cols, int rows, float* col, float* r
   erp_trig_thread(t, sc, cols, rows, col, row);
 }
 
+__global__ void k_tan_grid(SeqConst sc, MpaCache cache, TanEntry* out) {
+  tan_grid_thread((long)blockIdx.x * blockDim.x + threadIdx.x, sc, cache, out);
+}
+
 __global__ void k_setup(SeqConst sc, const JobDev* __restrict__ jobs, int n_jobs, const M3* __restrict__ ged,
                         BlockSetup* __restrict__ out) {
   int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -747,6 +751,7 @@ struct mm_ctx {
   EpipoleMap epipoles;                            // the context's EpipoleList (mm_epipole.h)
   mm_epipole_list epi_handle{&epipoles, false};   // its C-ABI handle (mm_get_epipole_list)
   float* trig = nullptr;  // separable toSphere table of the frame grid (MpaCache::trig_col / trig_row)
+  TanEntry* tan_grid = nullptr;  // TAN's first step per grid point (MpaCache::tan_grid), when TAN is active
   float* mpa_px = nullptr;  // the three MPA planes back to back (MpaCache)
   float* mpa_py = nullptr;
   uint8_t* mpa_vip = nullptr;
@@ -844,6 +849,7 @@ static MpaCache make_cache(mm_ctx* c) {
   mc.cols = c->geo.W / 4;
   mc.rows = c->geo.H / 4;
   mc.trig_col = c->trig;
+  mc.tan_grid = c->tan_grid;
   mc.trig_row = c->trig ? c->trig + 4 * mc.cols : nullptr;
   return mc;
 }
@@ -973,6 +979,19 @@ int mm_create(const mm_seq_params* p, int device, mm_ctx** out_ctx) {
   }
   hipLaunchKernelGGL(k_erp_trig, dim3((2 * (cols + rows) + 255) / 256), dim3(256), 0, c->stream, c->sc, cols, rows,
                      c->trig, c->trig + 4 * cols);
+  // TAN's first step per grid point and flavour, 2 x 16 B x (W/4 x H/4) (37.7 MB at 6144x3072): it
+  // depends on the grid point only, so TAN elements load it instead of computing sqrt + acosf +
+  // atan2f + a sin/cos pair each (profiles/r03_ab_tan_grid.txt)
+  if (p->active_models & (1u << TANGENTIAL)) {
+    const long nt = 2L * cols * rows;
+    if (hipMalloc(&c->tan_grid, (size_t)nt * sizeof(TanEntry)) != hipSuccess) {
+      mm_destroy(c);
+      return MM_ERR_HIP;
+    }
+    MpaCache tc = make_cache(c);
+    tc.tan_grid = nullptr;
+    hipLaunchKernelGGL(k_tan_grid, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, c->stream, c->sc, tc, c->tan_grid);
+  }
   if (c->d_status.ensure(2) != hipSuccess || hipMemsetAsync(c->d_status.p, 0, 2 * sizeof(unsigned long long), c->stream) != hipSuccess ||
       c->d_mvp_status.ensure(2) != hipSuccess ||
       hipMemsetAsync(c->d_mvp_status.p, 0, 2 * sizeof(unsigned long long), c->stream) != hipSuccess ||
@@ -990,6 +1009,7 @@ int mm_destroy(mm_ctx* c) {
   (void)hipStreamSynchronize(c->stream);
   if (c->pool) (void)hipFree(c->pool);
   if (c->trig) (void)hipFree(c->trig);
+  if (c->tan_grid) (void)hipFree(c->tan_grid);
   if (c->mpa_px) (void)hipFree(c->mpa_px);
   if (c->mpa_py) (void)hipFree(c->mpa_py);
   if (c->mpa_vip) (void)hipFree(c->mpa_vip);

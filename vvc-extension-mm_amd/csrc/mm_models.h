@@ -358,15 +358,31 @@ MM_HD void block_setup_f(BlockSetup* b, const SeqConst& s, int model, bool luma,
 // grid (optional, .valid): toSphere(gx, gy) of this element, taken from the separable per-column /
 // per-row trig table of the frame grid (mm_pipeline.h MpaCache) -- the same values, computed once.
 // Passed by value: a pointer to a caller's local would keep that local in scratch memory.
+// tan (optional, .tan_valid): TAN's first step on this grid point -- (alpha, sin(eps), cos(eps)) of
+// cartesianToSpherical(toSphere(grid)), eps = pi/2 - theta (TangentialMotionModel.cpp:16-22) -- from
+// the per-grid-point table (mm_pipeline.h MpaCache::tan_grid): it depends only on the grid point and
+// the element's packet flavour, not on the block.
 struct GridSphere {
   V3 p;
-  bool valid;
+  int valid;  // int, not bool (see Math)
+  int tan_valid;
+  float alpha, se, ce;
 };
 MM_HD GridSphere no_grid() {
   GridSphere g;
   g.p = {0.0f, 0.0f, 0.0f};
-  g.valid = false;
+  g.valid = 0;
+  g.tan_valid = 0;
+  g.alpha = g.se = g.ce = 0.0f;
   return g;
+}
+// The TAN grid entry of sphere point p in flavour m (what model_motion_element computes first)
+MM_HD void tan_grid_entry(V3 p, Math m, float* alpha, float* se, float* ce) {
+  const V3 sp = cart_to_sph(p, m, true);
+  const float eps = PI_2_F - sp.y;
+  *alpha = sp.z;
+  *se = m.sin(eps);
+  *ce = m.cos(eps);
 }
 MM_HD void model_motion_element(const SeqConst& s, const BlockSetup& b, float gx, float gy, bool packet,
                                 bool mpa_cached, float pers_x, float pers_y, bool pers_vip, float* omx, float* omy,
@@ -386,7 +402,7 @@ MM_HD void model_motion_element(const SeqConst& s, const BlockSetup& b, float gx
   // switch computes q and the shared tail projects it (one copy of the acosf/atan2f code).
   const bool mpa = b.model >= MPA_FRONT_BACK && b.model <= MPA_TOP_BOTTOM;
   V3 p = {0.0f, 0.0f, 0.0f};  // toSphere(grid) of TAN / 3DT / ROT / GED
-  if (!mpa) p = grid.valid ? grid.p : erp_to_sphere(gx, gy, s, m);
+  if (!mpa && !grid.tan_valid) p = grid.valid ? grid.p : erp_to_sphere(gx, gy, s, m);
   V3 q;
   switch (b.model) {
     case MPA_FRONT_BACK:
@@ -414,11 +430,14 @@ MM_HD void model_motion_element(const SeqConst& s, const BlockSetup& b, float gx
         q = {c.z, c.y, -c.x};
     } break;
     case TANGENTIAL: {  // TangentialMotionModel.cpp:8-48
-      const V3 sp = cart_to_sph(p, m, true);
-      const float eps = PI_2_F - sp.y;
-      const float alpha = sp.z;
-      const float se = m.sin(eps);
-      const float ce = m.cos(eps);
+      float alpha, se, ce;
+      if (grid.tan_valid) {
+        alpha = grid.alpha;
+        se = grid.se;
+        ce = grid.ce;
+      } else {
+        tan_grid_entry(p, m, &alpha, &se, &ce);
+      }
       const float sE = tan_sE(b), cE = tan_cE(b), alphaC = tan_alphaC(b);
       float dA = alpha - alphaC;
       float cdA = m.cos(dA);

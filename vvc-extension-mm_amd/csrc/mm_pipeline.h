@@ -100,6 +100,11 @@ MM_HD int bcw_w1(int bcw) { return (int)((0xC7650u >> (4 * bcw)) & 15u) - 2; }
 // px / py / vip hold the three MPA planes back to back (plane pl at pl * cols * rows): the plane is
 // picked by address arithmetic, never by indexing a pointer array with a per-lane model (which
 // would copy the kernel-argument struct to scratch memory).
+// tan_grid (optional, may be null): TAN's first step per grid point and flavour (mm_models.h
+// GridSphere), [packet][gj][gi], built by k_tan_grid when TANGENTIAL is active.
+struct alignas(16) TanEntry {
+  float alpha, se, ce, pad;
+};
 struct MpaCache {
   const float* px;
   const float* py;
@@ -107,6 +112,7 @@ struct MpaCache {
   int cols, rows;  // W/4, H/4
   const float* trig_col;
   const float* trig_row;
+  const TanEntry* tan_grid;
 };
 
 // One entry of the separable toSphere table (t over 2 * cols column entries, then 2 * rows rows)
@@ -144,13 +150,35 @@ MM_HD void mpa_lookup(const MpaCache& c, int model, int gi, int gj, float* px, f
   *py = c.py[k];
   *vip = c.vip[k] != 0;
 }
-// toSphere of a non-MPA element from the trig table, when the table exists
+// What a non-MPA element needs of its grid point from the tables, when they exist: TAN's first
+// step from tan_grid, the other models' sphere point from the trig table
 MM_HD GridSphere grid_point(const MpaCache& c, int model, int gi, int gj, bool packet) {
-  if (is_mpa_model(model) || !c.trig_col) return no_grid();
-  GridSphere g;
+  GridSphere g = no_grid();
+  if (is_mpa_model(model)) return g;
+  if (model == TANGENTIAL && c.tan_grid) {
+    const TanEntry e = c.tan_grid[(packet ? (long)c.cols * c.rows : 0L) + (long)gj * c.cols + gi];
+    g.tan_valid = 1;
+    g.alpha = e.alpha;
+    g.se = e.se;
+    g.ce = e.ce;
+    return g;
+  }
+  if (!c.trig_col) return g;
   g.p = grid_sphere(c, gi, gj, packet);
-  g.valid = true;
+  g.valid = 1;
   return g;
+}
+// One entry of tan_grid (t over 2 * cols * rows: flavour, row, column)
+MM_HD void tan_grid_thread(long t, const SeqConst& sc, const MpaCache& c, TanEntry* out) {
+  const long n = (long)c.cols * c.rows;
+  if (t >= 2 * n) return;
+  const bool packet = t >= n;
+  const long k = t - (packet ? n : 0);
+  const int gj = (int)(k / c.cols), gi = (int)(k - (long)gj * c.cols);
+  TanEntry e;
+  tan_grid_entry(grid_sphere(c, gi, gj, packet), Math{packet}, &e.alpha, &e.se, &e.ce);
+  e.pad = 0.0f;
+  out[t] = e;
 }
 
 struct Geometry {
