@@ -170,13 +170,12 @@ __global__ void __launch_bounds__(PLACE_BLOCK) k_plan_place(const mm_pu_desc* __
                                                     PlanMeta* __restrict__ meta, PlanCaps caps,
                                                     JobDev* __restrict__ jobs, int* __restrict__ job_off,
                                                     int* __restrict__ job_chunk, DmvrRecs dm) {
-  __shared__ unsigned long long s_pu[N_PU_KEYS], s_job[N_JOB_KEYS];
+  __shared__ unsigned long long s_job[N_JOB_KEYS];
   __shared__ unsigned long long g_pu[N_PU_KEYS], g_job[N_JOB_KEYS], g_dm;
   __shared__ PlanMeta s_meta;
   __shared__ int s_ok;
   const int tid = threadIdx.x;
   if (blockIdx.x == 0 && tid == 0 && next_status) *next_status = 0ull;
-  if (tid < N_PU_KEYS) s_pu[tid] = 0;
   if (tid < N_JOB_KEYS) s_job[tid] = 0;
   // bucket totals and this quarter's offsets inside the buckets: the column sums of blk, split
   // over the block's 4 waves (wave w takes count rows w, w + 4, ...), plus the quarters before this
@@ -284,29 +283,41 @@ __global__ void __launch_bounds__(PLACE_BLOCK) k_plan_place(const mm_pu_desc* __
     u = pus[i];
     classify_pu(u, t, &p);
     if (p.code == MM_OK) {
-      lp = atomicAdd(&s_pu[p.key], pu_count(p));
 #pragma unroll
       for (int k = 0; k < 4; k++)
         if (p.job[k].valid) lj[k] = atomicAdd(&s_job[p.job[k].key], job_count(p, k));
     }
   }
-  // DMVR sub-PUs are placed in list order (an exclusive scan over the block, not LDS-atomic arrival
-  // order): mm_pred_dmvr returns their refined deltas PU after PU
+  // PUs (the one PU bucket) and DMVR sub-PUs are placed in list order by an exclusive scan over the
+  // block -- not in LDS-atomic arrival order: the sub-block enumeration k_mc walks follows the list
+  // (CTU raster), and mm_pred_dmvr returns its refined deltas PU after PU
+  static_assert(N_PU_KEYS == 1, "one PU bucket, placed by the scan");
   {
-    __shared__ unsigned long long s_wsum[PLACE_BLOCK / 64];
-    const unsigned long long v = (p.code == MM_OK && p.dmvr) ? dmvr_count(p) : 0ull;
+    __shared__ unsigned long long s_wsum[2][PLACE_BLOCK / 64];
+    const unsigned long long v = p.code == MM_OK ? pu_count(p) : 0ull;
+    const unsigned long long vd = (p.code == MM_OK && p.dmvr) ? dmvr_count(p) : 0ull;
     const int lane = tid & 63, w = tid >> 6;
-    unsigned long long incl = v;
+    unsigned long long incl = v, incd = vd;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-      const unsigned long long u = __shfl_up(incl, d);
-      if (lane >= d) incl += u;
+      const unsigned long long a = __shfl_up(incl, d), b = __shfl_up(incd, d);
+      if (lane >= d) {
+        incl += a;
+        incd += b;
+      }
     }
-    if (lane == 63) s_wsum[w] = incl;
+    if (lane == 63) {
+      s_wsum[0][w] = incl;
+      s_wsum[1][w] = incd;
+    }
     __syncthreads();
-    unsigned long long before = 0;
-    for (int k = 0; k < w; k++) before += s_wsum[k];
-    ld = before + incl - v;
+    unsigned long long before = 0, befd = 0;
+    for (int k = 0; k < w; k++) {
+      before += s_wsum[0][k];
+      befd += s_wsum[1][k];
+    }
+    lp = before + incl - v;
+    ld = befd + incd - vd;
   }
   if (p.code != MM_OK) return;
   const unsigned long long bp = g_pu[p.key] + lp;
