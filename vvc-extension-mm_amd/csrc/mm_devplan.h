@@ -26,25 +26,33 @@ using mmdmvr::N_OFF;
 using mmdmvr::SubPuDev;
 
 constexpr int MAX_SLOTS = 16;  // reference pictures addressable by one picture (2 lists x 8)
-// PU bucket: one.  PUs keep the list's (decode, raster CTU) order, quarter block by quarter block,
-// so the sub-block enumeration k_mc reads is spatial, and k_mc handles bi and uni sub-blocks in one
-// body (the McRec meta word says which lists a sub-block uses), so no class buckets are needed.
-// k_mc cuts the enumeration into N_BANDS equal bands, one per XCD (mm_kernels.hip k_mc_dev): each
-// band is a run of CTU rows, whose PUs' reference windows -- overlapping by the MV spread plus the
-// filter reach -- one XCD's L2 fetches once.  (Sorting by 64 picture-row bins instead measured the
-// same k_mc and a 3x slower k_plan_place: profiles/r03_ab_pu_keys.txt.)
-constexpr int N_PU_KEYS = 1;
+// PU buckets: N_BANDS vertical strips of the picture (by the PU's left column), or one bucket.
+// Inside a bucket PUs keep the list's (decode, raster-CTU) order -- k_plan_place places them with
+// a block-wide scan per bucket -- so the sub-block enumeration k_mc reads is spatial, and k_mc
+// handles bi and uni sub-blocks in one body (the McRec meta word says which lists a sub-block
+// uses), so no class buckets are needed.  k_mc runs band r on the workgroups of one XCD
+// (mm_kernels.hip k_mc_dev), so the sub-blocks an XCD has in flight share reference lines in its
+// L2: with strips (PU_STRIPS) band r is strip r, walked CTU row by CTU row -- an XCD's working set
+// is a compact region of the picture -- otherwise it is an eighth of the list (a run of CTU rows
+// across the whole width).  (64 picture-row bins measured the same k_mc as one bucket and planned
+// slower: profiles/r03_ab_pu_keys.txt; strips: profiles/r03_ab_pu_strips.txt.)
+constexpr bool PU_STRIPS = false;
 constexpr int N_BANDS = 8;
-MM_HD int pu_key(int y, int H) {
-  (void)y;
-  (void)H;
-  return 0;
+constexpr int N_PU_KEYS = PU_STRIPS ? N_BANDS : 1;
+MM_HD int pu_key(int x, int W) {
+  if (!PU_STRIPS) return 0;
+  const int k = (int)(((long)x * N_BANDS) / W);
+  return k < N_BANDS - 1 ? k : N_BANDS - 1;
 }
 
-// band r = sub-blocks [band[r], band[r + 1])
+// band r = sub-blocks [band[r], band[r + 1]): the strips' buckets, or an equal split of the list
 MM_HD void band_cut(const int* sb_base, int n_sb, int* band) {
-  (void)sb_base;
-  for (int r = 0; r <= N_BANDS; r++) band[r] = (int)((long)n_sb * r / N_BANDS);
+  for (int r = 0; r <= N_BANDS; r++) {
+    if (PU_STRIPS)
+      band[r] = r < N_PU_KEYS ? sb_base[r] : n_sb;
+    else
+      band[r] = (int)((long)n_sb * r / N_BANDS);
+  }
 }
 constexpr int N_JOB_KEYS = 64;
 constexpr int DMVR_KEY = N_PU_KEYS + N_JOB_KEYS;  // one bucket of MM-DMVR sub-PUs after the PU and job keys
@@ -228,7 +236,7 @@ MM_HD void classify_pu(const mm_pu_desc& u, const PicTables& t, PuPlan* p) {
     p->bcw = u.bcw_idx;
   }
   p->n_sb = (u.w / 4) * (u.h / 4);
-  p->key = pu_key(u.y, t.H);
+  p->key = pu_key(u.x, t.W);
 }
 
 

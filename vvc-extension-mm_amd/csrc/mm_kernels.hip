@@ -288,35 +288,42 @@ __global__ void __launch_bounds__(PLACE_BLOCK) k_plan_place(const mm_pu_desc* __
         if (p.job[k].valid) lj[k] = atomicAdd(&s_job[p.job[k].key], job_count(p, k));
     }
   }
-  // PUs (the one PU bucket) and DMVR sub-PUs are placed in list order by an exclusive scan over the
-  // block -- not in LDS-atomic arrival order: the sub-block enumeration k_mc walks follows the list
-  // (CTU raster), and mm_pred_dmvr returns its refined deltas PU after PU
-  static_assert(N_PU_KEYS == 1, "one PU bucket, placed by the scan");
+  // PUs and DMVR sub-PUs are placed in list order inside their buckets by exclusive scans over the
+  // block (one per PU bucket) -- not in LDS-atomic arrival order: the sub-block enumeration k_mc
+  // walks follows the list (CTU raster, profiles/r03_ab_scan_place.txt), and mm_pred_dmvr returns
+  // its refined deltas PU after PU
   {
-    __shared__ unsigned long long s_wsum[2][PLACE_BLOCK / 64];
-    const unsigned long long v = p.code == MM_OK ? pu_count(p) : 0ull;
-    const unsigned long long vd = (p.code == MM_OK && p.dmvr) ? dmvr_count(p) : 0ull;
+    __shared__ unsigned long long s_wsum[N_PU_KEYS + 1][PLACE_BLOCK / 64];
     const int lane = tid & 63, w = tid >> 6;
-    unsigned long long incl = v, incd = vd;
+    const bool ok = p.code == MM_OK;
+    const unsigned long long v = ok ? pu_count(p) : 0ull;
+    const unsigned long long vd = (ok && p.dmvr) ? dmvr_count(p) : 0ull;
+    unsigned long long mine = 0, incd = vd;
+#pragma unroll
+    for (int k = 0; k < N_PU_KEYS; k++) {
+      const unsigned long long vk = (ok && p.key == k) ? v : 0ull;
+      unsigned long long inc = vk;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const unsigned long long a = __shfl_up(inc, d);
+        if (lane >= d) inc += a;
+      }
+      if (lane == 63) s_wsum[k][w] = inc;
+      if (ok && p.key == k) mine = inc - vk;
+    }
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-      const unsigned long long a = __shfl_up(incl, d), b = __shfl_up(incd, d);
-      if (lane >= d) {
-        incl += a;
-        incd += b;
-      }
+      const unsigned long long b = __shfl_up(incd, d);
+      if (lane >= d) incd += b;
     }
-    if (lane == 63) {
-      s_wsum[0][w] = incl;
-      s_wsum[1][w] = incd;
-    }
+    if (lane == 63) s_wsum[N_PU_KEYS][w] = incd;
     __syncthreads();
     unsigned long long before = 0, befd = 0;
     for (int k = 0; k < w; k++) {
-      before += s_wsum[0][k];
-      befd += s_wsum[1][k];
+      if (ok) before += s_wsum[p.key][k];
+      befd += s_wsum[N_PU_KEYS][k];
     }
-    lp = before + incl - v;
+    lp = before + mine;
     ld = befd + incd - vd;
   }
   if (p.code != MM_OK) return;
