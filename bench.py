@@ -335,24 +335,31 @@ def bench_c4(args, cfg, params, rank, world, local, dist):
         bufs[b].copy_(host)
         return None
 
-    def loop_for(gop_name, ref_waits=True):
+    def loop_for(gop_name, ref_waits=True, gather_all=False):
         """A DependencyLoop whose warm-up steps are the tail of the GOP before the timed one, so
         the timed steps start at a GOP boundary.  ref_waits False: the dependency-free upper bound
-        (every all-gather hidden behind the next picture, round 2's loop)."""
+        (every all-gather hidden behind the next picture, round 2's loop).  gather_all: all-gather
+        every picture, not only the referenced ones."""
         size = len(G.GOPS[gop_name])
         start = (size - args.warmup % size) % size
         return G.DependencyLoop(gop_name, n_bufs, lambda k, poc, rr, b: ctx.run_raw(*ptrs[b]), gather,
-                                lambda h: h.wait(), start=start, ref_waits=ref_waits)
+                                lambda h: h.wait(), start=start, ref_waits=ref_waits, gather_all=gather_all)
 
     t_mc = timed(args.steps, args.warmup, mc_only, dist)
     results = {}
-    for name, gop_name, ref_waits in (("ra32", "ra32", True), ("ra8", "ra8", True), ("independent", "ra32", False)):
+    for name, gop_name, ref_waits, gather_all in (("ra32", "ra32", True, False), ("ra32_all", "ra32", True, True),
+                                                  ("ra8", "ra8", True, False), ("independent", "ra32", False, True)):
         if world == 1:
             results[name] = t_mc
             continue
-        lp = loop_for(gop_name, ref_waits)
+        lp = loop_for(gop_name, ref_waits, gather_all)
         results[name] = timed(args.steps, args.warmup, lambda s: lp.step(), dist)
     t_e2e = results["ra32"]
+    # one more picture into buffer 0, all-gathered, for the bit-exact check below
+    mc_only(0)
+    h = gather(0) if world > 1 else None
+    if h is not None:
+        h.wait()
     torch.cuda.synchronize()
     ctx.synchronize()
     # stage timing of this rank's stripe
@@ -371,7 +378,7 @@ def bench_c4(args, cfg, params, rank, world, local, dist):
         from oracle.oracle import Oracle
         orc = Oracle(params, [(cur, -1, W.GED_EPIPOLE_Q24)])
         want = orc.predict_padded(orc.padded_refs(refs), cur, pus, cfg.width, cfg.height, cpu_threads())
-        got = lay.unpack(bufs[0].cpu().numpy())
+        got = lay.unpack(bufs[0].cpu().numpy())  # (buffer 0 was last written by the gathered check picture)
         bit_exact = all(np.array_equal(g, w) for g, w in zip(got, want))
     if rank == 0:
         ag_bytes = (world - 1) * lay.seg * 2
@@ -381,15 +388,18 @@ def bench_c4(args, cfg, params, rank, world, local, dist):
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(t_e2e / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "f32+int16", "data": "synthetic (seeded ERP planes + PU list, SURVEY 8(d))",
-            "config": {"workload": f"C4: {cfg.description}, CTU-row sharded across {world} GPU(s) with one packed "
-                                   f"RCCL all-gather per picture, pictures in the reference's RA GOP-32 decode "
-                                   f"order (cfg/encoder_randomaccess_vtm.cfg), each predicted after its "
-                                   f"references' all-gathers", "width": cfg.width, "height": cfg.height,
+            "config": {"workload": f"C4: {cfg.description}, CTU-row sharded across {world} GPU(s), pictures in "
+                                   f"the reference's RA GOP-32 decode order (cfg/encoder_randomaccess_vtm.cfg): "
+                                   f"each referenced picture is rebuilt on every GPU by one packed RCCL all-gather, "
+                                   f"each picture is predicted after its references' all-gathers, unreferenced "
+                                   f"(highest temporal layer) pictures stay sharded", "width": cfg.width, "height": cfg.height,
                        "pus": int(len(pus)), "pus_rank0": int(len(mine)), "luma_area": int(area),
                        "stripe_ctu_rows": lay.rows // 128, "allgather_bytes_in_per_rank": int(ag_bytes),
                        "gop": "ra32", "timed_pictures": "decode-order pictures 0..steps-1 of a GOP",
                        "plan_ahead": bool(args.plan_ahead), "parallelism": f"ctu-row stripes x{world}"},
             "ra_gop8": dict(per(results["ra8"]), note="same loop, dyadic hierarchical-B GOP-8 decode order"),
+            "ra32_gather_every_picture": dict(per(results["ra32_all"]),
+                                              note="same loop, unreferenced pictures all-gathered too"),
             "independent": dict(per(results["independent"]),
                                 note="no reference waits: every all-gather hidden behind the next picture (upper bound)"),
             "mc_only": dict(per(t_mc), note="same loop without the all-gather (references pre-replicated)"),
@@ -413,7 +423,7 @@ def bench_c4_emulate(args, cfg, params):
     (ring, ~153 GB/s) and at all 7 links (direct, 7 x 153 GB/s): hidden behind the next picture's
     MC regardless of dependencies (max(mc, allgather), the upper bound), or in random-access decode
     order (mm360.gop.schedule: a picture waits for its references' all-gathers; the reference's
-    GOP-32 and a dyadic GOP-8)."""
+    GOP-32 and a dyadic GOP-8; only referenced pictures are all-gathered, or every one: _all)."""
     from mm360 import gop as G
     (cur, pus, refs), = picture_set(cfg, 1)
     ctx = new_ctx(params, 0, [(cur, pus, refs)])
@@ -435,8 +445,8 @@ def bench_c4_emulate(args, cfg, params):
         ag = (n - 1) / n * pic_bytes
         ring, mesh = ag / link, ag / (7 * link) if n > 1 else 0.0
         mc = worst * 1e3
-        dep = {f"{g}_{k}": round(G.schedule(64, mc, a * 1e3, g)["ms_per_picture"], 4)
-               for g in ("ra32", "ra8") for k, a in (("ring", ring), ("mesh", mesh))}
+        dep = {f"{g}{'_all' if every else ''}_{k}": round(G.schedule(64, mc, a * 1e3, g, every)["ms_per_picture"], 4)
+               for g in ("ra32", "ra8") for every in (False, True) for k, a in (("ring", ring), ("mesh", mesh))}
         out["n"][n] = {"mc_ms": round(mc, 4),
                        "allgather_ms": {"ring": round(ring * 1e3, 4), "mesh": round(mesh * 1e3, 4)},
                        "pred_ms_per_picture": {"hidden_ring": round(max(worst, ring) * 1e3, 4),

@@ -153,6 +153,7 @@ def _chain_worker(rank, world, port, n_pictures, out_dir):
         mine = P.shard_pus(_chain_pus(k, poc, refs), cfg.height, world, rank)
         planes = twin.predict(params, poc, mine, {r: decoded[r] for r in refs}, cfg.width, cfg.height, epi)
         lay.pack(planes, rank, bufs[b])
+        decoded[poc] = planes  # this rank's stripe only, until (and unless) the picture is all-gathered
         cur["poc"] = poc
 
     def gather(b):
@@ -170,6 +171,8 @@ def _chain_worker(rank, world, port, n_pictures, out_dir):
     with open(os.path.join(out_dir, f"trace{rank}.txt"), "w") as f:
         for poc, waited in loop.trace:
             f.write(f"{poc}:{','.join(map(str, waited))}\n")
+    with open(os.path.join(out_dir, f"gathered{rank}.txt"), "w") as f:
+        f.write(",".join(map(str, loop.gathered)))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -193,19 +196,23 @@ def test_decode_sequences():
 def test_schedule_model():
     """The dependency-aware model: with every all-gather shorter than the MC, each picture that
     the next one references stalls the GPUs by one all-gather; half the pictures are referenced
-    leaves' parents in both GOPs.  Without all-gathers it is the MC time."""
+    in both GOPs, so gathering only those halves a link-bound loop.  Without all-gathers it is the
+    MC time."""
     for g in ("ra32", "ra8"):
+        assert sum(G.is_referenced(p, g) for p in range(1, 65)) == 32
         assert G.schedule(64, 1.0, 0.0, g)["ms_per_picture"] == 1.0
         r = G.schedule(64, 1.0, 0.3, g)
         assert 1.0 < r["ms_per_picture"] < 1.3 and r["stall_ms_per_picture"] > 0
-        slow = G.schedule(64, 0.1, 1.0, g)  # all-gather bound
-        assert slow["ms_per_picture"] >= 1.0
+        slow_all = G.schedule(64, 0.1, 1.0, g, gather_all=True)  # all-gather bound
+        slow_ref = G.schedule(64, 0.1, 1.0, g)
+        assert slow_all["ms_per_picture"] >= 1.0 and 0.5 <= slow_ref["ms_per_picture"] <= 0.61
 
 
 def test_gloo_decode_order_chain(tmp_path):
     """C4 decode-order loop, world 2: each picture of an RA GOP-8 sequence is predicted from its
-    gathered references; every rank ends with exactly the unsharded chain, and each picture waited
-    for the all-gathers of all its references decoded in the sequence."""
+    gathered references; only referenced pictures are all-gathered (every rank then holds exactly
+    the unsharded picture), unreferenced ones stay sharded (each rank holds its stripe of it), and
+    each picture waited for the all-gathers of all its references decoded in the sequence."""
     n = 6
     port = _free_port()
     mp.spawn(_chain_worker, args=(2, port, n, str(tmp_path)), nprocs=2, join=True)
@@ -218,11 +225,20 @@ def test_gloo_decode_order_chain(tmp_path):
     for k, (poc, _, refs) in enumerate(seq):
         decoded[poc] = twin.predict(params, poc, _chain_pus(k, poc, refs), {r: decoded[r] for r in refs},
                                     cfg.width, cfg.height, epi)
+    referenced = [poc for poc, _, _ in seq if G.is_referenced(poc, "ra8")]
+    assert referenced == [8, 4, 2, 6]  # the GOP-8 leaves 1, 3 (and 5, 7) are never referenced
     for r in range(2):
         z = np.load(os.path.join(tmp_path, f"chain{r}.npz"))
+        y0, y1 = P.stripe_rows(cfg.height, 2, r)
         for poc, _, _ in seq:
             for i, c in enumerate(("y", "cb", "cr")):
-                assert np.array_equal(z[f"poc{poc}_{c}"], decoded[poc][i]), (r, poc, c)
+                got, want = z[f"poc{poc}_{c}"], decoded[poc][i]
+                if poc in referenced:  # rebuilt on every rank by the all-gather
+                    assert np.array_equal(got, want), (r, poc, c)
+                else:  # stays sharded: this rank's stripe
+                    a, b = (y0, y1) if i == 0 else (y0 // 2, y1 // 2)
+                    assert np.array_equal(got[a:b], want[a:b]), (r, poc, c)
+        assert open(os.path.join(tmp_path, f"gathered{r}.txt")).read() == ",".join(map(str, referenced))
         trace = open(os.path.join(tmp_path, f"trace{r}.txt")).read().split()
         for (poc, _, refs), line in zip(seq, trace):
             p, w = line.split(":")

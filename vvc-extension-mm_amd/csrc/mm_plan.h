@@ -233,8 +233,11 @@ struct MeBatch {
   long n_elems = 0;
 };
 
+// host_chunks false: the 64-element chunk starts are left to the device (k_me_chunks) -- at C5 they
+// are 16 M entries per call, which the host would write and copy over PCIe
 inline int plan_me_window(const SeqInfo& s, const mmdev::PicTables& t, const mm_me_block* blocks, int n,
-                          const mmme::MeWindow& w, std::vector<MeBatch>* batches, std::string* err) {
+                          const mmme::MeWindow& w, std::vector<MeBatch>* batches, std::string* err,
+                          bool host_chunks = true) {
   batches->clear();
   MeBatch cur;
   for (int i = 0; i < n; i++) {
@@ -291,7 +294,8 @@ inline int plan_me_window(const SeqInfo& s, const mmdev::PicTables& t, const mm_
     cur.n_elems += (long)w.C * nsb;
   }
   if (!cur.blocks.empty()) batches->push_back(std::move(cur));
-  for (auto& bt : *batches) build_chunks(bt.blk_off, (int)bt.n_elems, &bt.chunk);
+  if (host_chunks)
+    for (auto& bt : *batches) build_chunks(bt.blk_off, (int)bt.n_elems, &bt.chunk);
   return MM_OK;
 }
 

@@ -87,11 +87,23 @@ def decode_sequence(n_pictures: int, gop: str = "ra32", start: int = 0) -> List[
     return out
 
 
-def schedule(n_pictures: int, mc_ms: float, allgather_ms: float, gop: str = "ra32") -> Dict[str, float]:
+def is_referenced(poc: int, gop: str = "ra32") -> bool:
+    """Whether any picture of the GOP structure references `poc` (periodic: by POC modulo the GOP
+    size).  The highest temporal layer -- half the pictures, the odd POCs -- is never referenced:
+    those pictures are output only, so the sharded decoder never needs them whole on every GPU."""
+    table = GOPS[gop]
+    size = len(table)
+    residues = {(p - d) % size for p, _, l0, l1 in table for d in l0 + l1}
+    return poc % size in residues
+
+
+def schedule(n_pictures: int, mc_ms: float, allgather_ms: float, gop: str = "ra32",
+             gather_all: bool = False) -> Dict[str, float]:
     """Modelled per-picture time of the CTU-row-sharded C4 loop: picture k's MC starts when the
     GPUs are free (picture k-1's MC is done) and the all-gathers of all its references have
-    landed; every picture is all-gathered after its MC, one all-gather at a time on the links
-    (RCCL's stream serialises them).  n_pictures should be a whole number of GOPs."""
+    landed; a referenced picture (every picture with gather_all) is all-gathered after its MC, one
+    all-gather at a time on the links (RCCL's stream serialises them).  n_pictures should be a
+    whole number of GOPs."""
     seq = decode_sequence(n_pictures, gop)
     landed: Dict[int, float] = {}
     t_mc = 0.0
@@ -101,8 +113,9 @@ def schedule(n_pictures: int, mc_ms: float, allgather_ms: float, gop: str = "ra3
         ready = max([t_mc] + [landed.get(r, 0.0) for r in refs])
         stall += ready - t_mc
         t_mc = ready + mc_ms
-        link = max(t_mc, link) + allgather_ms
-        landed[poc] = link
+        if gather_all or is_referenced(poc, gop):
+            link = max(t_mc, link) + allgather_ms
+            landed[poc] = link
     total = max(t_mc, link)
     return {"ms_per_picture": total / n_pictures, "stall_ms_per_picture": stall / n_pictures}
 
@@ -110,13 +123,17 @@ def schedule(n_pictures: int, mc_ms: float, allgather_ms: float, gop: str = "ra3
 class DependencyLoop:
     """Drives the picture loop of one rank in decode order: before picture k is predicted, the
     all-gathers of its references are waited for (`wait(handle)`, a stream wait for RCCL); then
-    `predict(k, buf)` writes the rank's stripe and `gather(buf)` starts the picture's all-gather
-    and returns its handle.  Picture buffers rotate over `n_bufs`; a buffer is reused only after
-    its previous picture's all-gather is done.  A None handle (a synchronous all-gather) is never
-    waited for.  ref_waits False drops the reference waits (the dependency-free upper bound)."""
+    `predict(k, poc, refs, buf)` writes the rank's stripe and, for a picture that later pictures
+    reference (every picture with gather_all), `gather(buf)` starts its all-gather and returns its
+    handle; an unreferenced picture stays sharded (each rank outputs its own stripe).  Picture
+    buffers rotate over `n_bufs`; a buffer is reused only after its previous picture's all-gather
+    is done.  A None handle (a synchronous all-gather) is never waited for.  ref_waits False drops
+    the reference waits (the dependency-free upper bound)."""
 
-    def __init__(self, gop: str, n_bufs: int, predict, gather, wait, start: int = 0, ref_waits: bool = True):
-        self.gop, self.n_bufs, self.ref_waits = gop, n_bufs, ref_waits
+    def __init__(self, gop: str, n_bufs: int, predict, gather, wait, start: int = 0, ref_waits: bool = True,
+                 gather_all: bool = False):
+        self.gop, self.n_bufs, self.ref_waits, self.gather_all = gop, n_bufs, ref_waits, gather_all
+        self.gathered: List[int] = []  # POCs all-gathered, in decode order
         self.predict, self.gather, self.wait = predict, gather, wait
         self.k = start
         self.handles: Dict[int, object] = {}
@@ -135,9 +152,12 @@ class DependencyLoop:
         if self.buf_handle[b] is not None:
             self.wait(self.buf_handle[b])
         self.predict(self.k, poc, refs, b)
-        h = self.gather(b)
+        h = None
+        if self.gather_all or is_referenced(poc, self.gop):
+            h = self.gather(b)
+            self.gathered.append(poc)
+            self.handles[poc] = h
         self.buf_handle[b] = h
-        self.handles[poc] = h
         for old in [p for p in self.handles if p < poc - 2 * len(GOPS[self.gop])]:
             del self.handles[old]
         self.trace.append((poc, waited))
