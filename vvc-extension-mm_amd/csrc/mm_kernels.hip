@@ -386,10 +386,11 @@ __global__ void __launch_bounds__(256) k_reproj_dev(SeqConst sc, const PlanMeta*
 // Band-per-XCD mapping: the sub-blocks are enumerated bin by bin in picture order and cut into
 // N_BANDS = 8 bands of about equal size (mm_devplan.h band_cut).  Workgroup b predicts band b % 8 --
 // workgroups b and b + 8 share an XCD under the round-robin dealing (MI355X_MICROARCH.md, workgroup
-// dispatch; speed only, results do not depend on it) -- looping over the band's 256-sub-block
-// blocks b / 8, b / 8 + gridDim / 8, ..., so each XCD walks one band of the picture in decode order
-// and keeps the reference rows that the band's neighbouring PUs share in its own L2.  Every
-// workgroup stages the tap tables and the reference table in LDS once for all its blocks.
+// dispatch; speed only, results do not depend on it) -- taking the band's 256-sub-block blocks
+// b / 8, b / 8 + gridDim / 8, ... (one block per workgroup with MC_BLOCKS_PER_WG = 1), so each XCD
+// walks one band of the picture in decode order and keeps the reference rows that the band's
+// neighbouring PUs share in its own L2.  Every workgroup stages the tap tables and the reference
+// table in LDS once for all its blocks.
 static_assert(N_BANDS == 8, "one band per XCD");
 template <bool UNI_HP>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_mc_dev(Geometry geo, const PlanMeta* __restrict__ meta, McRec mc,
@@ -423,7 +424,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
     cur = nxt;
   }
 }
-constexpr int MC_BLOCKS_PER_XCD = 128;  // 32 CUs x 4 workgroups (16 waves per CU at 4 per SIMD)
+// k_mc grid: enough workgroups for MC_BLOCKS_PER_WG blocks of its band each (the band sizes are only
+// known on the device; bands are at most ceil(sub-block capacity / 8) long).  One block per workgroup
+// measured faster than a persistent 8 x 128 grid (profiles/r03_ab_mc_grid.txt): the dispatcher
+// balances the workgroups over the CUs, and workgroups of the next picture's planning kernels that
+// hold CU slots under plan-ahead no longer fix a late start to a persistent workgroup's whole share.
+constexpr int MC_BLOCKS_PER_WG = 1;
 // plan-ahead gate: the next picture's planning may start once this picture's reprojection is done
 // (true: it overlaps k_mc) or once the previous picture is done (false: it overlaps k_reproj)
 constexpr bool GATE_AFTER_REPROJ = false;
@@ -1405,7 +1411,7 @@ static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables
   const int gp = (n + PLAN_BLOCK - 1) / PLAN_BLOCK;
   const int gs = (k.jobs + 255) / 256;
   const int gr = round_grid((k.elems + 255) / 256);
-  const int gm = 8 * std::max(1, std::min(MC_BLOCKS_PER_XCD, (k.sb / 8 + 255) / 256));
+  const int gm = 8 * std::max(1, (((k.sb + 7) / 8 + 255) / 256 + MC_BLOCKS_PER_WG - 1) / MC_BLOCKS_PER_WG);
   const int gq = (n + PLACE_BLOCK - 1) / PLACE_BLOCK;
   hipLaunchKernelGGL(k_plan_count, dim3(gp), dim3(PLAN_BLOCK), 0, st, d_in, n, base, t, status, S.blk.p, S.blkq.p, gq);
   const DmvrRecs dm{S.dmvr_sub.p, S.dmvr_off.p, S.dmvr_chunk.p};
