@@ -15,6 +15,7 @@
 // _dev variants read their sizes from the device plan.)
 // Reference planes stay resident in HBM, unpadded; the edge-replication margin of the reference
 // is realised by address clamping (identical results, no padded copies).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -430,9 +431,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
 // balances the workgroups over the CUs, and workgroups of the next picture's planning kernels that
 // hold CU slots under plan-ahead no longer fix a late start to a persistent workgroup's whole share.
 constexpr int MC_BLOCKS_PER_WG = 1;
-// plan-ahead gate: the next picture's planning may start once this picture's reprojection is done
-// (true: it overlaps k_mc) or once the previous picture is done (false: it overlaps k_reproj)
-constexpr bool GATE_AFTER_REPROJ = false;
+// Plan-ahead events bound to kernel dispatches (hipExtLaunchKernelGGL stop events): ev_plan completes
+// with k_setup_dev and a slot's gate with its k_mc_dev, so no marker packet sits between two
+// pictures on the context stream (profiles/r03_ab_kernel_events.txt).
+constexpr bool KERNEL_EVENTS = true;
 
 // --------------------------------------------------------------------------------------------
 // Encoder candidate windows (mm_sad_window, mm_me.h)
@@ -809,13 +811,12 @@ struct mm_ctx {
   hipStream_t aux = nullptr;    // odd stripes run here, overlapping the even stripes' kernels
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int n_stripes = MM_DEFAULT_STRIPES;
-  // plan-ahead (mm_set_plan_ahead): a picture's planning + setup run on `aux` once the context
-  // stream has reached the gate of the previous call, concurrently with that call's
-  // interpolation; the context stream waits for ev_plan before the reprojection
+  // plan-ahead (mm_set_plan_ahead): a picture's planning + setup run on `aux` once its slot's gate
+  // (the previous user's k_mc_dev) is done, concurrently with the previous call's kernels; the
+  // context stream waits for ev_plan before the reprojection
   bool plan_ahead = false;
   int ahead_par = 0;                               // slot of the next plan-ahead picture
-  hipEvent_t ev_gate[2] = {nullptr, nullptr};      // alternate: the last recorded one gates the next call
-  int gate_par = 0;
+  hipEvent_t ev_gate[2] = {nullptr, nullptr};      // ev_gate[s]: the last k_mc_dev using slot s is done
   hipEvent_t ev_plan = nullptr;
   // validation status words, one per picture, ping-pong: a picture reports into d_status[pic_par]
   // and its first stripe zeroes the other word for the next picture
@@ -996,7 +997,7 @@ int mm_create(const mm_seq_params* p, int device, mm_ctx** out_ctx) {
       hipEventCreateWithFlags(&c->ev_plan, SYNC) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_epi, SYNC) != hipSuccess ||
       hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
-      hipEventRecord(c->ev_gate[0], c->stream) != hipSuccess) {
+      hipEventRecord(c->ev_gate[0], c->stream) != hipSuccess || hipEventRecord(c->ev_gate[1], c->stream) != hipSuccess) {
     mm_destroy(c);
     return MM_ERR_HIP;
   }
@@ -1402,7 +1403,7 @@ static bool slot_fits(const PlanSlot& S, int n, bool dmvr) { return n <= S.n_ens
 static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables& t, const Geometry& geo,
                          const mm_pu_desc* d_in, int n, int base, unsigned long long* status,
                          unsigned long long* next_status, int16_t* dy, ptrdiff_t sdy, int16_t* dcb, int16_t* dcr,
-                         ptrdiff_t sdc, bool plan_ahead = false, bool want_mvd = false) {
+                         ptrdiff_t sdc, bool plan_ahead = false, bool want_mvd = false, hipEvent_t mc_done = nullptr) {
   // plan-ahead: `st` is the auxiliary stream for the planning kernels; the rest runs on the
   // context stream (which may be the null stream, so a flag, not a null handle, says so)
   hipStream_t st_back = c->stream;
@@ -1438,9 +1439,14 @@ static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables
     hipLaunchKernelGGL(k_dmvr_decide_dev, dim3(std::max(1, std::min(DMVR_GRID, (k.subs + 255) / 256))), dim3(256), 0, st,
                        S.meta.p, S.dmvr_sub.p, c->d_dmvr_cost.p, S.jobs.p, want_mvd ? c->d_dmvr_mvd.p : nullptr);
   }
-  hipLaunchKernelGGL(k_setup_dev, dim3(gs), dim3(256), 0, st, c->sc, S.meta.p, S.jobs.p, t, S.setup.p);
+  if (back && KERNEL_EVENTS) {  // plan-ahead: ev_plan completes with k_setup_dev
+    hipExtLaunchKernelGGL(k_setup_dev, dim3(gs), dim3(256), 0, st, nullptr, c->ev_plan, 0, c->sc, S.meta.p, S.jobs.p, t,
+                          S.setup.p);
+  } else {
+    hipLaunchKernelGGL(k_setup_dev, dim3(gs), dim3(256), 0, st, c->sc, S.meta.p, S.jobs.p, t, S.setup.p);
+    if (back) HIPCHK(c, hipEventRecord(c->ev_plan, st));
+  }
   if (back) {  // plan-ahead: reprojection and interpolation on the context stream
-    HIPCHK(c, hipEventRecord(c->ev_plan, st));
     HIPCHK(c, hipStreamWaitEvent(st_back, c->ev_plan, 0));
     st = st_back;
   }
@@ -1454,12 +1460,16 @@ static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables
   }
   hipLaunchKernelGGL(k_reproj_dev, dim3(gr), dim3(256), 0, st, c->sc, S.meta.p, S.jobs.p, S.job_off.p, S.job_chunk.p,
                      S.setup.p, make_cache(c), mc);
-  if (plan_ahead && GATE_AFTER_REPROJ) HIPCHK(c, hipEventRecord(c->ev_gate[c->gate_par], st));
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[2], st));
+  // mc_done (plan-ahead): the slot's gate, complete when this k_mc is
+  hipEvent_t stop = KERNEL_EVENTS ? mc_done : nullptr;
   if (geo.hp)
-    hipLaunchKernelGGL(k_mc_dev<true>, dim3(gm), dim3(256), 0, st, geo, S.meta.p, mc, t, dy, (int)sdy, dcb, dcr, (int)sdc);
+    hipExtLaunchKernelGGL(k_mc_dev<true>, dim3(gm), dim3(256), 0, st, nullptr, stop, 0, geo, S.meta.p, mc, t, dy, (int)sdy, dcb,
+                          dcr, (int)sdc);
   else
-    hipLaunchKernelGGL(k_mc_dev<false>, dim3(gm), dim3(256), 0, st, geo, S.meta.p, mc, t, dy, (int)sdy, dcb, dcr, (int)sdc);
+    hipExtLaunchKernelGGL(k_mc_dev<false>, dim3(gm), dim3(256), 0, st, nullptr, stop, 0, geo, S.meta.p, mc, t, dy, (int)sdy,
+                          dcb, dcr, (int)sdc);
+  if (mc_done && !KERNEL_EVENTS) HIPCHK(c, hipEventRecord(mc_done, st));
   HIPCHK(c, hipGetLastError());
   return MM_OK;
 }
@@ -1497,9 +1507,8 @@ static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, in
   unsigned long long* status = c->d_status.p + c->pic_par;
   unsigned long long* next_status = c->d_status.p + (c->pic_par ^ 1);
   if (may_plan_ahead && c->plan_ahead && K == 1 && !c->stage_timing) {
-    // Plan-ahead: planning + setup of this picture on `aux`, gated only by the context stream's
-    // position at the start of the previous call (its slot's previous user, two calls back, has
-    // finished there), so they overlap the previous picture's interpolation.
+    // Plan-ahead: planning + setup of this picture on `aux`, gated only by the k_mc_dev of the
+    // slot's previous user (two calls back), so they overlap the previous picture's kernels.
     if (!slot_fits(c->slot[0], per, dmvr) || !slot_fits(c->slot[1], per, dmvr)) {
       // growing frees buffers the other stream may still use, and zeroes on the context stream
       HIPCHK(c, hipStreamSynchronize(c->aux));
@@ -1509,13 +1518,12 @@ static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, in
     } else {
       for (int s = 0; s < 2; s++) RCCHK(ensure_slot_buffers(c, c->slot[s], per, dmvr));  // caps only
     }
-    HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_gate[c->gate_par], 0));
-    c->gate_par ^= 1;
-    if (!GATE_AFTER_REPROJ) HIPCHK(c, hipEventRecord(c->ev_gate[c->gate_par], c->stream));
+    // the slot's previous user (two calls back) has finished its k_mc_dev
+    HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_gate[c->ahead_par], 0));
     c->timed = c->call_timing;
     if (c->timed) HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     RCCHK(launch_stripe(c, c->slot[c->ahead_par], c->aux, t, geo, d_in, n, 0, status, next_status, dy, sdy, dcb, dcr,
-                        sdc, true, want_mvd));
+                        sdc, true, want_mvd, c->ev_gate[c->ahead_par]));
     c->ahead_par ^= 1;
     if (c->timed) HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     c->last_status = status;
@@ -1548,9 +1556,9 @@ static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, in
   if (c->timed) HIPCHK(c, hipEventRecord(c->ev1, c->stream));
   // a following plan-ahead call starts its planning only after this whole call (both slots used);
   // while plan-ahead is off, mm_set_plan_ahead records the gates when it is switched on
-  if (c->plan_ahead) {
-    c->gate_par ^= 1;
-    HIPCHK(c, hipEventRecord(c->ev_gate[c->gate_par], c->stream));
+  if (c->plan_ahead) {  // both slots may have been used by this call's stripes
+    HIPCHK(c, hipEventRecord(c->ev_gate[0], c->stream));
+    HIPCHK(c, hipEventRecord(c->ev_gate[1], c->stream));
   }
   c->last_status = status;
   c->pic_par ^= 1;
