@@ -1,0 +1,10 @@
+#!/bin/bash
+# A/B of library variants (tools/build_variant.sh) with extra bench arguments:
+#   tools/ab_args.sh "<bench args>" variant...
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+extra=$1; shift
+for v in "$@"; do
+  timeout -k 10 300 python3 bench.py --steps 5 --warmup 2 --kernel-steps 10 --no-cpu-baseline $extra --lib tmp_variants/$v/libmm360.so > gpurun_out/ab_$v.log 2>&1 || { echo "variant $v failed"; tail -5 gpurun_out/ab_$v.log; exit 1; }
+  python3 -c "import json,sys; d=json.loads(open('gpurun_out/ab_$v.log').read().strip().splitlines()[-1]); print('$v', d['value'], d['ms_per_step'], d['bit_exact'], d['stages_ms'])"
+done

@@ -435,6 +435,7 @@ constexpr int MC_BLOCKS_PER_WG = 1;
 // with k_setup_dev and a slot's gate with its k_mc_dev, so no marker packet sits between two
 // pictures on the context stream (profiles/r03_ab_kernel_events.txt).
 constexpr bool KERNEL_EVENTS = true;
+constexpr bool GATE_NO_FENCE = true;
 
 // --------------------------------------------------------------------------------------------
 // Encoder candidate windows (mm_sad_window, mm_me.h)
@@ -986,14 +987,18 @@ int mm_create(const mm_seq_params* p, int device, mm_ctx** out_ctx) {
   // writes back the L2 after each picture's 57 MB of output: ~5 us per event, ~17 us per picture
   // with the three events a call records (profiles/r03_ab_event_scope.txt).
   constexpr unsigned TIMED = hipEventReleaseToDevice, SYNC = hipEventDisableTiming | hipEventReleaseToDevice;
+  // the plan-ahead slot gates order the next planning after a k_mc_dev (a write-after-read on the
+  // slot's records) and publish nothing, so they skip the release: with one, the gate's completion
+  // writes k_mc_dev's dirty output lines back from every XCD's L2 before either queue moves on
+  constexpr unsigned GATE = GATE_NO_FENCE ? hipEventDisableTiming | hipEventDisableSystemFence : SYNC;
   if (hipEventCreateWithFlags(&c->ev0, TIMED) != hipSuccess || hipEventCreateWithFlags(&c->ev1, TIMED) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_stage[0], TIMED) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_stage[1], TIMED) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_stage[2], TIMED) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, SYNC) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_join, SYNC) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_gate[0], SYNC) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_gate[1], SYNC) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_gate[0], GATE) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_gate[1], GATE) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_plan, SYNC) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_epi, SYNC) != hipSuccess ||
       hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
