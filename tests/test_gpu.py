@@ -396,6 +396,55 @@ def test_pred_plan_ahead_rotating_pictures():
         assert ctx.status() == (mm360.MM_OK, -1)
 
 
+def test_pred_plan_ahead_interleaved_call_kinds():
+    """Plan-ahead stays on while other call kinds use the plan slots in between: a 2-stripe call
+    (both slots, context and auxiliary streams), a per-list call (mm_pred_list) and a host-list
+    call (mm_pred), each followed by plan-ahead device calls that reuse the slots.  The slot gates
+    (events bound to the k_mc_dev of each slot's last user) must order every reuse; every output
+    == the oracle."""
+    cfg = W.CONFIGS["C2"]
+    params = mm360.seq_params(cfg.width, cfg.height, cfg.models)
+    lists = [W.pu_list(cfg, frame=f) for f in (11, 12, 13)]
+    refs = {poc: W.ref_planes(cfg.width, cfg.height, poc) for poc in W.REF_POCS}
+    orc = Oracle(params, EPI)
+    want = [orc.predict(W.CUR_POC, p, refs, cfg.width, cfg.height) for p in lists]
+    l0 = lists[0][lists[0]["ref_poc"][:, 0] >= 0]
+    want_l0 = orc.predict_list(W.CUR_POC, l0, 0, False, refs, cfg.width, cfg.height)
+    with _ctx(params) as ctx:
+        _upload(ctx, refs)
+        d_lists = [mm360.pus_to_device(p) for p in lists]
+        torch.cuda.synchronize()
+        ctx.set_plan_ahead(True)
+        checks = []
+
+        def dev(k):
+            o = _planes(cfg)
+            ctx.predict_device(W.CUR_POC, d_lists[k], *o)
+            checks.append((o, want[k], f"device list {k}"))
+
+        dev(0)
+        dev(1)
+        ctx.set_stripes(2)
+        o = _planes(cfg)
+        ctx.predict(W.CUR_POC, lists[2], *o)  # host list, two stripes on both streams
+        checks.append((o, want[2], "2-stripe host call"))
+        ctx.set_stripes(1)
+        dev(1)
+        dev(2)
+        o = _planes(cfg)
+        ctx.predict_list(W.CUR_POC, l0, 0, False, *o)
+        checks.append((o, want_l0, "per-list call"))
+        dev(0)
+        dev(2)
+        dev(1)
+        assert ctx.status() == (mm360.MM_OK, -1)
+        torch.cuda.synchronize()
+        for o, w, what in checks:
+            for x, t, name in zip(w, o, ("y", "cb", "cr")):
+                got = t.cpu().numpy()
+                assert np.array_equal(got, x), (what, plane_mismatch(name, got, x))
+
+
 def test_c4_stripe_sublists_into_packed_picture():
     """C4 on one GPU: each of the 8 CTU-row stripe sub-lists of the C3 PU list (one per rank of an
     8-GPU node) is predicted through the C-ABI straight into its segment of the stripe-major packed
