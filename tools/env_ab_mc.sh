@@ -1,4 +1,5 @@
 #!/bin/bash
+# (the MM_AB_* knobs exist only on branch exp/mc-pair-lanes; profiles/r03_ab_mc_pair.txt)
 # A/B of the paired-lane k_mc and the plan-ahead gate position through the library's temporary
 # MM_AB_* knobs (mm_create): MM_AB_MC_OLD=1 old one-lane k_mc; MM_AB_GATE=1 gate the next picture's
 # planning after k_reproj instead of k_mc; MM_AB_MC_LDS=<bytes> dynamic LDS per k_mc_pair_dev

@@ -347,74 +347,6 @@ __device__ __forceinline__ void predict_subblock_pool(const RefPool& pool, uint3
   const PtrRows rows{pool.base + plane_off + soff + (long)((yPos - H0) * stride + x0) * 2, stride * 2};
   predict_rows<NT, SBW, SBH>(rows, ht, vt, bi, bd, out);
 }
-
-// Luma 8-tap 4x4 by a pair of lanes (k_mc_pair_dev): lanes 2k (h = 0) and 2k + 1 (h = 1) predict one
-// sub-block together, lane h taking output columns 2h and 2h + 1 at the 14-bit intermediate (bi).
-// Output column c reads dwords (c >> 1) .. (c >> 1) + 4 of the 6-dword window row (predict_rows), so
-// lane h needs d[h .. h + 4]: h = 0 loads d0..d3 and h = 1 loads d2..d5 -- one 16-byte load per lane
-// and row, so a row's bytes are fetched once per pair instead of as x4 + x2 by every lane -- and each
-// takes its fifth dword from the partner lane (one v_mov_dpp quad_perm [1,0,3,2]): h = 0 receives d4
-// (the partner's third dword), h = 1 receives d1 (the partner's second).  The registers
-// Rg = {own0..own3, recv} are d0..d4 for h = 0 and d2, d3, d4, d5, d1 for h = 1, so lane h = 1 pairs
-// Rg[j] with tap pair (j + 1) % 5: the dot2 chains are the same instructions in both lanes and the
-// integer sums are those of predict_rows (exact, order-independent).
-// `base`: byte address of this lane's first dword in window row 0; out[r * 2 + cc] = column 2h + cc.
-__device__ __forceinline__ uint32_t swap_pair_lanes_(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-}
-__device__ __forceinline__ void predict_luma_pair(const char* base, int row_bytes, int h, const uint32_t* __restrict__ ht,
-                                                  const uint32_t* __restrict__ vt, int bd, int16_t* out) {
-  constexpr int R = 11, NP = 4, NQ = 5, RP = 6;
-  const FiltParam fh = filt_param(true, false, bd);
-  const FiltParam fv = filt_param(false, false, bd);
-  uint32_t he[NQ], ho[NQ], ve[NP], vo[NQ];
-#pragma unroll
-  for (int k = 0; k < NQ; k++) {
-    const int kk = (k + 1 < NQ) ? k + 1 : 0;  // rotated pair index of lane h = 1
-    he[k] = h ? ht[kk] : ht[k];
-    ho[k] = h ? ht[NQ + kk] : ht[NQ + k];
-    vo[k] = vt[NP + k];
-  }
-#pragma unroll
-  for (int k = 0; k < NP; k++) ve[k] = vt[k];
-  typedef uint32_t u4 __attribute__((ext_vector_type(4), aligned(4)));
-  uint32_t tmp[R + 1][2];
-  tmp[R][0] = tmp[R][1] = 0u;
-#pragma unroll
-  for (int r = 0; r < R; r++) {
-    const u4 a = *reinterpret_cast<const u4*>(base + (long)r * row_bytes);
-    const uint32_t recv = swap_pair_lanes_(h ? a.z : a.y);
-    const uint32_t rg[NQ] = {a.x, a.y, a.z, a.w, recv};
-#pragma unroll
-    for (int cc = 0; cc < 2; cc++) {
-      const uint32_t* tp = cc ? ho : he;
-      int sum = dot2_seed_(rg[0], tp[0], fh.offset);
-#pragma unroll
-      for (int k = 1; k < NQ; k++) sum = dot2_(rg[k], tp[k], sum);
-      tmp[r][cc] = (uint32_t)(sum >> fh.shift);
-    }
-  }
-#pragma unroll
-  for (int cc = 0; cc < 2; cc++) {
-    uint32_t pr[RP];
-#pragma unroll
-    for (int m = 0; m < RP; m++) pr[m] = pack_lo16_(tmp[2 * m][cc], tmp[2 * m + 1][cc]);
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      int sum;
-      if (r & 1) {
-        sum = dot2_seed_(pr[r >> 1], vo[0], fv.offset);
-#pragma unroll
-        for (int k = 1; k < NQ; k++) sum = dot2_(pr[(r >> 1) + k], vo[k], sum);
-      } else {
-        sum = dot2_seed_(pr[r >> 1], ve[0], fv.offset);
-#pragma unroll
-        for (int k = 1; k < NP; k++) sum = dot2_(pr[(r >> 1) + k], ve[k], sum);
-      }
-      out[r * 2 + cc] = (int16_t)(sum >> fv.shift);
-    }
-  }
-}
 #else
 // predict_subblock for an interior window (host): same arithmetic, window rows read with wide loads
 template <int NT, int SBW, int SBH>

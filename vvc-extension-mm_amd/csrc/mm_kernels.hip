@@ -425,32 +425,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
     cur = nxt;
   }
 }
-// The picture path's k_mc with a pair of lanes per sub-block (mmpipe::mc_pair_impl): a workgroup
-// predicts 128 sub-blocks of its band (band = blockIdx % 8, block = blockIdx / 8, as k_mc_dev).
-constexpr int MC_PAIR_SB = 128;
-__global__ void __launch_bounds__(256) k_mc_pair_dev(Geometry geo, const PlanMeta* __restrict__ meta, McRec mc,
-                                                     const PicTables t, int16_t* __restrict__ dst_y, int dsy,
-                                                     int16_t* __restrict__ dst_cb, int16_t* __restrict__ dst_cr, int dsc) {
-  const int band = blockIdx.x & 7;
-  const int n_sb = meta->n_sb;
-  const int b0 = meta->band[band], b1 = min(meta->band[band + 1], n_sb);
-  __shared__ PackedTaps s_taps;
-  __shared__ RefDev s_ref[MAX_SLOTS];
-  const int first = b0 + (int)(blockIdx.x >> 3) * MC_PAIR_SB;
-  if (first >= b1) return;  // whole workgroup past the band's end
-  if (threadIdx.x < sizeof(PackedTaps) / 16)
-    reinterpret_cast<uint4*>(&s_taps)[threadIdx.x] = reinterpret_cast<const uint4*>(&c_packed_taps)[threadIdx.x];
-  if (threadIdx.x < sizeof(s_ref) / 8)
-    reinterpret_cast<uint2*>(s_ref)[threadIdx.x] = reinterpret_cast<const uint2*>(t.ref)[threadIdx.x];
-  __syncthreads();
-  const Taps taps{c_luma_taps, c_chroma_taps, &s_taps, t.pool};
-  const int g = first + (int)(threadIdx.x >> 1);
-#if defined(__HIP_DEVICE_COMPILE__)  // mc_pair_impl is device code only (no host twin: mc_thread_rec is that)
-  if (g < b1) mc_pair_impl(g, (int)(threadIdx.x & 1), mc_rec_load(mc, g), geo, taps, mc, s_ref, dst_y, dsy, dst_cb, dst_cr, dsc);
-#endif
-}
-constexpr bool MC_PAIRED = true;
-
 // k_mc grid: enough workgroups for MC_BLOCKS_PER_WG blocks of its band each (the band sizes are only
 // known on the device; bands are at most ceil(sub-block capacity / 8) long).  One block per workgroup
 // measured faster than a persistent 8 x 128 grid (profiles/r03_ab_mc_grid.txt): the dispatcher
@@ -843,8 +817,6 @@ struct mm_ctx {
   // context stream waits for ev_plan before the reprojection
   bool plan_ahead = false;
   int ahead_par = 0;                               // slot of the next plan-ahead picture
-  // A/B knobs (temporary): dynamic LDS of k_mc_pair_dev, plan-ahead gate after k_reproj, old k_mc
-  int ab_mc_lds = 0, ab_gate = 0, ab_mc_old = 0;
   hipEvent_t ev_gate[2] = {nullptr, nullptr};      // ev_gate[s]: the last k_mc_dev using slot s is done
   hipEvent_t ev_plan = nullptr;
   // validation status words, one per picture, ping-pong: a picture reports into d_status[pic_par]
@@ -1009,9 +981,6 @@ int mm_create(const mm_seq_params* p, int device, mm_ctx** out_ctx) {
   c->geo.hp = 0;
   c->geo.store = 3;
   c->geo.padded = 1;
-  if (const char* e = getenv("MM_AB_MC_LDS")) c->ab_mc_lds = atoi(e);
-  if (const char* e = getenv("MM_AB_GATE")) c->ab_gate = atoi(e);
-  if (const char* e = getenv("MM_AB_MC_OLD")) c->ab_mc_old = atoi(e);
   // Every event the library records is a device-scope release: it orders work between the
   // context and auxiliary streams and times it, and never publishes device memory to the host
   // (status words and results reach the host through copies).  The default system-scope release
@@ -1439,8 +1408,7 @@ static bool slot_fits(const PlanSlot& S, int n, bool dmvr) { return n <= S.n_ens
 static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables& t, const Geometry& geo,
                          const mm_pu_desc* d_in, int n, int base, unsigned long long* status,
                          unsigned long long* next_status, int16_t* dy, ptrdiff_t sdy, int16_t* dcb, int16_t* dcr,
-                         ptrdiff_t sdc, bool plan_ahead = false, bool want_mvd = false, hipEvent_t mc_done = nullptr,
-                         hipEvent_t reproj_done = nullptr) {
+                         ptrdiff_t sdc, bool plan_ahead = false, bool want_mvd = false, hipEvent_t mc_done = nullptr) {
   // plan-ahead: `st` is the auxiliary stream for the planning kernels; the rest runs on the
   // context stream (which may be the null stream, so a flag, not a null handle, says so)
   hipStream_t st_back = c->stream;
@@ -1450,7 +1418,6 @@ static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables
   const int gs = (k.jobs + 255) / 256;
   const int gr = round_grid((k.elems + 255) / 256);
   const int gm = 8 * std::max(1, (((k.sb + 7) / 8 + 255) / 256 + MC_BLOCKS_PER_WG - 1) / MC_BLOCKS_PER_WG);
-  const int gmp = 8 * std::max(1, ((k.sb + 7) / 8 + MC_PAIR_SB - 1) / MC_PAIR_SB);
   const int gq = (n + PLACE_BLOCK - 1) / PLACE_BLOCK;
   hipLaunchKernelGGL(k_plan_count, dim3(gp), dim3(PLAN_BLOCK), 0, st, d_in, n, base, t, status, S.blk.p, S.blkq.p, gq);
   const DmvrRecs dm{S.dmvr_sub.p, S.dmvr_off.p, S.dmvr_chunk.p};
@@ -1496,17 +1463,14 @@ static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables
     mc.cpos[l] = S.mc_cpos[l].p;
     for (int q = 0; q < 2; q++) mc.far[l][q] = S.mc_far[l][q].p;
   }
-  hipExtLaunchKernelGGL(k_reproj_dev, dim3(gr), dim3(256), 0, st, nullptr, reproj_done, 0, c->sc, S.meta.p, S.jobs.p,
-                        S.job_off.p, S.job_chunk.p, S.setup.p, make_cache(c), mc);
+  hipLaunchKernelGGL(k_reproj_dev, dim3(gr), dim3(256), 0, st, c->sc, S.meta.p, S.jobs.p, S.job_off.p, S.job_chunk.p,
+                     S.setup.p, make_cache(c), mc);
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[2], st));
   // mc_done (plan-ahead): the slot's gate, complete when this k_mc is
   hipEvent_t stop = KERNEL_EVENTS ? mc_done : nullptr;
   if (geo.hp)
     hipExtLaunchKernelGGL(k_mc_dev<true>, dim3(gm), dim3(256), 0, st, nullptr, stop, 0, geo, S.meta.p, mc, t, dy, (int)sdy, dcb,
                           dcr, (int)sdc);
-  else if (MC_PAIRED && geo.padded && !c->ab_mc_old)
-    hipExtLaunchKernelGGL(k_mc_pair_dev, dim3(gmp), dim3(256), c->ab_mc_lds, st, nullptr, stop, 0, geo, S.meta.p, mc, t, dy, (int)sdy,
-                          dcb, dcr, (int)sdc);
   else
     hipExtLaunchKernelGGL(k_mc_dev<false>, dim3(gm), dim3(256), 0, st, nullptr, stop, 0, geo, S.meta.p, mc, t, dy, (int)sdy,
                           dcb, dcr, (int)sdc);
@@ -1564,8 +1528,7 @@ static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, in
     c->timed = c->call_timing;
     if (c->timed) HIPCHK(c, hipEventRecord(c->ev0, c->stream));
     RCCHK(launch_stripe(c, c->slot[c->ahead_par], c->aux, t, geo, d_in, n, 0, status, next_status, dy, sdy, dcb, dcr,
-                        sdc, true, want_mvd, c->ab_gate ? nullptr : c->ev_gate[c->ahead_par],
-                        c->ab_gate ? c->ev_gate[c->ahead_par ^ 1] : nullptr));
+                        sdc, true, want_mvd, c->ev_gate[c->ahead_par]));
     c->ahead_par ^= 1;
     if (c->timed) HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     c->last_status = status;

@@ -536,98 +536,4 @@ MM_HD void mc_thread_in(int g, const McIn& in, const Geometry& geo, const Taps& 
   mc_rec_impl<UNI_HP>(g, in, geo, taps, mc, refs, dst_y, dsy, dst_cb, dst_cr, dsc);
 }
 
-#if defined(__HIP_DEVICE_COMPILE__)
-// mc_rec_impl (bi / uni picture path, padded references) by a pair of lanes: lane h of the pair
-// (threads 2k + h) predicts luma columns 2h, 2h + 1 of the 4x4 sub-block (mmflt::predict_luma_pair)
-// and the chroma plane h (0: Cb, 1: Cr) of its 2x2 sub-blocks.  Both lanes hold the same record, so
-// every branch is uniform over the pair and the cross-lane exchange always finds its partner.  The
-// texture-address path is charged per wave-instruction and per distinct 128-B line it touches
-// (DESIGN 4.1): one x4 per lane and window row instead of x4 + x2, and one plane per lane, halve the
-// load instructions per sub-block while the lines each one touches stay those of half as many PUs.
-__device__ __forceinline__ void mc_pair_impl(int g, int h, const McIn& in, const Geometry& geo, const Taps& taps,
-                                             const McRec& mc, const RefDev* refs, int16_t* dst_y, int dsy,
-                                             int16_t* dst_cb, int16_t* dst_cr, int dsc) {
-  const mm_int2 meta = in.meta;
-  const bool used[2] = {(meta.y & MM_META_USE0) != 0, (meta.y & MM_META_USE1) != 0};
-  const int ox = meta.x & 0xffff, oy = meta.x >> 16;
-  mm_int4 P[2];
-#pragma unroll
-  for (int l = 0; l < 2; l++) {
-    if (!used[l]) continue;
-    const uint32_t lp = in.lp[l], cp = in.cp[l];
-    P[l].x = 16 * ox + (int16_t)(lp & 0xffffu);
-    P[l].y = 16 * oy + (int16_t)(lp >> 16);
-    P[l].z = 16 * ox + (int16_t)(cp & 0xffffu);
-    P[l].w = 16 * oy + (int16_t)(cp >> 16);
-    if (lp == MM_POS_FAR) {
-      const mm_int2 f = mc.far[l][0][g];
-      P[l].x = f.x;
-      P[l].y = f.y;
-    }
-    if (cp == MM_POS_FAR) {
-      const mm_int2 f = mc.far[l][1][g];
-      P[l].z = f.x;
-      P[l].w = f.y;
-    }
-  }
-  const int slot[2] = {meta.y & 15, (meta.y >> 4) & 15};
-  const bool bi = used[0] && used[1];
-  const int w1b = bcw_w1((meta.y >> 8) & 7);
-  const int wa = bi ? 8 - w1b : 8, wb = bi ? w1b : 0;
-  const int pa = used[0] ? 0 : 1;  // uni L1: the list-1 prediction takes the first weight
-  if (geo.store & 1) {
-    int16_t pl[2][8];
-#pragma unroll
-    for (int l = 0; l < 2; l++) {
-      for (int i = 0; i < 8; i++) pl[l][i] = 0;
-      if (!used[l]) continue;
-      const int32_t fx = P[l].x, fy = P[l].y;
-      const int xPos = fx >> 4, yPos = fy >> 4, xFrac = fx & 15, yFrac = fy & 15;
-      if (sb_out_of_range(xPos, yPos, geo.W, geo.H, geo.maxCUw, geo.maxCUh, 4, 4)) continue;
-      const RefDev r = refs[slot[l]];
-      const char* base = taps.pool.base + r.off_y + (long)((yPos - 3) * r.stride_y + ((xPos - 3) & ~1)) * 2 + 8 * h;
-      mmflt::predict_luma_pair(base, r.stride_y * 2, h, taps.packed->lh[xFrac][(xPos - 3) & 1], taps.packed->lv[yFrac],
-                               geo.bd, pl[l]);
-    }
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      int16_t o[2];
-#pragma unroll
-      for (int c = 0; c < 2; c++) {
-        const int i = r * 2 + c;
-        const int a = pa ? pl[1][i] : pl[0][i];
-        o[c] = weighted_avg(a, pl[1][i], wa, wb, geo.bd);
-      }
-      store_row<2>(dst_y + (long)(oy + r) * dsy + ox + 2 * h, o, geo.vec_store);
-    }
-  }
-  if (!geo.chroma || !(geo.store & 2)) return;
-  int16_t pc[2][4];
-#pragma unroll
-  for (int l = 0; l < 2; l++) {
-    for (int i = 0; i < 4; i++) pc[l][i] = 0;
-    if (!used[l]) continue;
-    const int32_t fx = P[l].z, fy = P[l].w;
-    const int xPos = fx >> 5, yPos = fy >> 5, xFrac = fx & 31, yFrac = fy & 31;
-    if (sb_out_of_range(xPos, yPos, geo.Wc, geo.Hc, geo.maxCUwc, geo.maxCUhc, 2, 2)) continue;
-    const RefDev r = refs[slot[l]];
-    predict_subblock_pool<4, 2, 2>(taps.pool, r.off_cb, h ? taps.pool.cr_delta : 0, r.stride_c, xPos, yPos,
-                                   taps.packed->ch[xFrac][(xPos - 1) & 1], taps.packed->cv[yFrac], true, geo.bd, pc[l]);
-  }
-  int16_t* const dst_c = h ? dst_cr : dst_cb;
-  const int cx = ox >> 1, cy = oy >> 1;
-#pragma unroll
-  for (int r = 0; r < 2; r++) {
-    int16_t o[2];
-#pragma unroll
-    for (int c = 0; c < 2; c++) {
-      const int i = r * 2 + c;
-      const int a = pa ? pc[1][i] : pc[0][i];
-      o[c] = weighted_avg(a, pc[1][i], wa, wb, geo.bd);
-    }
-    store_row<2>(dst_c + (long)(cy + r) * dsc + cx, o, geo.vec_store);
-  }
-}
-#endif
-
 }  // namespace mmpipe
