@@ -436,6 +436,7 @@ constexpr int MC_BLOCKS_PER_WG = 1;
 // pictures on the context stream (profiles/r03_ab_kernel_events.txt).
 constexpr bool KERNEL_EVENTS = true;
 constexpr bool GATE_NO_FENCE = true;
+constexpr bool PLAN_AHEAD_HOST_WAIT = true;  // see launch_stripe
 
 // --------------------------------------------------------------------------------------------
 // Encoder candidate windows (mm_sad_window, mm_me.h)
@@ -1452,6 +1453,12 @@ static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables
     if (back) HIPCHK(c, hipEventRecord(c->ev_plan, st));
   }
   if (back) {  // plan-ahead: reprojection and interpolation on the context stream
+    // The host waits for this picture's planning (bound to k_setup_dev) before it issues the context
+    // stream's wait: the event is then complete, so the runtime issues no cross-queue barrier packet
+    // between the previous picture's k_mc_dev and this k_reproj_dev (C3 0.178-0.180 -> 0.173-0.175 ms
+    // per picture, profiles/r03_ab_hostsync.txt).  The planning waits only for the k_mc_dev of two
+    // calls back, so the host still runs about one picture ahead of the GPU.
+    if (PLAN_AHEAD_HOST_WAIT) HIPCHK(c, hipEventSynchronize(c->ev_plan));
     HIPCHK(c, hipStreamWaitEvent(st_back, c->ev_plan, 0));
     st = st_back;
   }
