@@ -360,8 +360,10 @@ int mm_set_dmvr(mm_ctx* ctx, int on);
  * reprojection and interpolation stay on the context stream after them.  Contract while on: the
  * device PU list of a call is complete by the time the previous call is issued (written by the
  * host, or by work enqueued on the context stream before that call).  Applies to one-stripe calls
- * without stage timing; results do not depend on the setting.  (No reference counterpart: VTM
- * decodes a picture's PUs inside its own CTU loop.) */
+ * without stage timing; results do not depend on the setting.  While on, each call returns only
+ * after its picture's planning has run on the device (it waits for the previous picture's
+ * interpolation but one), so the host stays about one picture ahead of the GPU.  (No reference
+ * counterpart: VTM decodes a picture's PUs inside its own CTU loop.) */
 int mm_set_plan_ahead(mm_ctx* ctx, int on);
 
 #ifdef __cplusplus
