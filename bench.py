@@ -120,10 +120,15 @@ def planes(cfg):
     return dy, dcb, torch.zeros_like(dcb)
 
 
-def timed(steps, warmup, body, dist):
+def timed(steps, warmup, body, dist, before=None):
+    """before(): runs after the warm-up, outside the timed region (e.g. poisons the output buffers
+    so that the self-check reads what the timed steps wrote)."""
     for s in range(warmup):
         body(s)
     torch.cuda.synchronize()
+    if before is not None:
+        before()
+        torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -142,7 +147,7 @@ def timed(steps, warmup, body, dist):
     return elapsed
 
 
-def cpu_baseline_and_check(args, cfg, params, pictures, gpu_out):
+def cpu_baseline_and_check(args, cfg, params, pictures, gpu_out, n_checked=None):
     """The oracle on the host cores of this box: (a) one thread, as VTM's serial decoder, over a
     bounded sample (~cpu_seconds) of the bench pictures; (b) PU-parallel on all available threads
     (std::thread-style pthreads in the oracle) over the same pictures.  References are padded
@@ -157,8 +162,9 @@ def cpu_baseline_and_check(args, cfg, params, pictures, gpu_out):
     # (b) all threads, every picture once -> bit-exact check (MM_PUF_DMVR PUs: the oracle's serial
     # DMVR restatement after the PU-parallel rest)
     mismatches = 0
+    n_checked = len(pictures) if n_checked is None else n_checked
     t_all, area_all = 0.0, 0
-    for (cur, pus, refs), pr, got in zip(pictures, padded, gpu_out):
+    for (cur, pus, refs), pr, got in list(zip(pictures, padded, gpu_out))[:n_checked]:
         t = time.perf_counter()
         want = orc.predict_mixed(cur, pus, refs, cfg.width, cfg.height, prefs=pr, threads=threads)
         t_all += time.perf_counter() - t
@@ -176,7 +182,7 @@ def cpu_baseline_and_check(args, cfg, params, pictures, gpu_out):
     info = host_info(threads)
     cpu = {"value": round(area_one / t_one / 1e6, 3), "unit": "Mpixels/s", "cores": 1, "kind": "port",
            "sample": f"{n_one} full {cfg.width}x{cfg.height} pictures of the bench workload through the oracle "
-                     f"(oracle/mm_oracle.c: array-at-a-time restatement, glibc libm + SSE packets, gcc -O2), "
+                     f"(oracle/mm_oracle.c: array-at-a-time restatement, glibc libm + SSE packets, gcc -O3), "
                      f"one host thread, {t_one:.1f} s; reference padding (extendPicBorder) {pad_s * 1e3:.0f} ms per "
                      f"picture done once outside the timing",
            "all_cores": {"value": round(area_all / t_all / 1e6, 3), "unit": "Mpixels/s", "threads": threads,
@@ -210,8 +216,17 @@ def bench_pictures(args, cfg, params, rank, world, local, dist):
         f = s % P_
         ctx.predict_device(pictures[f][0], d_pus[f], *outs[f])
 
-    elapsed = timed(args.steps, args.warmup, step, dist)
+    def poison():
+        for o in outs:
+            for t in o:
+                t.fill_(-1)
+
+    elapsed = timed(args.steps, args.warmup, step, dist, before=poison)
     ctx.synchronize()  # raises if the device planner rejected a PU
+    # the timed plan-ahead pictures, copied out before anything else writes the buffers: the
+    # bit-exact check below reads these (every sample of a C3 picture is predicted, so a sample the
+    # timed steps left unwritten would read -1 and fail the check)
+    got = [tuple(t.cpu().numpy() for t in o) for o in outs]
     steps_area = sum(area[s % P_] for s in range(args.steps))
     total_area = float(steps_area)
     if dist:
@@ -229,13 +244,13 @@ def bench_pictures(args, cfg, params, rank, world, local, dist):
     kernel_ms = float(st[3])
     alg_step = float(np.mean([alg[s % P_] for s in range(args.kernel_steps)]))
     achieved = alg_step / (kernel_ms * 1e-3) / 1e9
-    got = [tuple(t.cpu().numpy() for t in o) for o in outs]
     mvp = (mvp_per_picture(ctx, cfg, int(np.mean([len(p) for _, p, _ in pictures])))
            if args.config == "C3" and not args.no_mvp else None)
 
     cpu, bit_exact, mism = None, None, None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu, bit_exact, mism = cpu_baseline_and_check(args, cfg, params, pictures, got)
+        # pictures the timed steps predicted (all of them unless --steps < --pictures)
+        cpu, bit_exact, mism = cpu_baseline_and_check(args, cfg, params, pictures, got, min(P_, args.steps))
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(total_area / elapsed / 1e6, 2), "unit": "Mpixels/s", "n_gpus": world,

@@ -1059,10 +1059,24 @@ static void sub_pel_error_srfc(const uint64_t* sadBuffer, int32_t* deltaMv) { /*
 
 static int clip_mv18(int v) { return v < -(1 << 17) ? -(1 << 17) : (v > (1 << 17) - 1 ? (1 << 17) - 1 : v); }
 
-int orc_pred_dmvr(void* h, int cur_poc, const mm_pu_desc* pus, int n, int n_refs, const int32_t* pocs,
-                  const int16_t* const* ys, const int16_t* const* cbs, const int16_t* const* crs, ptrdiff_t stride_y,
-                  ptrdiff_t stride_c, int16_t* dy, ptrdiff_t sdy, int16_t* dcb, int16_t* dcr, ptrdiff_t sdc,
-                  int32_t* mvd_out) {
+/* Branch trace of one sub-PU's decision (orc_pred_dmvr_trace; tests assert that every branch of
+ * :2516-2531 and :1996-2048 is reached): bit 0 early exit (minCost < dx*dy, notZeroCost = false);
+ * bits 1-5 the best offset index; bit 6 best on the window border (no error surface); bits 8-9 / 10-11
+ * the horizontal / vertical error-surface case: 0 denominator 0 (no change), 1 div_for_maxq7,
+ * 2 SAD tie on the -1 side (-8, half pel), 3 tie on the +1 side (+8).  The `!minCost` exit (:2528-2531)
+ * is unreachable in the reference's single iteration: it follows the minCost >= dx*dy > 0 test. */
+#define DMVR_TR_EARLY 1
+#define DMVR_TR_BORDER 64
+static int surface_case(const uint64_t* s, int a, int b) {
+  const int64_t den = (int64_t)(s[a] + s[b] - (s[0] << 1));
+  if (den == 0) return 0;
+  if (s[a] != s[0] && s[b] != s[0]) return 1;
+  return s[a] == s[0] ? 2 : 3;
+}
+static int pred_dmvr_impl(void* h, int cur_poc, const mm_pu_desc* pus, int n, int n_refs, const int32_t* pocs,
+                          const int16_t* const* ys, const int16_t* const* cbs, const int16_t* const* crs,
+                          ptrdiff_t stride_y, ptrdiff_t stride_c, int16_t* dy, ptrdiff_t sdy, int16_t* dcb,
+                          int16_t* dcr, ptrdiff_t sdc, int32_t* mvd_out, int32_t* trace) {
   Orc* o = (Orc*)h;
   OPic* pics = pad_refs(o, n_refs, pocs, ys, cbs, crs, stride_y, stride_c);
   int rc = 0, k = 0;
@@ -1091,7 +1105,7 @@ int orc_pred_dmvr(void* h, int cur_poc, const mm_pu_desc* pus, int n, int n_refs
         uint64_t minCost = dmvr_cost(s0, s1, dxs, dys);
         minCost -= (minCost >> 2);
         if (minCost < (uint64_t)(dxs * dys)) notZeroCost = 0;
-        int best = 12;
+        int best = 12, tr = notZeroCost ? 0 : DMVR_TR_EARLY;
         if (notZeroCost) {
           sads[12] = minCost;
           for (int j = 0; j < 25 && !rc; j++) {
@@ -1103,15 +1117,20 @@ int orc_pred_dmvr(void* h, int cur_poc, const mm_pu_desc* pus, int n, int n_refs
           }
           tdx = (best % 5 - 2) << 4;
           tdy = (best / 5 - 2) << 4;
+          tr |= best << 1;
           if (abs(tdx) != 32 && abs(tdy) != 32) {
             uint64_t sb[5] = {sads[best], sads[best - 1], sads[best - 5], sads[best + 1], sads[best + 5]};
             int32_t d[2] = {0, 0};
             sub_pel_error_srfc(sb, d);
             tdx += d[0];
             tdy += d[1];
+            tr |= surface_case(sb, 1, 3) << 8 | surface_case(sb, 2, 4) << 10;
+          } else {
+            tr |= DMVR_TR_BORDER;
           }
         }
         if (mvd_out) { mvd_out[2 * k] = tdx; mvd_out[2 * k + 1] = tdy; }
+        if (trace) trace[k] = tr;
         k++;
         mm_pu_desc sp = *u;
         sp.x = x; sp.y = y; sp.w = dxs; sp.h = dys;
@@ -1126,6 +1145,21 @@ int orc_pred_dmvr(void* h, int cur_poc, const mm_pu_desc* pus, int n, int n_refs
     for (int c = 0; c < 3; c++) free(pred[l][c]);
   free_refs(pics, n_refs);
   return rc;
+}
+
+int orc_pred_dmvr(void* h, int cur_poc, const mm_pu_desc* pus, int n, int n_refs, const int32_t* pocs,
+                  const int16_t* const* ys, const int16_t* const* cbs, const int16_t* const* crs, ptrdiff_t stride_y,
+                  ptrdiff_t stride_c, int16_t* dy, ptrdiff_t sdy, int16_t* dcb, int16_t* dcr, ptrdiff_t sdc,
+                  int32_t* mvd_out) {
+  return pred_dmvr_impl(h, cur_poc, pus, n, n_refs, pocs, ys, cbs, crs, stride_y, stride_c, dy, sdy, dcb, dcr, sdc,
+                        mvd_out, NULL);
+}
+int orc_pred_dmvr_trace(void* h, int cur_poc, const mm_pu_desc* pus, int n, int n_refs, const int32_t* pocs,
+                        const int16_t* const* ys, const int16_t* const* cbs, const int16_t* const* crs,
+                        ptrdiff_t stride_y, ptrdiff_t stride_c, int16_t* dy, ptrdiff_t sdy, int16_t* dcb, int16_t* dcr,
+                        ptrdiff_t sdc, int32_t* mvd_out, int32_t* trace) {
+  return pred_dmvr_impl(h, cur_poc, pus, n, n_refs, pocs, ys, cbs, crs, stride_y, stride_c, dy, sdy, dcb, dcr, sdc,
+                        mvd_out, trace);
 }
 
 /* mm_filter twin: raw filterHor / filterVer on a host block with margin */

@@ -58,6 +58,7 @@ def load(variant=None):
     lib.orc_pred_dmvr.argtypes = [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                   ctypes.c_ssize_t, ctypes.c_ssize_t, c_void_p, ctypes.c_ssize_t, c_void_p, c_void_p,
                                   ctypes.c_ssize_t, c_void_p]
+    lib.orc_pred_dmvr_trace.argtypes = lib.orc_pred_dmvr.argtypes + [c_void_p]
     lib.orc_mvp.argtypes = [c_void_p, c_void_p, c_int, c_void_p]
     lib.orc_sad_window.argtypes = [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                    ctypes.c_ssize_t, c_void_p, ctypes.c_ssize_t, c_void_p]
@@ -169,9 +170,10 @@ class Oracle:
             raise RuntimeError(f"oracle predict_list failed: {rc}")
         return dy, dcb, dcr
 
-    def predict_dmvr(self, cur_poc, pus, refs, W, H, out=None):
+    def predict_dmvr(self, cur_poc, pus, refs, W, H, out=None, trace=False):
         """MM-DMVR PUs (xProcessDMVRProjected): predicted planes and the per-sub-PU L0 deltas.
-        out: (Y, Cb, Cr) planes to predict into (only the PUs' samples are written)."""
+        out: (Y, Cb, Cr) planes to predict into (only the PUs' samples are written).
+        trace: also return the per-sub-PU branch words (mm_oracle.c DMVR_TR_*, dmvr_branches)."""
         pus = np.ascontiguousarray(pus)
         pocs = sorted(refs)
         ys = [np.ascontiguousarray(refs[p][0]) for p in pocs]
@@ -186,13 +188,16 @@ class Oracle:
         nsub = int(sum(((int(u["w"]) + 15) // 16) * ((int(u["h"]) + 15) // 16) for u in pus))
         mvd = np.zeros((max(nsub, 1), 2), dtype=np.int32)
         pa = np.array(pocs, dtype=np.int32)
-        rc = self.lib.orc_pred_dmvr(self.h, cur_poc, c_void_p(pus.ctypes.data), len(pus), len(pocs),
-                                    c_void_p(pa.ctypes.data), _ptr_array(ys), _ptr_array(cbs), _ptr_array(crs),
-                                    ys[0].shape[1], cbs[0].shape[1], c_void_p(dy.ctypes.data), W,
-                                    c_void_p(dcb.ctypes.data), c_void_p(dcr.ctypes.data), W // 2,
-                                    c_void_p(mvd.ctypes.data))
+        tr = np.zeros(max(nsub, 1), dtype=np.int32)
+        rc = self.lib.orc_pred_dmvr_trace(self.h, cur_poc, c_void_p(pus.ctypes.data), len(pus), len(pocs),
+                                          c_void_p(pa.ctypes.data), _ptr_array(ys), _ptr_array(cbs), _ptr_array(crs),
+                                          ys[0].shape[1], cbs[0].shape[1], c_void_p(dy.ctypes.data), W,
+                                          c_void_p(dcb.ctypes.data), c_void_p(dcr.ctypes.data), W // 2,
+                                          c_void_p(mvd.ctypes.data), c_void_p(tr.ctypes.data))
         if rc:
             raise RuntimeError(f"oracle predict_dmvr failed: {rc}")
+        if trace:
+            return (dy, dcb, dcr), mvd[:nsub], tr[:nsub]
         return (dy, dcb, dcr), mvd[:nsub]
 
     def predict_mixed(self, cur_poc, pus, refs, W, H, prefs=None, threads=1):
@@ -245,6 +250,22 @@ class Oracle:
         if rc:
             raise RuntimeError(f"oracle filter failed: {rc}")
         return dst
+
+
+def dmvr_branches(trace):
+    """Counts of the MM-DMVR decision branches in an orc_pred_dmvr_trace word array
+    (InterPrediction.cpp:2516-2531 early exit, :2567-2580 border best, xSubPelErrorSrfc :1996-2048)."""
+    t = np.asarray(trace, dtype=np.int64)
+    searched = (t & 1) == 0
+    surf = searched & ((t & 64) == 0)
+    out = {"sub_pus": int(len(t)), "early_exit": int((~searched).sum()), "searched": int(searched.sum()),
+           "border_best": int((searched & ((t & 64) != 0)).sum()),
+           "centre_best": int((searched & (((t >> 1) & 31) == 12)).sum())}
+    for axis, sh in (("h", 8), ("v", 10)):
+        case = (t >> sh) & 3
+        for k, name in enumerate(("den0", "div", "tie_minus", "tie_plus")):
+            out[f"{axis}_{name}"] = int((surf & (case == k)).sum())
+    return out
 
 
 def effective_blocks(tools, pus, sub_motion, pu_dtype, cap=1 << 16):

@@ -66,3 +66,59 @@ def test_twin_mixed_picture_matches_oracle(w, h, models, share):
     # without the picture's DMVR enable the flagged PUs are rejected
     with pytest.raises(RuntimeError, match="1"):
         twin.predict(params, W.CUR_POC, pus, refs, w, h, EPI)
+
+
+# ---- every branch of the decision (tests/golden/dmvr_branches.npz, tools/gen_dmvr_branch_fixture.py) ----
+def branch_fixture():
+    """(params, width, height, [(family, refs, pus, mvd, trace)]) of the DMVR branch fixture."""
+    import os
+    from helpers import GOLDEN
+    z = np.load(os.path.join(GOLDEN, "dmvr_branches.npz"))
+    w, h = int(z["width"]), int(z["height"])
+    models = [int(m) for m in z["models"]]
+    params = mm360.seq_params(w, h, models)
+    fams = []
+    for fam in [str(f) for f in z["families"]]:
+        refs = {poc: W.dmvr_branch_planes(fam, w, h, poc) for poc in W.REF_POCS}
+        fams.append((fam, refs, z[f"{fam}_pus"], z[f"{fam}_mvd"], z[f"{fam}_trace"]))
+    return params, w, h, fams
+
+
+def test_dmvr_branch_fixture_reaches_every_branch():
+    """The fixture pins the oracle's decision (deltas and branch words) and covers every branch of
+    InterPrediction.cpp:2516-2531 (early exit), the border rule of xDMVRSubPixelErrorSurface
+    (:2162-2163) and xSubPelErrorSrfc (:1996-2048: division, half-pel tie on each side of each axis,
+    zero denominator).  The `!minCost` exit (:2528-2531) cannot be reached after the dx*dy test."""
+    from oracle.oracle import dmvr_branches
+    params, w, h, fams = branch_fixture()
+    orc = Oracle(params, EPI)
+    tot = {}
+    for fam, refs, pus, mvd, tr in fams:
+        _, got_mvd, got_tr = orc.predict_dmvr(W.CUR_POC, pus, refs, w, h, trace=True)
+        assert np.array_equal(got_mvd, mvd), (fam, np.argwhere(got_mvd != mvd)[:5])
+        assert np.array_equal(got_tr, tr), fam
+        for k, v in dmvr_branches(tr).items():
+            tot[k] = tot.get(k, 0) + v
+    for k in ("early_exit", "border_best", "centre_best", "h_div", "v_div", "h_tie_minus", "h_tie_plus",
+              "v_tie_minus", "v_tie_plus", "v_den0"):
+        assert tot[k] > 0, (k, tot)
+
+
+def test_twin_dmvr_branch_fixture_matches_oracle():
+    """The product's DMVR bodies (CPU twin: planner, search kernels' bodies, decision) on every
+    branch: the deltas and the refined predictions == the oracle, per family; and the same PUs
+    mixed into a picture with unflagged PUs (mm_pred_device path)."""
+    params, w, h, fams = branch_fixture()
+    orc = Oracle(params, EPI)
+    for fam, refs, pus, mvd, _ in fams:
+        got, got_mvd = twin.predict_dmvr(params, W.CUR_POC, pus, refs, w, h, EPI)
+        assert np.array_equal(got_mvd, mvd), (fam, np.argwhere(got_mvd != mvd)[:5])
+        want, _ = orc.predict_dmvr(W.CUR_POC, pus, refs, w, h)
+        for name, a, b in zip(("y", "cb", "cr"), got, want):
+            assert np.array_equal(a, b), describe_mismatch(f"{fam} {name}", a, b)
+        mixed = pus.copy()
+        mixed["flags"][::2] |= mm360.PUF_DMVR
+        want = orc.predict_mixed(W.CUR_POC, mixed, refs, w, h)
+        got = twin.predict(params, W.CUR_POC, mixed, refs, w, h, EPI, dmvr=True)
+        for name, a, b in zip(("y", "cb", "cr"), got, want):
+            assert np.array_equal(a, b), describe_mismatch(f"{fam} mixed {name}", a, b)

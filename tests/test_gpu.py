@@ -666,6 +666,48 @@ def test_pred_dmvr_vs_oracle(w, h):
         assert np.array_equal(got, x), plane_mismatch(name, got, x)
 
 
+def test_pred_dmvr_every_branch_vs_oracle():
+    """MM-DMVR on the GPU over the branch fixture (tests/golden/dmvr_branches.npz): early exits,
+    border bests, division and half-pel tie cases on both axes and sides, a zero denominator
+    (InterPrediction.cpp:2516-2531, :2162-2163, :1996-2048).  mm_pred_dmvr's deltas == the
+    fixture's (the oracle's), its planes == the oracle's; then the same PUs with every other one
+    flagged MM_PUF_DMVR in ONE mm_pred_device picture (plan-ahead on) == predict_mixed."""
+    from oracle.oracle import dmvr_branches
+    from test_dmvr import branch_fixture
+    params, w, h, fams = branch_fixture()
+    cfg = W.Config("T", w, h, tuple(int(m) for m in W.ALL_MODELS), 1, "test")
+    orc = Oracle(params, EPI)
+    tot = {}
+    for fam, refs, pus, mvd, tr in fams:
+        for k, v in dmvr_branches(tr).items():
+            tot[k] = tot.get(k, 0) + v
+        want, _ = orc.predict_dmvr(W.CUR_POC, pus, refs, w, h)
+        mixed = pus.copy()
+        mixed["flags"][::2] |= mm360.PUF_DMVR
+        want_mixed = orc.predict_mixed(W.CUR_POC, mixed, refs, w, h)
+        with _ctx(params) as ctx:
+            for poc, (y, cb, cr) in refs.items():
+                ctx.upload_ref(poc, y, cb, cr)
+            dst = _planes(cfg)
+            got_mvd = ctx.predict_dmvr(W.CUR_POC, pus, *dst)
+            assert np.array_equal(got_mvd, mvd), (fam, np.argwhere(got_mvd != mvd)[:5])
+            for name, t, x in zip(("y", "cb", "cr"), dst, want):
+                got = t.cpu().numpy()
+                assert np.array_equal(got, x), plane_mismatch(f"{fam} {name}", got, x)
+            ctx.set_dmvr(True)
+            ctx.set_plan_ahead(True)
+            d_list = mm360.pus_to_device(mixed)
+            out = _planes(cfg)  # 16x8 / 8x16 PUs leave part of their cell unpredicted (zero in both)
+            torch.cuda.synchronize()
+            ctx.predict_device(W.CUR_POC, d_list, *out)
+            ctx.synchronize()
+            for name, t, x in zip(("y", "cb", "cr"), out, want_mixed):
+                got = t.cpu().numpy()
+                assert np.array_equal(got, x), plane_mismatch(f"{fam} mixed {name}", got, x)
+    for k in ("early_exit", "border_best", "h_tie_minus", "h_tie_plus", "v_tie_minus", "v_tie_plus", "v_den0"):
+        assert tot[k] > 0, (k, tot)
+
+
 def test_mvp_convert_vs_oracle():
     """Batched MM-MVP on the GPU == the oracle for every model pair (incl. CLASSIC), both epipoles."""
     from test_mvp import ALL as MVP_ALL, EPI2
@@ -715,6 +757,34 @@ def test_mvp_device_errors_and_epipole_refresh():
         with pytest.raises(mm360.MMError) as e:
             ctx.synchronize()
         assert e.value.code == mm360.MM_ERR_ARG and "MVP query 123" in str(e.value)
+
+
+def test_mvp_device_error_in_later_waves_is_reported():
+    """A failing query only in waves 1-3 of its 256-query workgroup (lanes 64-255) still reaches the
+    status word: k_mvp_dev zeroes its workgroup's status before any wave records a failure.  Many
+    workgroups, each with its one bad query at a different lane >= 64; repeated launches."""
+    from test_mvp import ALL as MVP_ALL, EPI2
+    params = mm360.seq_params(256, 128, MVP_ALL)
+    q = W.mvp_queries(256, 128, MVP_ALL, 256 * 64, seed=9)
+    rng = np.random.default_rng(3)
+    lanes = rng.integers(64, 256, size=64)
+    bad = q.copy()
+    for b, lane in enumerate(lanes):
+        bad["shift_hor"][256 * b + int(lane)] = 9  # invalid shift: MM_ERR_ARG for that query only
+    first = int(256 * 0 + lanes[0])
+    with _ctx(params, EPI2) as ctx:
+        d_q = mm360.queries_to_device(bad)
+        d_out = torch.zeros((len(q), 2), dtype=torch.int32, device="cuda")
+        for _ in range(20):
+            ctx.mvp_convert_device(d_q, d_out)
+            with pytest.raises(mm360.MMError) as e:
+                ctx.mvp_status()
+            assert e.value.code == mm360.MM_ERR_ARG and f"MVP query {first}:" in str(e.value), str(e.value)
+        # the valid queries are still converted
+        ok = np.ones(len(q), dtype=bool)
+        ok[[256 * b + int(l) for b, l in enumerate(lanes)]] = False
+        want = Oracle(params, EPI2).mvp(q[ok])
+        assert np.array_equal(d_out.cpu().numpy()[ok], want)
 
 
 @pytest.mark.parametrize("plan_ahead", [False, True])

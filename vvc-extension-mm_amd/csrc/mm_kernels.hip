@@ -616,6 +616,7 @@ __global__ void __launch_bounds__(MVP_BLOCK) k_mvp_dev(SeqConst sc, const mm_mvp
   const int tid = threadIdx.x, i0 = blockIdx.x * MVP_BLOCK, i = i0 + tid;
   if (tid == 0) s_status = 0;
   if (blockIdx.x == 0 && tid == 0) *next_status = 0ull;
+  __syncthreads();  // s_status is zeroed before any wave's atomicMax (waves 1-3 may run ahead of wave 0)
   int key = -1;
   if (i < n) {
     const mm_mvp_query x = q[i];

@@ -306,3 +306,65 @@ def mvp_queries(width: int, height: int, models: Sequence[int], n: int, seed: in
         q[i] = (x, y, mv[0], mv[1], mo, md, shift, shift, CUR_POC, REF_POCS[i % 2], CUR_POC, REF_POCS[(i // 2) % 2],
                 cx, cy, cw, ch, x, y, w, h)
     return q
+
+
+# MM-DMVR decision branches (InterPrediction.cpp:2516-2531 early exit, :2576-2580 border best,
+# xSubPelErrorSrfc :1996-2048 division / half-pel tie / zero denominator).  The ERP-like planes
+# above carry independent noise per POC, so the centre cost never falls below dx * dy and the
+# 25 costs almost never tie.  These content families make every branch reachable: identical
+# reference pictures (early exits when both lists' positions coincide), and piecewise-flat
+# content (costs on a coarse lattice: ties and zero denominators).
+DMVR_FAMILIES = ("steps", "sparse", "flatdots", "erp_same")
+
+
+def dmvr_branch_planes(family: str, width: int, height: int, poc: int, bit_depth: int = 10):
+    """Reference planes (Y, Cb, Cr) of one DMVR branch family.  Every family gives POCs 0 and 16
+    the same content, except `sparse`, whose POC-16 dots are drawn independently."""
+    def plane(w, h, salt):
+        rng = np.random.default_rng(0x4D4D6000 + salt + (17 * poc if family == "sparse" else 0))
+        y, x = np.mgrid[0:h, 0:w].astype(np.float64)
+        if family == "steps":
+            v = 400 + 8 * np.floor(x / 5) + 4 * np.floor(y / 7)
+        elif family == "sparse":
+            v = 500 + 64 * (rng.random((h, w)) < 0.02)
+        elif family == "flatdots":
+            v = np.full((h, w), 500.0)
+            v[::9, ::11] += 40
+        elif family == "erp_same":
+            v = ref_planes(width, height, 0, bit_depth)[0 if salt == 0 else salt].astype(np.float64)
+        else:
+            raise ValueError(family)
+        return np.clip(np.rint(v), 0, (1 << bit_depth) - 1).astype(np.int16)
+
+    return plane(width, height, 0), plane(width // 2, height // 2, 1), plane(width // 2, height // 2, 2)
+
+
+def dmvr_branch_candidates(family: str, width: int, height: int, models: Sequence[int], seed: int) -> np.ndarray:
+    """One DMVR candidate PU per 16x16 cell of the picture (16x16, 16x8 or 8x16 at the cell origin,
+    bi from POCs 0 / 16, one model for both lists), with the motion pattern that reaches the
+    family's branches: equal MVs on identical content (early exits), mirrored integer MVs, or
+    small independent MVs (costs near the threshold)."""
+    rng = np.random.default_rng(0x4D4D7000 + 131 * seed + DMVR_FAMILIES.index(family))
+    cells = [(x, y) for y in range(0, height, 16) for x in range(0, width, 16)]
+    out = new_pus(len(cells))
+    for i, (x, y) in enumerate(cells):
+        r = rng.random()
+        w, h = (16, 16) if r < 0.7 else ((16, 8) if r < 0.85 else (8, 16))
+        m = int(models[rng.integers(0, len(models))])
+        kind = rng.random()
+        if family == "erp_same" and kind < 0.6:
+            mv0 = [int(rng.integers(-64, 65)), int(rng.integers(-64, 65))]
+            mv1 = list(mv0)
+            if kind < 0.2:  # one list a quarter sample off: costs just around dx * dy
+                mv1[int(rng.integers(0, 2))] += int(rng.choice([-4, 4]))
+        elif family in ("sparse", "flatdots") or kind < 0.5:
+            mv0 = [int(rng.integers(-3, 4)) * 16, int(rng.integers(-3, 4)) * 16]
+            mv1 = [-mv0[0], -mv0[1]]
+        else:
+            mv0 = [int(rng.integers(-20, 21)), int(rng.integers(-20, 21))]
+            mv1 = [int(rng.integers(-20, 21)), int(rng.integers(-20, 21))]
+        out[i]["x"], out[i]["y"], out[i]["w"], out[i]["h"] = x, y, w, h
+        out[i]["mv"] = np.array([mv0, mv1], dtype=np.int32)
+        out[i]["ref_poc"] = REF_POCS
+        out[i]["model"] = (m, m)
+    return out
