@@ -145,23 +145,11 @@ static int twin_pred_list(const Twin& t, const mmdev::PicTables& tab, const mm_p
     std::vector<BlockSetup> dset((size_t)m.n_sub * N_OFF * 2);
 #pragma omp parallel for schedule(static)
     for (int j = 0; j < m.n_sub * N_OFF * 2; j++) dmvr_setup_thread(j, t.sc, subs.data(), tab.ged, dset.data());
-    std::vector<uint32_t> costs((size_t)m.n_sub * N_OFF, 0);
-    std::vector<mm_int2> dpos(2 * (size_t)m.n_dmvr_elems + 2);
-#pragma omp parallel for schedule(static, 256)
-    for (long g = 0; g < m.n_dmvr_elems; g++)
-      dmvr_reproj_thread((int)g, find_item(sub_off.data(), sub_chunk.data(), (int)g, m.n_sub), t.sc, subs.data(),
-                         dset.data(), c, dpos.data());
-#pragma omp parallel for schedule(static, 256)
-    for (long g = 0; g < m.n_dmvr_elems; g++) {
-      int idx;
-      const int si = find_item(sub_off.data(), sub_chunk.data(), (int)g, m.n_sub);
-      uint32_t v = dmvr_sad_thread((int)g, si, t.geo, taps, subs.data(), dpos.data(), tab.ref, &idx);
-#pragma omp atomic
-      costs[idx] += v;
-    }
     if (mvd) mvd->assign(2 * (size_t)m.n_sub, 0);
+#pragma omp parallel for schedule(dynamic, 4)
     for (int s = 0; s < m.n_sub; s++)
-      dmvr_decide_jobs_thread(s, subs.data(), costs.data(), jobs.data(), mvd ? mvd->data() : nullptr);
+      dmvr_search_host(s, t.sc, t.geo, taps, subs.data(), dset.data(), c, tab.ref, jobs.data(),
+                       mvd ? mvd->data() : nullptr);
   }
   std::vector<BlockSetup> setups(m.n_jobs);
 #pragma omp parallel for schedule(static)

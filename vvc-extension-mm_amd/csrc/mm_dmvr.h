@@ -11,8 +11,9 @@
 //   3. parabolic sub-pel refinement from the 5 costs around the best offset unless it lies on the
 //      window border (xDMVRSubPixelErrorSurface :2157-2175, xSubPelErrorSrfc :1996-2048);
 //   4. the sub-PU is predicted as a bi PU at merge0 + mvd / merge1 - mvd (all components, addAvg).
-// Steps 1-3 run here (k_dmvr_setup_dev, k_dmvr_reproj_dev + k_dmvr_sad_dev, k_dmvr_decide_dev) inside the picture's device-planned
-// launch sequence: the planner (mm_devplan.h) places every sub-PU of an MM_PUF_DMVR PU as a bi PU
+// Steps 1-3 run here (k_dmvr_setup_dev, then k_dmvr_search_dev: one workgroup per sub-PU, the
+// centre cost first, the other 24 offsets only when the centre does not end the search) inside
+// the picture's device-planned launch sequence: the planner (mm_devplan.h) places every sub-PU of an MM_PUF_DMVR PU as a bi PU
 // with its reprojection jobs and a SubPuDev record pointing at them, the search runs on the
 // records, and k_dmvr_decide writes the refined MVs into those jobs before k_setup reads them --
 // step 4 is then the ordinary setup / reprojection / interpolation of the picture.
@@ -50,16 +51,14 @@ MM_HD void dmvr_setup_thread(int t, const SeqConst& sc, const SubPuDev* sp, cons
   block_setup(&out[t], sc, u.model, true, u.x, u.y, u.w, u.h, mvh, mvv, u.ged_idx[l] >= 0 ? &ged[u.ged_idx[l]] : nullptr);
 }
 
-// element = (sub-PU, offset, luma 4x4 sub-block) -> the reprojected luma positions of both lists
-// (1/16 pel): L0 at merge0 + offset, L1 at merge1 - offset (setups[(s * N_OFF + o) * 2 + l]).
-// The search runs as two kernels like the picture path -- this VALU-heavy reprojection (k_reproj's
-// footprint), then the window-load-heavy prediction + SAD (k_mc's) -- since one kernel doing both
-// needed 163-179 VGPRs (2 waves per SIMD) and ran at half the rate (profiles/r03_ab_dmvr_split.txt).
-MM_HD void dmvr_reproj_thread(int g, int si, const SeqConst& sc, const SubPuDev* sp, const BlockSetup* setups,
-                              const MpaCache& cache, mm_int2* pos) {
-  const SubPuDev& u = sp[si];
-  const int local = g - u.elem_off;
-  const int o = local / u.n, e = local - o * u.n;
+MM_HD int dmvr_setup_index(int s, int o, int l) { return (s * N_OFF + o) * 2 + l; }
+
+// Luma 4x4 sub-block e (Eigen column-major index over the sub-PU) at offset o: the reprojected
+// positions of both lists (1/16 pel) -- L0 at merge0 + offset, L1 at merge1 - offset, from the
+// (sub-PU, offset, list) setups b0 / b1 (reprojectMotionVectorSubblocks of the sub-PU at that MV,
+// InterPrediction.cpp:2510-2515, 2544-2549).
+MM_HD void dmvr_positions(const SeqConst& sc, const SubPuDev& u, const BlockSetup& b0, const BlockSetup& b1,
+                          const MpaCache& cache, int e, int32_t* fx, int32_t* fy) {
   const int col = e / u.rows, row = e - col * u.rows;
   const float gx = (float)(u.x + 4 * col) + sc.off, gy = (float)(u.y + 4 * row) + sc.off;
   const bool mpa = u.model >= MPA_FRONT_BACK && u.model <= MPA_TOP_BOTTOM;
@@ -70,58 +69,18 @@ MM_HD void dmvr_reproj_thread(int g, int si, const SeqConst& sc, const SubPuDev*
   }
   const bool packet = packet_lane(e, u.n);
   const GridSphere pg = grid_point(cache, u.model, (u.x >> 2) + col, (u.y >> 2) + row, packet);
-#pragma unroll
-  for (int l = 0; l < 2; l++) {
-    int32_t fx, fy;
-    reproject_element(sc, setups[(si * N_OFF + o) * 2 + l], gx, gy, packet, mpa, px, py, vip, 0, &fx, &fy, pg);
-    mm_int2 q;
-    q.x = fx;
-    q.y = fy;
-    pos[2 * (long)g + l] = q;
-  }
+  reproject_element(sc, b0, gx, gy, packet, mpa, px, py, vip, 0, &fx[0], &fy[0], pg);
+  reproject_element(sc, b1, gx, gy, packet, mpa, px, py, vip, 0, &fx[1], &fy[1], pg);
 }
 
-// element g's two 14-bit luma predictions from its positions and its share of xDMVRCost (SAD over
-// the even rows of the sub-PU, which are the even rows of each 4x4 sub-block).
-// *cost_index = s * N_OFF + o.
-MM_HD uint32_t dmvr_sad_thread(int g, int si, const Geometry& geo, const Taps& taps, const SubPuDev* sp,
-                               const mm_int2* pos, const RefDev* refs, int* cost_index) {
-  const SubPuDev& u = sp[si];
-  const int local = g - u.elem_off;
-  const int o = local / u.n;
-  *cost_index = si * N_OFF + o;
-  int16_t p[2][16];
-#pragma unroll
-  for (int l = 0; l < 2; l++) {
-    const mm_int2 q = pos[2 * (long)g + l];
-    const int32_t fx = q.x, fy = q.y;
-    const int xPos = fx >> 4, yPos = fy >> 4, xFrac = fx & 15, yFrac = fy & 15;
-    const RefDev r = refs[u.slot[l]];
-    if (sb_out_of_range(xPos, yPos, geo.W, geo.H, geo.maxCUw, geo.maxCUh, 4, 4)) {
-      for (int i = 0; i < 16; i++) p[l][i] = 0;
-#if defined(__HIP_DEVICE_COMPILE__)
-    } else if (geo.padded || window_interior<8, 4, 4>(xPos, yPos, geo.W, geo.H)) {
-      // padded pool planes: every in-range window is readable without clamping (as in k_mc)
-      predict_subblock_pool<8, 4, 4>(taps.pool, r.off_y, 0, r.stride_y, xPos, yPos, taps.packed->lh[xFrac][(xPos - 3) & 1],
-                                     taps.packed->lv[yFrac], true, geo.bd, p[l]);
-#else
-    } else if (window_interior<8, 4, 4>(xPos, yPos, geo.W, geo.H)) {
-      predict_subblock_interior<8, 4, 4>(r.y, r.stride_y, xPos, yPos, taps.luma[xFrac], taps.luma[yFrac], true, geo.bd,
-                                         p[l]);
-#endif
-    } else {
-      predict_subblock<8, 4, 4>(r.y, r.stride_y, geo.W, geo.H, xPos, yPos, taps.luma[xFrac], taps.luma[yFrac], true,
-                                geo.bd, p[l]);
-    }
-  }
+// xDMVRCost's share of one 4x4 sub-block: SAD of its rows 0 and 2 (the sub-PU's even rows, RdCost
+// subShift 1) between the two 14-bit predictions p0 / p1, given as those two rows (8 samples each).
+MM_HD uint32_t dmvr_sad_rows02(const int16_t* p0, const int16_t* p1) {
   uint32_t sum = 0;
-#pragma unroll
-  for (int rr = 0; rr < 4; rr += 2)
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int d = (int)p[0][rr * 4 + k] - (int)p[1][rr * 4 + k];
-      sum += (uint32_t)(d < 0 ? -d : d);
-    }
+  for (int k = 0; k < 8; k++) {
+    const int d = (int)p0[k] - (int)p1[k];
+    sum += (uint32_t)(d < 0 ? -d : d);
+  }
   return sum;
 }
 
@@ -168,24 +127,25 @@ MM_HD int clip_mv_storage(int v) {  // Mv::clipToStorageBitDepth, MV_BITS = 18
   return v < lo ? lo : (v > hi ? hi : v);
 }
 
-// The refinement decision of one sub-PU from its 25 costs: the total L0 delta (1/16 luma)
+// The refinement decision of one sub-PU from its 25 costs: the total L0 delta (1/16 luma).  The costs
+// are read in place (c may be LDS); the centre entry stands for the adjusted minCost, as
+// pSADsArray[0] does in the reference (:2526).
 MM_HD void dmvr_decide(const SubPuDev& u, const uint32_t* c, int* tdx_out, int* tdy_out) {
-  unsigned long long sad[N_OFF];
-  for (int i = 0; i < N_OFF; i++) sad[i] = c[i];
   int tdx = 0, tdy = 0;  // total delta, 1/16
-  unsigned long long minCost = sad[12] - (sad[12] >> 2);
-  if (minCost >= (unsigned long long)(u.w * u.h)) {  // else: notZeroCost = false, no refinement
-    sad[12] = minCost;
+  const unsigned long long centre = (unsigned long long)c[12] - (c[12] >> 2);
+  if (centre >= (unsigned long long)(u.w * u.h)) {  // else: notZeroCost = false, no refinement
+    auto sad = [&](int i) -> unsigned long long { return i == 12 ? centre : (unsigned long long)c[i]; };
+    unsigned long long minCost = centre;
     int best = 12;
     for (int i = 0; i < N_OFF; i++)
-      if (sad[i] < minCost) {
-        minCost = sad[i];
+      if (sad(i) < minCost) {
+        minCost = sad(i);
         best = i;
       }
     tdx = off_x(best) << 4;
     tdy = off_y(best) << 4;
     if (tdx != 32 && tdx != -32 && tdy != 32 && tdy != -32) {
-      const unsigned long long sb[5] = {sad[best], sad[best - 1], sad[best - 5], sad[best + 1], sad[best + 5]};
+      const unsigned long long sb[5] = {sad(best), sad(best - 1), sad(best - 5), sad(best + 1), sad(best + 5)};
       int d[2] = {0, 0};
       sub_pel_error_surface(sb, d);
       tdx += d[0];
@@ -196,13 +156,10 @@ MM_HD void dmvr_decide(const SubPuDev& u, const uint32_t* c, int* tdx_out, int* 
   *tdy_out = tdy;
 }
 
-// thread per sub-PU: the decision, and the refined MVs (merge0 + delta, merge1 - delta, clipped to
-// the MV storage range as pu.mvdL0SubPu is applied) written into the sub-PU's planned jobs, which
+// The refined MVs of sub-PU s (merge0 + delta, merge1 - delta, clipped to the MV storage range as
+// pu.mvdL0SubPu is applied, InterPrediction.cpp:2602-2606) written into its planned jobs, which
 // k_setup reads next.  mvd (optional): the delta per sub-PU.
-MM_HD void dmvr_decide_jobs_thread(int s, const SubPuDev* sp, const uint32_t* costs, JobDev* jobs, int32_t* mvd) {
-  const SubPuDev& u = sp[s];
-  int tdx, tdy;
-  dmvr_decide(u, costs + (size_t)s * N_OFF, &tdx, &tdy);
+MM_HD void dmvr_apply(int s, const SubPuDev& u, int tdx, int tdy, JobDev* jobs, int32_t* mvd) {
   for (int k = 0; k < 4; k++) {
     if (u.jidx[k] < 0) continue;
     const int l = k >> 1, sg = l ? -1 : 1;
@@ -215,5 +172,48 @@ MM_HD void dmvr_decide_jobs_thread(int s, const SubPuDev* sp, const uint32_t* co
     mvd[2 * s + 1] = tdy;
   }
 }
+
+#if !defined(__HIP_DEVICE_COMPILE__)
+// The search of sub-PU s, sequentially (CPU twin): the centre cost, the early exit, the other 24
+// offsets, the decision -- the same per-element bodies the device search kernel runs in parallel
+// (mm_kernels.hip k_dmvr_search_dev), with the host's clamped-address filter.
+inline void dmvr_search_host(int s, const SeqConst& sc, const Geometry& geo, const Taps& taps, const SubPuDev* sp,
+                             const BlockSetup* setups, const MpaCache& cache, const RefDev* refs, JobDev* jobs,
+                             int32_t* mvd) {
+  const SubPuDev& u = sp[s];
+  uint32_t cost[N_OFF];
+  for (int i = 0; i < N_OFF; i++) cost[i] = 0;
+  auto eval = [&](int o) {
+    uint32_t sum = 0;
+    for (int e = 0; e < u.n; e++) {
+      int32_t fx[2], fy[2];
+      dmvr_positions(sc, u, setups[dmvr_setup_index(s, o, 0)], setups[dmvr_setup_index(s, o, 1)], cache, e, fx, fy);
+      int16_t p[2][16];
+      for (int l = 0; l < 2; l++) {
+        const int xPos = fx[l] >> 4, yPos = fy[l] >> 4, xFrac = fx[l] & 15, yFrac = fy[l] & 15;
+        const RefDev& r = refs[u.slot[l]];
+        if (sb_out_of_range(xPos, yPos, geo.W, geo.H, geo.maxCUw, geo.maxCUh, 4, 4)) {
+          for (int i = 0; i < 16; i++) p[l][i] = 0;
+        } else {
+          predict_subblock<8, 4, 4>(r.y, r.stride_y, geo.W, geo.H, xPos, yPos, taps.luma[xFrac], taps.luma[yFrac], true,
+                                    geo.bd, p[l]);
+        }
+      }
+      const int16_t a[8] = {p[0][0], p[0][1], p[0][2], p[0][3], p[0][8], p[0][9], p[0][10], p[0][11]};
+      const int16_t b[8] = {p[1][0], p[1][1], p[1][2], p[1][3], p[1][8], p[1][9], p[1][10], p[1][11]};
+      sum += dmvr_sad_rows02(a, b);
+    }
+    return sum;
+  };
+  cost[12] = eval(12);
+  const uint32_t minc = cost[12] - (cost[12] >> 2);
+  if (minc >= (uint32_t)(u.w * u.h))  // else the early exit: dmvr_decide reads only the centre
+    for (int o = 0; o < N_OFF; o++)
+      if (o != 12) cost[o] = eval(o);
+  int tdx, tdy;
+  dmvr_decide(u, cost, &tdx, &tdy);
+  dmvr_apply(s, u, tdx, tdy, jobs, mvd);
+}
+#endif
 
 }  // namespace mmdmvr

@@ -336,6 +336,65 @@ __device__ __forceinline__ void predict_rows(const Rows& rows, const uint32_t* _
     }
   }
 }
+// Rows 0 and 2 of a luma 4x4 14-bit (bi) prediction -- all that MM-DMVR's xDMVRCost reads of a sub-block
+// (RdCost subShift 1 over the sub-PU: its even rows, InterPrediction.cpp:2147-2155): the H pass over
+// window rows 0..9, the V pass for output rows 0 and 2 only; the same integer sums as predict_rows.
+// out: row 0 (4 samples), then row 2.
+template <class Rows>
+__device__ __forceinline__ void predict_rows02(const Rows& rows, const uint32_t* __restrict__ ht,
+                                               const uint32_t* __restrict__ vt, int bd, int16_t* out) {
+  constexpr int SBW = 4, R = 10, ND = 6, NP = 4, NQ = 5, RP = 5;
+  const FiltParam fh = filt_param(true, false, bd);
+  const FiltParam fv = filt_param(false, false, bd);
+  uint32_t he[NQ], ho[NQ], ve[NP];
+#pragma unroll
+  for (int k = 0; k < NQ; k++) {
+    he[k] = ht[k];
+    ho[k] = ht[NQ + k];
+  }
+#pragma unroll
+  for (int k = 0; k < NP; k++) ve[k] = vt[k];
+  uint32_t tmp[R][SBW];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    uint32_t d[ND];
+    rows.template load<ND>(r, d);
+#pragma unroll
+    for (int c = 0; c < SBW; c++) {
+      const uint32_t* tp = (c & 1) ? ho : he;
+      int sum = dot2_seed_(d[c >> 1], tp[0], fh.offset);
+#pragma unroll
+      for (int k = 1; k < NQ; k++) sum = dot2_(d[(c >> 1) + k], tp[k], sum);
+      tmp[r][c] = (uint32_t)(sum >> fh.shift);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < SBW; c++) {
+    uint32_t pr[RP];
+#pragma unroll
+    for (int m = 0; m < RP; m++) pr[m] = pack_lo16_(tmp[2 * m][c], tmp[2 * m + 1][c]);
+#pragma unroll
+    for (int h = 0; h < 2; h++) {  // output rows 0 (pairs 0..3) and 2 (pairs 1..4)
+      int sum = dot2_seed_(pr[h], ve[0], fv.offset);
+#pragma unroll
+      for (int k = 1; k < NP; k++) sum = dot2_(pr[h + k], ve[k], sum);
+      out[4 * h + c] = (int16_t)(sum >> fv.shift);
+    }
+  }
+}
+// Window rows staged in LDS: row r of the window is `stride` dwords after row r - 1 (dword-aligned
+// rows, read as dwords)
+struct LdsRows {
+  const uint32_t* base;
+  int stride;
+  template <int ND>
+  __device__ __forceinline__ void load(int r, uint32_t* d) const {
+    const uint32_t* p = base + r * stride;
+#pragma unroll
+    for (int k = 0; k < ND; k++) d[k] = p[k];
+  }
+};
+
 // Interior window of sub-block (xPos, yPos) of a pooled plane whose first sample is at byte
 // `plane_off` of the pool (soff: uniform extra offset, e.g. Cr = Cb + cr_delta).
 template <int NT, int SBW, int SBH>

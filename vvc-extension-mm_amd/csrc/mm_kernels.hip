@@ -500,75 +500,190 @@ __global__ void __launch_bounds__(256) k_me_sad(SeqConst sc, Geometry geo, MeWin
 // --------------------------------------------------------------------------------------------
 // MM-DMVR inside the device-planned picture (MM_PUF_DMVR PUs, mm_dmvr.h): k_plan_place placed the
 // sub-PU records; these run between k_plan_place and k_setup_dev.  Their sizes live on the device
-// (the DMVR share of a device-resident list is unknown to the host), so they are grid-stride loops
-// over a fixed grid instead of capacity-sized grids of mostly idle workgroups.
+// (the DMVR share of a device-resident list is unknown to the host), so they loop over a fixed grid
+// instead of capacity-sized grids of mostly idle workgroups.
 // --------------------------------------------------------------------------------------------
 using namespace mmdmvr;
-constexpr int DMVR_GRID = 2048;  // workgroups of 256 of the grid-stride DMVR kernels
+constexpr int DMVR_GRID = 2048;  // workgroups of 256 of the grid-stride setup kernel
 
-// thread per (sub-PU, offset, list) setup; the (sub-PU, offset) cost word is zeroed with list 0's
+// thread per (sub-PU, offset, list) setup
 __global__ void __launch_bounds__(256) k_dmvr_setup_dev(SeqConst sc, const PlanMeta* __restrict__ meta,
                                                         const SubPuDev* __restrict__ sp, const PicTables t,
-                                                        BlockSetup* __restrict__ out, uint32_t* __restrict__ costs) {
+                                                        BlockSetup* __restrict__ out) {
   const int n_jobs = meta->n_sub * N_OFF * 2;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n_jobs; i += gridDim.x * blockDim.x) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n_jobs; i += gridDim.x * blockDim.x)
     dmvr_setup_thread(i, sc, sp, t.ged, out);
-    if ((i & 1) == 0) costs[i >> 1] = 0u;
-  }
 }
 
-// thread per (sub-PU, offset, 4x4 sub-block): both lists' reprojected luma positions
-__global__ void __launch_bounds__(256) k_dmvr_reproj_dev(SeqConst sc, const PlanMeta* __restrict__ meta,
-                                                         const SubPuDev* __restrict__ sp, const int* __restrict__ off,
-                                                         const int* __restrict__ chunk,
-                                                         const BlockSetup* __restrict__ setups, MpaCache cache,
-                                                         mm_int2* __restrict__ pos) {
-  const int n_elems = meta->n_dmvr_elems, n_sub = meta->n_sub;
-  const int lane = __lane_id();
-  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, n_waves = (gridDim.x * blockDim.x) >> 6;
-  for (int g0 = wave * 64; g0 < n_elems; g0 += n_waves * 64) {
-    const int g = g0 + lane;
-    const int si = wave_find_item(off, chunk, g, n_sub);
-    if (g < n_elems) dmvr_reproj_thread(g, si, sc, sp, setups, cache, pos);
-  }
-}
+// The search of one sub-PU per workgroup iteration (xProcessDMVRProjected, InterPrediction.cpp:
+// 2488-2580), one thread per (non-centre offset, 4x4 sub-block):
+//   1. the centre cost (wave 0, one lane per sub-block, window rows straight from the pool); the
+//      search ends there when cost - cost/4 < dx*dy (:2520-2525) -- then nothing else is evaluated;
+//   2. both lists' reprojected positions of the 24 other offsets (the VALU-heavy part);
+//   3. the union of every offset's luma window, per list, staged once into LDS (16-byte loads): the
+//      24 x 16 windows of a list lie within about (dx + 11) x (dy + 11) samples, so each staged
+//      sample serves ~50 window reads that would otherwise each be a global load; a union larger
+//      than the LDS window (strong warping, the ERP seam) reads the pool directly instead;
+//   4. rows 0 and 2 of both 14-bit predictions from LDS and their SAD, summed per offset over the
+//      16 lanes of its sub-blocks (xor shuffles inside the 16-lane segment);
+//   5. the decision (first strict minimum, error surface) and the refined MVs into the sub-PU's jobs.
+// Costs never leave the workgroup.
+constexpr int DMVR_SEARCH_WG = (N_OFF - 1) * 16;  // 384 threads: 24 offsets x 16 sub-blocks
+constexpr int DMVR_SEARCH_GRID = 1536;            // 6 workgroups per CU, grid-stride over the sub-PUs
+constexpr int DMVR_WIN_W = 64;                    // staged union window per list: samples x rows
+[[maybe_unused]] constexpr int DMVR_WIN_H = 48;
+[[maybe_unused]] constexpr int DMVR_WIN_STRIDE = DMVR_WIN_W / 2 + 1;  // dwords per LDS row: odd, so rows start on different banks
+static_assert(DMVR_SEARCH_WG == 384, "one thread per (non-centre offset, sub-block)");
 
-// thread per (sub-PU, offset, 4x4 sub-block): the two luma predictions and the sub-block's SAD share;
-// each wave's segments of equal cost index are summed across lanes (shuffle scan) and added by their
-// last lane
-__global__ void __launch_bounds__(256) k_dmvr_sad_dev(Geometry geo, const PlanMeta* __restrict__ meta,
-                                                      const SubPuDev* __restrict__ sp, const int* __restrict__ off,
-                                                      const int* __restrict__ chunk, const mm_int2* __restrict__ pos,
-                                                      const PicTables t, uint32_t* __restrict__ costs) {
-  const int n_elems = meta->n_dmvr_elems, n_sub = meta->n_sub;
-  const int lane = __lane_id();
-  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, n_waves = (gridDim.x * blockDim.x) >> 6;
-  const Taps taps{c_luma_taps, c_chroma_taps, &c_packed_taps, t.pool};
-  for (int g0 = wave * 64; g0 < n_elems; g0 += n_waves * 64) {
-    const int g = g0 + lane;
-    const int si = wave_find_item(off, chunk, g, n_sub);
-    const bool active = g < n_elems;
-    int idx = -1 - lane;
-    uint32_t v = 0;
-    if (active) v = dmvr_sad_thread(g, si, geo, taps, sp, pos, t.ref, &idx);
+__device__ __forceinline__ uint32_t seg16_sum(uint32_t v) {  // sum over the 16-lane segment of this lane
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t vu = __shfl_up(v, d);
-      const int iu = __shfl_up(idx, d);
-      if (lane >= d && iu == idx) v += vu;
-    }
-    const int inext = __shfl_down(idx, 1);
-    if (active && (lane == 63 || inext != idx)) atomicAdd(&costs[idx], v);
-  }
+  for (int d = 1; d < 16; d <<= 1) v += __shfl_xor(v, d);
+  return v;
 }
 
-// thread per sub-PU: decision, refined MVs into the sub-PU's planned jobs (read next by k_setup_dev)
-__global__ void __launch_bounds__(256) k_dmvr_decide_dev(const PlanMeta* __restrict__ meta, const SubPuDev* __restrict__ sp,
-                                                         const uint32_t* __restrict__ costs, JobDev* __restrict__ jobs,
-                                                         int32_t* __restrict__ mvd) {
+__global__ void __launch_bounds__(DMVR_SEARCH_WG) k_dmvr_search_dev(SeqConst sc, Geometry geo,
+                                                                   const PlanMeta* __restrict__ meta,
+                                                                   const SubPuDev* __restrict__ sp,
+                                                                   const BlockSetup* __restrict__ setups, MpaCache cache,
+                                                                   const PicTables t, JobDev* __restrict__ jobs,
+                                                                   int32_t* __restrict__ mvd) {
+#if defined(__HIP_DEVICE_COMPILE__)  // device-only filter paths (mm_filter.h predict_rows02, PtrRows, LdsRows)
+  __shared__ PackedTaps s_taps;
+  __shared__ uint32_t s_win[2][DMVR_WIN_H * DMVR_WIN_STRIDE];
+  __shared__ int s_box[2][4];  // per list: min / max of the in-range xPos, yPos
+  __shared__ uint32_t s_cost[N_OFF];
+  __shared__ RefDev s_ref[MAX_SLOTS];  // looked up by the sub-PU's slots (indexing the kernel argument would copy it to scratch)
+  const int tid = threadIdx.x;
+  if (tid < sizeof(PackedTaps) / 16)
+    reinterpret_cast<uint4*>(&s_taps)[tid] = reinterpret_cast<const uint4*>(&c_packed_taps)[tid];
+  static_assert(sizeof(s_ref) % 8 == 0 && sizeof(s_ref) / 8 <= DMVR_SEARCH_WG, "one 8-byte word per thread");
+  if (tid < sizeof(s_ref) / 8) reinterpret_cast<uint2*>(s_ref)[tid] = reinterpret_cast<const uint2*>(t.ref)[tid];
   const int n_sub = meta->n_sub;
-  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < n_sub; s += gridDim.x * blockDim.x)
-    dmvr_decide_jobs_thread(s, sp, costs, jobs, mvd);
+  const RefPool pool = t.pool;
+  for (int s = blockIdx.x; s < n_sub; s += gridDim.x) {
+    const SubPuDev u = sp[s];
+    const uint32_t off_y[2] = {s_ref[u.slot[0]].off_y, s_ref[u.slot[1]].off_y};
+    const int stride_y[2] = {s_ref[u.slot[0]].stride_y, s_ref[u.slot[1]].stride_y};
+    if (tid < 8) (&s_box[0][0])[tid] = (tid & 1) ? INT_MIN : INT_MAX;
+    __syncthreads();  // s_taps staged; the previous sub-PU's LDS reads are done
+    // 1. centre cost
+    if (tid < 64) {
+      uint32_t v = 0;
+      if (tid < u.n) {
+        int32_t fx[2], fy[2];
+        dmvr_positions(sc, u, setups[dmvr_setup_index(s, 12, 0)], setups[dmvr_setup_index(s, 12, 1)], cache, tid, fx, fy);
+        int16_t p[2][8];
+#pragma unroll
+        for (int l = 0; l < 2; l++) {
+          const int xPos = fx[l] >> 4, yPos = fy[l] >> 4;
+          if (sb_out_of_range(xPos, yPos, geo.W, geo.H, geo.maxCUw, geo.maxCUh, 4, 4)) {
+#pragma unroll
+            for (int i = 0; i < 8; i++) p[l][i] = 0;
+          } else {
+            const int x0 = (xPos - 3) & ~1;
+            const PtrRows rows{pool.base + off_y[l] + (long)((yPos - 3) * stride_y[l] + x0) * 2, stride_y[l] * 2};
+            predict_rows02(rows, s_taps.lh[fx[l] & 15][(xPos - 3) & 1], s_taps.lv[fy[l] & 15], geo.bd, p[l]);
+          }
+        }
+        v = dmvr_sad_rows02(p[0], p[1]);
+      }
+      v = seg16_sum(v);
+      if (tid == 0) s_cost[12] = v;
+    }
+    __syncthreads();
+    const uint32_t c12 = s_cost[12];
+    const bool early = c12 - (c12 >> 2) < (uint32_t)(u.w * u.h);  // notZeroCost = false (:2520-2525)
+    if (!early) {
+      // 2. positions of the other 24 offsets
+      const int oo = tid >> 4, e = tid & 15, o = oo < 12 ? oo : oo + 1;
+      const bool valid = e < u.n;
+      int32_t fx[2] = {0, 0}, fy[2] = {0, 0};
+      bool inr[2] = {false, false};
+      if (valid) {
+        dmvr_positions(sc, u, setups[dmvr_setup_index(s, o, 0)], setups[dmvr_setup_index(s, o, 1)], cache, e, fx, fy);
+#pragma unroll
+        for (int l = 0; l < 2; l++)
+          inr[l] = !sb_out_of_range(fx[l] >> 4, fy[l] >> 4, geo.W, geo.H, geo.maxCUw, geo.maxCUh, 4, 4);
+      }
+#pragma unroll
+      for (int l = 0; l < 2; l++) {  // union box of the in-range windows: wave min / max, then LDS atomics
+        int xmin = inr[l] ? (fx[l] >> 4) : INT_MAX, xmax = inr[l] ? (fx[l] >> 4) : INT_MIN;
+        int ymin = inr[l] ? (fy[l] >> 4) : INT_MAX, ymax = inr[l] ? (fy[l] >> 4) : INT_MIN;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          xmin = min(xmin, __shfl_xor(xmin, d));
+          xmax = max(xmax, __shfl_xor(xmax, d));
+          ymin = min(ymin, __shfl_xor(ymin, d));
+          ymax = max(ymax, __shfl_xor(ymax, d));
+        }
+        if ((tid & 63) == 0 && xmin <= xmax) {
+          atomicMin(&s_box[l][0], xmin);
+          atomicMax(&s_box[l][1], xmax);
+          atomicMin(&s_box[l][2], ymin);
+          atomicMax(&s_box[l][3], ymax);
+        }
+      }
+      __syncthreads();
+      // 3. stage the union windows: columns [bx0, bx0 + 8 cw), rows [by0, by0 + rows)
+      int bx0[2], by0[2];
+      bool staged[2];
+#pragma unroll
+      for (int l = 0; l < 2; l++) {
+        const int xmin = s_box[l][0], xmax = s_box[l][1], ymin = s_box[l][2], ymax = s_box[l][3];
+        bx0[l] = (xmin - 3) & ~1;
+        by0[l] = ymin - 3;
+        const int cw = (xmax + 9 - bx0[l] + 7) >> 3, rows = ymax - ymin + 11;  // 16-byte chunks per row, rows
+        staged[l] = xmin <= xmax && cw * 8 <= DMVR_WIN_W && rows <= DMVR_WIN_H;
+        if (staged[l]) {
+          const char* src = pool.base + off_y[l] + (long)(by0[l] * stride_y[l] + bx0[l]) * 2;
+          for (int k = tid; k < rows * cw; k += DMVR_SEARCH_WG) {
+            const int r = k / cw, c = k - r * cw;
+            typedef uint32_t u4a4 __attribute__((ext_vector_type(4), aligned(4)));
+            const u4a4 q = *reinterpret_cast<const u4a4*>(src + ((long)r * stride_y[l] + 8 * c) * 2);
+            uint32_t* d = &s_win[l][r * DMVR_WIN_STRIDE + 4 * c];
+            d[0] = q.x;
+            d[1] = q.y;
+            d[2] = q.z;
+            d[3] = q.w;
+          }
+        }
+      }
+      __syncthreads();
+      // 4. rows 0 and 2 of both predictions, SAD per offset
+      uint32_t v = 0;
+      if (valid) {
+        int16_t p[2][8];
+#pragma unroll
+        for (int l = 0; l < 2; l++) {
+          const int xPos = fx[l] >> 4, yPos = fy[l] >> 4;
+          const uint32_t* ht = s_taps.lh[fx[l] & 15][(xPos - 3) & 1];
+          const uint32_t* vt = s_taps.lv[fy[l] & 15];
+          const int x0 = (xPos - 3) & ~1;
+          if (!inr[l]) {
+#pragma unroll
+            for (int i = 0; i < 8; i++) p[l][i] = 0;
+          } else if (staged[l]) {
+            const LdsRows rows{&s_win[l][(yPos - 3 - by0[l]) * DMVR_WIN_STRIDE + ((x0 - bx0[l]) >> 1)], DMVR_WIN_STRIDE};
+            predict_rows02(rows, ht, vt, geo.bd, p[l]);
+          } else {
+            const PtrRows rows{pool.base + off_y[l] + (long)((yPos - 3) * stride_y[l] + x0) * 2, stride_y[l] * 2};
+            predict_rows02(rows, ht, vt, geo.bd, p[l]);
+          }
+        }
+        v = dmvr_sad_rows02(p[0], p[1]);
+      }
+      v = seg16_sum(v);
+      if (e == 0) s_cost[o] = v;
+      __syncthreads();
+    }
+    // 5. the decision (the early exit reads only the centre) and the refined MVs
+    if (tid == 0) {
+      int tdx, tdy;
+      dmvr_decide(u, s_cost, &tdx, &tdy);
+      dmvr_apply(s, u, tdx, tdy, jobs, mvd);
+    }
+  }
+#endif
 }
 
 // --------------------------------------------------------------------------------------------
@@ -836,8 +951,6 @@ struct mm_ctx {
   // list) setups, the 25 costs and the refined deltas of every sub-PU; used on the context stream only
   bool dmvr = false;
   DevBuf<int> d_dmvr_mvd;
-  DevBuf<uint32_t> d_dmvr_cost;
-  DevBuf<mm_int2> d_dmvr_pos;  // both lists' reprojected positions per cost element
   DevBuf<BlockSetup> d_dmvr_setup;
   // MM-MVP: the device copy of the epipole list (refreshed when its version moves, staged through a
   // pinned buffer on the context stream), the host-buffer API's query / result buffers and the
@@ -1077,8 +1190,6 @@ int mm_destroy(mm_ctx* c) {
   for (auto& kv : c->orgs) (void)hipFree(kv.second.y);
   c->d_me_blocks.release();
   c->d_dmvr_mvd.release();
-  c->d_dmvr_cost.release();
-  c->d_dmvr_pos.release();
   c->d_dmvr_setup.release();
   c->d_mvp_q.release();
   c->d_mvp_out.release();
@@ -1367,8 +1478,6 @@ static int ensure_slot_buffers(mm_ctx* c, PlanSlot& S, int n, bool dmvr) {
     HIPCHK(c, S.dmvr_off.ensure(k.subs));
     HIPCHK(c, S.dmvr_chunk.ensure((size_t)k.dmvr_elems / 64 + 1));
     HIPCHK(c, c->d_dmvr_setup.ensure((size_t)k.subs * N_OFF * 2));
-    HIPCHK(c, c->d_dmvr_cost.ensure((size_t)k.subs * N_OFF));
-    HIPCHK(c, c->d_dmvr_pos.ensure(2 * (size_t)k.dmvr_elems));
     HIPCHK(c, c->d_dmvr_mvd.ensure(2 * (size_t)k.subs));
     S.dmvr_ensured = true;
   }
@@ -1436,15 +1545,10 @@ static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables
       back = false;
     }
     const int gd = (int)std::min<long>(DMVR_GRID, ((long)k.subs * N_OFF * 2 + 255) / 256 + 1);
-    const int gc = (int)std::min<long>(DMVR_GRID, ((long)k.dmvr_elems + 255) / 256 + 1);
-    hipLaunchKernelGGL(k_dmvr_setup_dev, dim3(gd), dim3(256), 0, st, c->sc, S.meta.p, S.dmvr_sub.p, t, c->d_dmvr_setup.p,
-                       c->d_dmvr_cost.p);
-    hipLaunchKernelGGL(k_dmvr_reproj_dev, dim3(gc), dim3(256), 0, st, c->sc, S.meta.p, S.dmvr_sub.p, S.dmvr_off.p,
-                       S.dmvr_chunk.p, c->d_dmvr_setup.p, make_cache(c), c->d_dmvr_pos.p);
-    hipLaunchKernelGGL(k_dmvr_sad_dev, dim3(gc), dim3(256), 0, st, geo, S.meta.p, S.dmvr_sub.p, S.dmvr_off.p,
-                       S.dmvr_chunk.p, c->d_dmvr_pos.p, t, c->d_dmvr_cost.p);
-    hipLaunchKernelGGL(k_dmvr_decide_dev, dim3(std::max(1, std::min(DMVR_GRID, (k.subs + 255) / 256))), dim3(256), 0, st,
-                       S.meta.p, S.dmvr_sub.p, c->d_dmvr_cost.p, S.jobs.p, want_mvd ? c->d_dmvr_mvd.p : nullptr);
+    hipLaunchKernelGGL(k_dmvr_setup_dev, dim3(gd), dim3(256), 0, st, c->sc, S.meta.p, S.dmvr_sub.p, t, c->d_dmvr_setup.p);
+    hipLaunchKernelGGL(k_dmvr_search_dev, dim3(std::max(1, std::min(DMVR_SEARCH_GRID, k.subs))), dim3(DMVR_SEARCH_WG),
+                       0, st, c->sc, geo, S.meta.p, S.dmvr_sub.p, c->d_dmvr_setup.p, make_cache(c), t, S.jobs.p,
+                       want_mvd ? c->d_dmvr_mvd.p : nullptr);
   }
   if (back && KERNEL_EVENTS) {  // plan-ahead: ev_plan completes with k_setup_dev
     hipExtLaunchKernelGGL(k_setup_dev, dim3(gs), dim3(256), 0, st, nullptr, c->ev_plan, 0, c->sc, S.meta.p, S.jobs.p, t,
