@@ -244,8 +244,10 @@ def bench_pictures(args, cfg, params, rank, world, local, dist):
     kernel_ms = float(st[3])
     alg_step = float(np.mean([alg[s % P_] for s in range(args.kernel_steps)]))
     achieved = alg_step / (kernel_ms * 1e-3) / 1e9
-    mvp = (mvp_per_picture(ctx, cfg, int(np.mean([len(p) for _, p, _ in pictures])))
-           if args.config == "C3" and not args.no_mvp else None)
+    mvp = None
+    if args.config == "C3" and not args.no_mvp:
+        mvp = mvp_per_picture(ctx, cfg, int(np.mean([len(p) for _, p, _ in pictures])))
+        mvp["in_loop"] = mvp_in_loop(args, ctx, cfg, pictures, d_pus, outs, area)
 
     cpu, bit_exact, mism = None, None, None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -279,8 +281,10 @@ def bench_pictures(args, cfg, params, rank, world, local, dist):
         }
         if mvp is not None:
             line["mvp"] = mvp
-        print(json.dumps(line), flush=True)
+        ctx.close()
+        return line
     ctx.close()
+    return None
 
 
 def mvp_per_picture(ctx, cfg, n_pus, reps=10):
@@ -315,6 +319,69 @@ def mvp_per_picture(ctx, cfg, n_pus, reps=10):
     return {"queries_per_picture": int(len(q)), "ms_per_picture": round(wall * 1e3, 4),
             "kernel_ms": round(float(np.mean(dev)), 4), "host_buffer_call_ms": round(host * 1e3, 4),
             "note": "device-resident queries (mm_mvp_convert_device), back-to-back calls; not part of value"}
+
+
+def mvp_in_loop(args, ctx, cfg, pictures, d_pus, outs, area):
+    """C3 with MM-MVP in the decode loop: picture t+1's conversions (one per PU and list, one
+    batch) run on their own stream (mm_set_mvp_stream) while picture t is predicted on the context
+    stream, and picture t's prediction -- planning included, so plan-ahead is off here -- waits for
+    its own conversions (an event): a decoder that derives the next picture's MVs while the
+    current one is motion-compensated.  Also the latency of one CTU row's and one CTU's batch
+    (merge lists that chain, UnitTools.cpp:2269-2302, convert in dependent batches): device time of
+    the call and host wall time of the synchronous host-buffer call."""
+    P_ = len(pictures)
+    qs = [np.resize(W.mvp_queries(cfg.width, cfg.height, cfg.models, 20000, seed=11 + f), 2 * len(p))
+          for f, (_, p, _) in enumerate(pictures)]
+    d_q = [mm360.queries_to_device(q) for q in qs]
+    d_o = [torch.zeros((len(q), 2), dtype=torch.int32, device="cuda") for q in qs]
+    side = torch.cuda.Stream()
+    ctx.set_plan_ahead(False)
+    ctx.set_call_timing(False)
+    ctx.set_mvp_stream(side.cuda_stream)
+    ready = [torch.cuda.Event() for _ in range(P_)]
+    main = torch.cuda.current_stream()
+
+    def convert(f):
+        ctx.mvp_convert_device(d_q[f], d_o[f])
+        ready[f].record(side)
+
+    def step(s):
+        f = s % P_
+        if s == 0:
+            convert(0)
+        convert((s + 1) % P_)  # the next picture's MV derivation, overlapping this picture's MC
+        main.wait_event(ready[f])
+        ctx.predict_device(pictures[f][0], d_pus[f], *outs[f])
+
+    elapsed = timed(args.steps, args.warmup, step, None)
+    ctx.mvp_status()
+    ctx.synchronize()
+    ms = elapsed / args.steps * 1e3
+    steps_area = sum(area[s % P_] for s in range(args.steps))
+    # dependent batches: one CTU row (W / 128 CTUs) and one CTU of conversions
+    n_pic = len(qs[0])
+    rows = cfg.height // 128
+    lat = {}
+    ctx.set_mvp_stream(None)
+    ctx.set_call_timing(True)
+    for name, n in (("ctu_row", max(1, n_pic // rows)), ("ctu", max(1, n_pic // (rows * (cfg.width // 128))))):
+        dq, do = d_q[0][:n], d_o[0][:n]  # [queries, 20 words], [queries, 2]
+        dev = []
+        for _ in range(20):
+            ctx.mvp_convert_device(dq, do)
+            dev.append(ctx.last_timing_ms())
+        ctx.mvp_status()
+        host = float("inf")
+        for _ in range(20):
+            t0 = time.perf_counter()
+            ctx.mvp_convert(qs[0][:n])
+            host = min(host, time.perf_counter() - t0)
+        lat[name] = {"queries": int(n), "device_ms": round(float(np.median(dev[5:])), 4),
+                     "host_call_ms": round(host * 1e3, 4)}
+    return {"ms_per_picture": round(ms, 4), "mpix_s": round(steps_area / elapsed / 1e6, 2),
+            "note": "conversions of picture t+1 on their own stream during picture t's prediction; "
+                    "prediction of t (planning included, plan-ahead off) waits for its conversions",
+            "batch_latency": lat}
 
 
 def bench_c4(args, cfg, params, rank, world, local, dist):
@@ -475,6 +542,58 @@ def bench_c4_emulate(args, cfg, params):
     ctx.close()
 
 
+def c5_record(args, steps=3, warmup=1):
+    """The C5 configuration (encoder ME candidate evaluation, 2048x1024, all models, 33x33 integer
+    window per 16x16 block and model) beside the C3 line: Mcandidates/s over `steps` full windows,
+    bit_exact of the device SADs against the oracle on a seeded sample of blocks, and the bound of
+    k_me_sad from the committed PMC profile of this very library (VALU, not HBM: every candidate
+    reprojects its block), when one exists."""
+    import hashlib
+    cfg = W.CONFIGS["C5"]
+    params = mm360.seq_params(cfg.width, cfg.height, cfg.models)
+    blocks = W.me_blocks(cfg.width, cfg.height, cfg.models, grid=16, seed=5)
+    C = (2 * W.ME_RANGE + 1) ** 2
+    ctx = mm360.MMContext(params, device=torch.cuda.current_device())
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    ctx.set_epipole(W.CUR_POC, -1, W.GED_EPIPOLE_Q24)
+    refs = {poc: W.ref_planes(cfg.width, cfg.height, poc) for poc in W.REF_POCS}
+    for poc, (y, cb, cr) in refs.items():
+        ctx.upload_ref(poc, torch.from_numpy(y).cuda(), torch.from_numpy(cb).cuda(), torch.from_numpy(cr).cuda())
+    org = W.org_plane(cfg.width, cfg.height)
+    ctx.upload_org(W.CUR_POC, torch.from_numpy(org).cuda())
+    sads = torch.zeros((len(blocks), C), dtype=torch.int32, device="cuda")
+    kms = []
+
+    def step(s):
+        ctx.sad_window(W.CUR_POC, blocks, W.ME_RANGE, 16, out=sads)
+        kms.append(ctx.last_timing_ms())
+
+    elapsed = timed(steps, warmup, step, None)
+    got = sads.cpu().numpy().view(np.uint32)
+    ctx.close()
+    rng = np.random.default_rng(0x4D4D8000)
+    pick = np.sort(rng.choice(len(blocks), size=48, replace=False))
+    bit_exact = None
+    if not args.no_cpu_baseline:
+        from oracle.oracle import Oracle
+        want = Oracle(params, [(W.CUR_POC, -1, W.GED_EPIPOLE_Q24)]).sad_window(
+            W.CUR_POC, blocks[pick], W.ME_RANGE, 16, {poc: r[0] for poc, r in refs.items()}, org)
+        bit_exact = bool(np.array_equal(got[pick], want))
+    bound = None
+    path = os.path.join(ROOT, "profiles", "r04_c5_pmc.json")
+    if os.path.exists(path):
+        d = json.load(open(path))
+        if d.get("lib_sha256") == hashlib.sha256(open(mm360.LIB_PATH, "rb").read()).hexdigest():
+            bound = {k: d[k] for k in ("kernel", "valu_busy", "valu_utilization", "note") if k in d}
+    n_cand = len(blocks) * C
+    return {"workload": f"C5: {cfg.description}", "blocks": int(len(blocks)), "candidates": int(n_cand),
+            "value": round(n_cand * steps / elapsed / 1e6, 2), "unit": "Mcandidates/s",
+            "ms_per_window_set": round(elapsed / steps * 1e3, 3),
+            "kernel_ms": round(float(np.mean(kms[warmup:])), 3),
+            "bit_exact": bit_exact, "bit_exact_sample": f"{len(pick)} seeded blocks x {C} candidates vs the oracle",
+            "bound": bound}
+
+
 def bench_me(args, cfg, params, rank, world, local, dist):
     """C5: encoder ME candidate evaluation -- every block of the 16x16 PU grid once per model, a
     33x33 integer window each, reprojection + 8-tap + SAD per candidate (mm_sad_window).  Each
@@ -551,6 +670,7 @@ def main():
     ap.add_argument("--pictures", type=int, default=4, help="C3: distinct pictures (each with its own references)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-mvp", action="store_true", help="C3: skip the MM-MVP figure beside the line")
+    ap.add_argument("--no-c5", action="store_true", help="C3: skip the C5 (encoder ME) sub-record beside the line")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="length of the one-thread CPU baseline sample")
     ap.add_argument("--kernel-steps", type=int, default=8, help="extra steps timed per launch with HIP events")
     ap.add_argument("--lib", default=None, help="alternative build of libmm360.so (A/B experiments)")
@@ -598,7 +718,11 @@ def main():
     elif args.config == "C4":
         bench_c4(args, cfg, params, rank, world, local, dist)
     else:
-        bench_pictures(args, cfg, params, rank, world, local, dist)
+        line = bench_pictures(args, cfg, params, rank, world, local, dist)
+        if line is not None:
+            if args.config == "C3" and world == 1 and not args.no_c5:
+                line["c5"] = c5_record(args)
+            print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()
 

@@ -294,6 +294,14 @@ int mm_mvp_convert(mm_ctx* ctx, const mm_mvp_query* queries, int n, int32_t* mv_
  * mm_synchronize (its result words are 0). */
 int mm_mvp_convert_device(mm_ctx* ctx, const mm_mvp_query* d_queries, int n, int32_t* d_mv_out);
 int mm_mvp_status(mm_ctx* ctx, int* first_bad_query);
+/* The stream MM-MVP conversions run on (hipStream_t; NULL = the context stream, the default).  A
+ * decoder that derives picture t+1's MVs while picture t is motion-compensated converts on its
+ * own stream, so the conversions overlap the picture kernels; it orders the prediction of t+1
+ * after them itself (an event on this stream).  Epipole-table refreshes (made on the context
+ * stream) are ordered before the conversions that follow them.  mm_mvp_status / mm_mvp_convert
+ * wait for this stream; the call's device time (mm_last_timing) is recorded only while call
+ * timing is on. */
+int mm_set_mvp_stream(mm_ctx* ctx, void* hip_stream);
 
 /* Single-block interpolation (InterpolationFilter::filterHor/filterVer on the device), for
  * parity tests of the integer pel pipeline.  comp 0 = luma 8-tap (16 phases), else chroma 4-tap
@@ -355,15 +363,20 @@ int mm_set_stripes(mm_ctx* ctx, int stripes);
 int mm_set_dmvr(mm_ctx* ctx, int on);
 
 /* Plan-ahead for mm_pred_device (default off): a picture's planning and setup kernels run on the
- * internal auxiliary stream, gated by the context stream's position when the PREVIOUS
- * mm_pred_device call was issued, so they overlap the previous picture's interpolation; the
- * reprojection and interpolation stay on the context stream after them.  Contract while on: the
- * device PU list of a call is complete by the time the previous call is issued (written by the
- * host, or by work enqueued on the context stream before that call).  Applies to one-stripe calls
- * without stage timing; results do not depend on the setting.  While on, each call returns only
- * after its picture's planning has run on the device (it waits for the previous picture's
- * interpolation but one), so the host stays about one picture ahead of the GPU.  (No reference
- * counterpart: VTM decodes a picture's PUs inside its own CTU loop.) */
+ * internal auxiliary stream, gated only by the completion of the interpolation kernel of the call
+ * TWO back (the last user of the plan buffers they overwrite), so they overlap the previous
+ * picture's reprojection and interpolation; the reprojection and interpolation stay on the
+ * context stream after them.  Contract while on: the device PU list of call N is complete before
+ * call N is issued AND is not written by device work that could still run after call N-2's
+ * interpolation -- i.e. it is written by the host, by device work the caller has synchronised, or
+ * by work enqueued on the context stream before call N-2 was issued.  A list written on the
+ * context stream between calls N-2 and N is NOT ordered before call N's planning (synchronise
+ * first, or keep plan-ahead off).  mm_pred / mm_pred_prepare + mm_pred_run copy and synchronise, so
+ * they always qualify.  Applies to one-stripe calls without stage timing; results do not depend
+ * on the setting.  While on, each call returns only after its picture's planning has run on the
+ * device (it waits for the interpolation of the call two back), so the host stays about one
+ * picture ahead of the GPU.  (No reference counterpart: VTM decodes a picture's PUs inside its
+ * own CTU loop.) */
 int mm_set_plan_ahead(mm_ctx* ctx, int on);
 
 #ifdef __cplusplus

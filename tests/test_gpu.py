@@ -396,6 +396,47 @@ def test_pred_plan_ahead_rotating_pictures():
         assert ctx.status() == (mm360.MM_OK, -1)
 
 
+def test_pred_plan_ahead_lists_written_on_the_context_stream():
+    """Plan-ahead contract (mm360.h mm_set_plan_ahead): the planning of call N waits for the
+    interpolation of call N-2, so a device list written by work on the context stream is ordered
+    before call N's planning when that work was enqueued before call N-2 was issued.  Each list is
+    copied into its device buffer (hipMemcpyAsync on the context stream, from pinned host memory)
+    just before the call two ahead of it; a buffer is rewritten only after its previous picture's
+    call completed.  Every output == the oracle."""
+    cfg = W.CONFIGS["C2"]
+    params = mm360.seq_params(cfg.width, cfg.height, cfg.models)
+    lists = [W.pu_list(cfg, frame=f) for f in (11, 12, 13, 14, 15)]
+    n_max = max(len(p) for p in lists)
+    refs = {poc: W.ref_planes(cfg.width, cfg.height, poc) for poc in W.REF_POCS}
+    orc = Oracle(params, EPI)
+    want = [orc.predict(W.CUR_POC, p, refs, cfg.width, cfg.height) for p in lists]
+    stream = torch.cuda.current_stream()
+    with _ctx(params) as ctx:
+        ctx.set_stream(stream.cuda_stream)
+        for poc, (y, cb, cr) in refs.items():
+            ctx.upload_ref(poc, torch.from_numpy(y).cuda(), torch.from_numpy(cb).cuda(), torch.from_numpy(cr).cuda())
+        ctx.set_plan_ahead(True)
+        host = [torch.from_numpy(p.view(np.uint8)).pin_memory() for p in lists]
+        bufs = [torch.zeros(n_max * mm360.PU_DTYPE.itemsize, dtype=torch.uint8, device="cuda") for _ in range(3)]
+        outs = [_planes(cfg, -1) for _ in lists]
+        torch.cuda.synchronize()
+        order = list(range(len(lists))) * 2
+        for i, k in enumerate(order):
+            if i == 0:  # lists 0 and 1 ahead of the first call
+                for j in (0, 1):
+                    bufs[j][: host[order[j]].numel()].copy_(host[order[j]], non_blocking=True)
+            if i + 2 < len(order):  # list i + 2 now: before call i, two calls ahead of its own
+                b = bufs[(i + 2) % 3]
+                b[: host[order[i + 2]].numel()].copy_(host[order[i + 2]], non_blocking=True)
+            buf = bufs[i % 3]
+            ctx.predict_device(W.CUR_POC, buf[: host[k].numel()].view(torch.int32), *outs[k])
+        assert ctx.status() == (mm360.MM_OK, -1)
+        for k, o in enumerate(outs):
+            for x, t, name in zip(want[k], o, ("y", "cb", "cr")):
+                got = t.cpu().numpy()
+                assert np.array_equal(got, x), (k, plane_mismatch(name, got, x))
+
+
 def test_pred_plan_ahead_interleaved_call_kinds():
     """Plan-ahead stays on while other call kinds use the plan slots in between: a 2-stripe call
     (both slots, context and auxiliary streams), a per-list call (mm_pred_list) and a host-list

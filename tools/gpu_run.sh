@@ -34,6 +34,7 @@ for step in "$@"; do
     pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 ;;
     pmc_valu) run pmc_valu 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES -d gpurun_out/pmc_valu -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 ;;
     counters) run counters 300 rocprofv3 -L ;;
+    pmc_c5) run pmc_c5 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES GRBM_GUI_ACTIVE -d gpurun_out/pmc_c5 -o run --output-format csv -- python3 bench.py --config C5 --steps 2 --warmup 1 --no-cpu-baseline ;;
     pmc_mem) run pmc_mem 600 rocprofv3 --pmc TA_BUSY_avr TA_BUSY_max TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum -d gpurun_out/pmc_mem -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 ;;
     pmc_sq) run pmc_sq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU -d gpurun_out/pmc_sq -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 ;;
     pmc=*)  # pmc=<tag>=<counter,counter,...>: one rocprofv3 --pmc pass over a short bench run

@@ -961,6 +961,9 @@ struct mm_ctx {
   hipEvent_t ev_epi = nullptr;
   unsigned long long epi_version = ~0ull;
   int epi_n = 0;
+  hipStream_t mvp_stream = nullptr;  // mm_set_mvp_stream; mvp_on_own = false: the context stream
+  bool mvp_on_own = false;
+  bool epi_fresh = false;  // an epipole-table copy on the context stream the MVP stream has not waited for
   DevBuf<mm_mvp_query> d_mvp_q;
   DevBuf<int32_t> d_mvp_out;
   DevBuf<unsigned long long> d_mvp_status;
@@ -1905,15 +1908,17 @@ static int sync_epi_table(mm_ctx* c) {
     std::copy(e.begin(), e.end(), c->h_epi);
     HIPCHK(c, hipMemcpyAsync(c->d_epi.p, c->h_epi, e.size() * sizeof(mmmvp::EpiDev), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipEventRecord(c->ev_epi, c->stream));
+    c->epi_fresh = true;
   }
   c->epi_n = (int)e.size();
   c->epi_version = c->epipoles.version();
   return MM_OK;
 }
 
+static hipStream_t mvp_stream_of(const mm_ctx* c) { return c->mvp_on_own ? c->mvp_stream : c->stream; }
 static int read_mvp_status(mm_ctx* c, int* first_bad) {
   if (first_bad) *first_bad = -1;
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipStreamSynchronize(mvp_stream_of(c)));
   if (!c->mvp_pending) return MM_OK;
   c->mvp_pending = false;
   unsigned long long w = 0;
@@ -1928,14 +1933,27 @@ int mm_mvp_convert_device(mm_ctx* c, const mm_mvp_query* d_q, int n, int32_t* d_
   RCCHK(sync_epi_table(c));
   const mmmvp::EpiTable et{c->d_epi.p, c->epi_n};
   unsigned long long* st = c->d_mvp_status.p + c->mvp_par;
-  c->timed = true;
-  HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-  hipLaunchKernelGGL(k_mvp_dev, dim3((n + MVP_BLOCK - 1) / MVP_BLOCK), dim3(MVP_BLOCK), 0, c->stream, c->sc, d_q, n,
+  const hipStream_t ms = mvp_stream_of(c);
+  if (c->mvp_on_own && c->epi_fresh) HIPCHK(c, hipStreamWaitEvent(ms, c->ev_epi, 0));  // the table copy
+  c->epi_fresh = false;
+  c->timed = c->call_timing || !c->mvp_on_own;
+  if (c->timed) HIPCHK(c, hipEventRecord(c->ev0, ms));
+  hipLaunchKernelGGL(k_mvp_dev, dim3((n + MVP_BLOCK - 1) / MVP_BLOCK), dim3(MVP_BLOCK), 0, ms, c->sc, d_q, n,
                      c->prm.active_models, et, d_mv_out, st, c->d_mvp_status.p + (c->mvp_par ^ 1));
   HIPCHK(c, hipGetLastError());
-  HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+  if (c->timed) HIPCHK(c, hipEventRecord(c->ev1, ms));
   c->mvp_par ^= 1;  // read_mvp_status reads the word of this call (mvp_par ^ 1 from now on)
   c->mvp_pending = true;
+  return MM_OK;
+}
+
+int mm_set_mvp_stream(mm_ctx* c, void* s) {
+  if (!c) return MM_ERR_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(mvp_stream_of(c)));  // conversions already issued finish where they were
+  c->mvp_stream = (hipStream_t)s;
+  c->mvp_on_own = s != nullptr;
+  c->epi_fresh = c->mvp_on_own;  // order the next conversion after any table copy made so far
   return MM_OK;
 }
 
@@ -1950,9 +1968,10 @@ int mm_mvp_convert(mm_ctx* c, const mm_mvp_query* q, int n, int32_t* mv_out) {
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, c->d_mvp_q.ensure(n));
   HIPCHK(c, c->d_mvp_out.ensure(2 * (size_t)n));
-  HIPCHK(c, hipMemcpyAsync(c->d_mvp_q.p, q, (size_t)n * sizeof(mm_mvp_query), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_mvp_q.p, q, (size_t)n * sizeof(mm_mvp_query), hipMemcpyHostToDevice, mvp_stream_of(c)));
   RCCHK(mm_mvp_convert_device(c, c->d_mvp_q.p, n, c->d_mvp_out.p));
-  HIPCHK(c, hipMemcpyAsync(mv_out, c->d_mvp_out.p, 2 * (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(mv_out, c->d_mvp_out.p, 2 * (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost,
+                           mvp_stream_of(c)));
   return read_mvp_status(c, nullptr);
 }
 

@@ -54,6 +54,7 @@ EXPORTED_SYMBOLS = (
     "mm_set_stripes", "mm_set_plan_ahead", "mm_pred_list", "mm_derive_effective_blocks", "mm_epipole_list_create",
     "mm_epipole_list_destroy", "mm_get_epipole_list", "mm_epipole_add", "mm_epipole_make_available", "mm_epipole_has",
     "mm_epipole_find", "mm_epipole_derive_predictor", "mm_epipole_count", "mm_mvp_convert_device", "mm_mvp_status", "mm_set_dmvr",
+    "mm_set_mvp_stream",
 )
 
 BCW_DEFAULT = 2  # CommonDef.h:348-349; g_BcwWeights = {-2, 3, 4, 5, 10} (Rom.cpp:203)
@@ -167,6 +168,7 @@ def load_library() -> ctypes.CDLL:
         "mm_mvp_convert_device": (c_int, [vp, vp, c_int, vp]),
         "mm_mvp_status": (c_int, [vp, POINTER(c_int)]),
         "mm_set_dmvr": (c_int, [vp, c_int]),
+        "mm_set_mvp_stream": (c_int, [vp, vp]),
         "mm_pred_dmvr": (c_int, [vp, c_int, vp, c_int, vp, ctypes.c_ssize_t, vp, vp, ctypes.c_ssize_t, vp]),
         "mm_sad_window": (c_int, [vp, c_int, vp, c_int, c_int, c_int, vp]),
         "mm_last_stage_timing": (c_int, [vp, POINTER(c_float)]),
@@ -186,7 +188,10 @@ def load_library() -> ctypes.CDLL:
         "mm_epipole_derive_predictor": (c_int, [vp, c_int, POINTER(c_int32)]),
         "mm_epipole_count": (c_int, [vp]),
     }
+    default_lib = os.path.abspath(LIB_PATH) == os.path.join(os.path.dirname(_HERE), "lib", "libmm360.so")
     for name, (res, args) in sig.items():
+        if not default_lib and not hasattr(lib, name):
+            continue  # an older A/B build (bench.py --lib) without a newer entry point
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -416,6 +421,10 @@ class MMContext:
         import torch
         assert d_out.numel() >= 2 * n and d_out.dtype == torch.int32
         self._check(self.lib.mm_mvp_convert_device(self.h, c_void_p(_ptr(d_queries)), n, c_void_p(_ptr(d_out))))
+
+    def set_mvp_stream(self, stream_handle):
+        """mm_set_mvp_stream: MM-MVP conversions on this HIP stream (None: the context stream)."""
+        self._check(self.lib.mm_set_mvp_stream(self.h, c_void_p(stream_handle) if stream_handle else None))
 
     def mvp_status(self):
         """(code, first failing query) of the last mm_mvp_convert_device; raises MMError on failure."""
