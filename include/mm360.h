@@ -359,7 +359,12 @@ int mm_set_stripes(mm_ctx* ctx, int stripes);
  * integer + parabolic sub-pel, InterPrediction.cpp:2442-2634) on their <= 16x16 sub-PUs inside the
  * same asynchronous launch sequence -- planning, search, decision, then the refined sub-PUs'
  * setup / reprojection / interpolation with the rest of the picture.  Forces one stripe.  With it
- * off, a flagged PU is rejected (MM_ERR_ARG). */
+ * off, a flagged PU is rejected (MM_ERR_ARG).
+ * Device memory: the DMVR work buffers are sized for the largest list the picture can hold, since
+ * a device-resident list's DMVR share is unknown to the host -- per context, 56 * 50 bytes per
+ * possible sub-PU (W*H/128 of them: the per-offset block setups) plus 16 * 25 bytes per luma 4x4
+ * sub-block (the reprojected positions of both lists): about 0.9 GB at 6144x3072, allocated on the
+ * first DMVR picture and kept until mm_destroy. */
 int mm_set_dmvr(mm_ctx* ctx, int on);
 
 /* Plan-ahead for mm_pred_device (default off): a picture's planning and setup kernels run on the

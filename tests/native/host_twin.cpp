@@ -6,9 +6,6 @@
 // without a GPU; the GPU suite then checks the HIP library itself.
 //   g++ -O2 -std=c++17 -ffp-contract=off -fopenmp -fPIC -shared host_twin.cpp -o libhosttwin.so
 #include <algorithm>
-#include <climits>
-#include <cstdio>
-#include <cstdlib>
 #include <cmath>
 #include <string>
 #include <vector>
@@ -101,96 +98,6 @@ extern "C" int twin_reproject(const mm_seq_params* p, int n_epi, const int32_t* 
   return 0;
 }
 
-// Emulation of k_dmvr_search_dev's union-window staging (MM_TWIN_STAGING_CHECK=1, a debugging aid):
-// for sub-PU s, the bounding box of the in-range positions of the 24 non-centre offsets per list,
-// the staged region [bx0, bx0 + 8 cw) x [by0, by0 + rows) and each element's LDS row offset, checked
-// against the padded reference margins and the LDS window, and the rows-0/2 prediction read through
-// the staged window against the direct prediction.  Returns the number of violations.
-static int dmvr_staging_check(int s, const SeqConst& sc, const Geometry& geo, const mmdmvr::SubPuDev* sp,
-                              const BlockSetup* setups, const MpaCache& cache, const RefDev* refs) {
-  using namespace mmdmvr;
-  const SubPuDev& u = sp[s];
-  constexpr int WIN_W = 64, WIN_H = 48, STRIDE = WIN_W / 2 + 1;
-  int bad = 0;
-  int fx[24][16][2], fy[24][16][2];
-  bool inr[24][16][2];
-  int box[2][4] = {{INT_MAX, INT_MIN, INT_MAX, INT_MIN}, {INT_MAX, INT_MIN, INT_MAX, INT_MIN}};
-  for (int oo = 0; oo < 24; oo++)
-    for (int e = 0; e < 16; e++) {
-      const int o = oo < 12 ? oo : oo + 1;
-      for (int l = 0; l < 2; l++) inr[oo][e][l] = false;
-      if (e >= u.n) continue;
-      dmvr_positions(sc, u, setups[dmvr_setup_index(s, o, 0)], setups[dmvr_setup_index(s, o, 1)], cache, e, fx[oo][e],
-                     fy[oo][e]);
-      for (int l = 0; l < 2; l++) {
-        const int xPos = fx[oo][e][l] >> 4, yPos = fy[oo][e][l] >> 4;
-        inr[oo][e][l] = !sb_out_of_range(xPos, yPos, geo.W, geo.H, geo.maxCUw, geo.maxCUh, 4, 4);
-        if (!inr[oo][e][l]) continue;
-        box[l][0] = std::min(box[l][0], xPos);
-        box[l][1] = std::max(box[l][1], xPos);
-        box[l][2] = std::min(box[l][2], yPos);
-        box[l][3] = std::max(box[l][3], yPos);
-      }
-    }
-  const int mx = (geo.maxCUw + 4 + 8 + 63) & ~63, my = geo.maxCUh + 3 + 8;  // mm_kernels.hip plane_layout
-  for (int l = 0; l < 2; l++) {
-    const int xmin = box[l][0], xmax = box[l][1], ymin = box[l][2], ymax = box[l][3];
-    if (xmin > xmax) continue;
-    const int bx0 = (xmin - 3) & ~1, by0 = ymin - 3;
-    const int cw = (xmax + 9 - bx0 + 7) >> 3, rows = ymax - ymin + 11;
-    if (!(cw * 8 <= WIN_W && rows <= WIN_H)) continue;
-    if (bx0 < -mx || bx0 + 8 * cw > geo.W + mx || by0 < -my || by0 + rows > geo.H + my) {
-      fprintf(stderr, "staging s=%d l=%d outside the padded plane: box %d..%d x %d..%d\n", s, l, xmin, xmax, ymin, ymax);
-      bad++;
-    }
-    // the staged window, read from the clamped plane (== the padded margins)
-    std::vector<int16_t> win((size_t)WIN_H * STRIDE * 2, 0);
-    const RefDev& r = refs[u.slot[l]];
-    for (int rr = 0; rr < rows; rr++)
-      for (int k = 0; k < 8 * cw; k++) {
-        const int yy = std::min(std::max(by0 + rr, 0), geo.H - 1), xx = std::min(std::max(bx0 + k, 0), geo.W - 1);
-        win[(size_t)rr * STRIDE * 2 + k] = r.y[(long)yy * r.stride_y + xx];
-      }
-    for (int oo = 0; oo < 24; oo++)
-      for (int e = 0; e < u.n; e++) {
-        if (!inr[oo][e][l]) continue;
-        const int xPos = fx[oo][e][l] >> 4, yPos = fy[oo][e][l] >> 4, xFrac = fx[oo][e][l] & 15, yFrac = fy[oo][e][l] & 15;
-        const int x0 = (xPos - 3) & ~1;
-        const int li = (yPos - 3 - by0) * STRIDE + ((x0 - bx0) >> 1);
-        if (li < 0 || li + 9 * STRIDE + 6 > WIN_H * STRIDE) {
-          fprintf(stderr, "lds s=%d l=%d li=%d\n", s, l, li);
-          bad++;
-          continue;
-        }
-        // the window rows through the staged copy: sample k of row rr at 2 * li + rr * 2 * STRIDE + k
-        const int odd = (xPos - 3) & 1;
-        int h[10][4];
-        for (int rr = 0; rr < 10; rr++)
-          for (int c = 0; c < 4; c++) {
-            int sum = 0;
-            for (int t = 0; t < 8; t++) sum += win[(size_t)2 * li + (size_t)rr * 2 * STRIDE + odd + c + t] * LUMA_T[xFrac][t];
-            const FiltParam fh = filt_param(true, false, geo.bd);
-            h[rr][c] = (int16_t)((sum + fh.offset) >> fh.shift);
-          }
-        int16_t direct[16];
-        predict_subblock<8, 4, 4>(r.y, r.stride_y, geo.W, geo.H, xPos, yPos, LUMA_T[xFrac], LUMA_T[yFrac], true, geo.bd,
-                                  direct);
-        for (int hr = 0; hr < 2; hr++)
-          for (int c = 0; c < 4; c++) {
-            int sum = 0;
-            for (int t = 0; t < 8; t++) sum += h[2 * hr + t][c] * LUMA_T[yFrac][t];
-            const FiltParam fv = filt_param(false, false, geo.bd);
-            const int16_t v = (int16_t)((sum + fv.offset) >> fv.shift);
-            if (v != direct[2 * hr * 4 + c]) {
-              if (bad < 20) fprintf(stderr, "staged prediction s=%d l=%d o=%d e=%d differs\n", s, l, oo, e);
-              bad++;
-            }
-          }
-      }
-  }
-  return bad;
-}
-
 // The device-planned prediction path (mm_devplan.h + mm_pipeline.h bodies), run sequentially,
 // including the MM-DMVR search of MM_PUF_DMVR PUs (mm_dmvr.h bodies) between placement and setup.
 // mvd (optional): the refined deltas of the DMVR sub-PUs in placement order.
@@ -239,12 +146,6 @@ static int twin_pred_list(const Twin& t, const mmdev::PicTables& tab, const mm_p
 #pragma omp parallel for schedule(static)
     for (int j = 0; j < m.n_sub * N_OFF * 2; j++) dmvr_setup_thread(j, t.sc, subs.data(), tab.ged, dset.data());
     if (mvd) mvd->assign(2 * (size_t)m.n_sub, 0);
-    if (getenv("MM_TWIN_STAGING_CHECK")) {
-      int bad = 0;
-#pragma omp parallel for schedule(dynamic, 4) reduction(+ : bad)
-      for (int s = 0; s < m.n_sub; s++) bad += dmvr_staging_check(s, t.sc, t.geo, subs.data(), dset.data(), c, tab.ref);
-      fprintf(stderr, "staging check: %d sub-PUs, %d violations\n", m.n_sub, bad);
-    }
 #pragma omp parallel for schedule(dynamic, 4)
     for (int s = 0; s < m.n_sub; s++)
       dmvr_search_host(s, t.sc, t.geo, taps, subs.data(), dset.data(), c, tab.ref, jobs.data(),
@@ -282,6 +183,42 @@ static int twin_pred_list(const Twin& t, const mmdev::PicTables& tab, const mm_p
       mc_thread_rec<true>(g, geo, taps, mc, tab.ref, dy, sdy, dcb, dcr, sdc);
     else
       mc_thread_rec<false>(g, geo, taps, mc, tab.ref, dy, sdy, dcb, dcr, sdc);
+  return 0;
+}
+
+// One 4x4 luma / 2x2 chroma sub-block through the interpolation body (mm_pipeline.h mc_rec_impl)
+// at explicit positions, bypassing reprojection -- so positions ERP never produces (windows out of
+// range) can be checked.  use: bit 0 / 1 = list 0 / 1; pos[l] = luma x, y (1/16), chroma x, y
+// (1/32); one reference picture serves both lists.  out_y: 16 samples, out_cb / out_cr: 4 each.
+extern "C" int twin_mc_subblock(const mm_seq_params* p, int use, int bcw, int hp, const int32_t* pos,
+                                const int16_t* y, const int16_t* cb, const int16_t* cr, int stride_y, int stride_c,
+                                int16_t* out_y, int16_t* out_cb, int16_t* out_cr) {
+  Twin t;
+  t.geo = Geometry{p->width,        p->height,           p->width >> 1,        p->height >> 1,
+                   p->max_cu_width, p->max_cu_height,    p->max_cu_width >> 1, p->max_cu_height >> 1,
+                   p->bit_depth,    p->chroma_format == 1, 0,                     0,
+                   3,               0};
+  mm_int2 meta{0, (use & 1 ? MM_META_USE0 : 0) | (use & 2 ? MM_META_USE1 : 0) | ((bcw & 7) << 8)};
+  uint32_t lpos[2] = {MM_POS_FAR, MM_POS_FAR}, cpos[2] = {MM_POS_FAR, MM_POS_FAR};
+  mm_int2 far[2][2];
+  McRec mc;
+  mc.meta = &meta;
+  for (int l = 0; l < 2; l++) {
+    mc.lpos[l] = &lpos[l];
+    mc.cpos[l] = &cpos[l];
+    for (int q = 0; q < 2; q++) {
+      far[l][q] = mm_int2{pos[4 * l + 2 * q], pos[4 * l + 2 * q + 1]};
+      mc.far[l][q] = &far[l][q];
+    }
+  }
+  const RefDev refs[1] = {RefDev{y, cb, cr, stride_y, stride_c, 0u, 0u}};
+  const Taps taps{LUMA_T, CHROMA_T, nullptr, RefPool{}};
+  Geometry geo = t.geo;
+  geo.hp = hp;
+  if (hp)
+    mc_thread_rec<true>(0, geo, taps, mc, refs, out_y, 4, out_cb, out_cr, 2);
+  else
+    mc_thread_rec<false>(0, geo, taps, mc, refs, out_y, 4, out_cb, out_cr, 2);
   return 0;
 }
 

@@ -37,6 +37,8 @@ def load():
                                     c_int]
     lib.twin_sad_window.argtypes = [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
                                     c_void_p, c_int, c_void_p, c_int, c_void_p]
+    lib.twin_mc_subblock.argtypes = [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                                     c_int, c_void_p, c_void_p, c_void_p]
     return lib
 
 
@@ -156,3 +158,19 @@ def mvp(params, queries, epipoles=()):
     if rc:
         raise RuntimeError(f"twin mvp failed: {rc}")
     return out[:len(q)]
+
+
+def mc_subblock(params, use, bcw, hp, pos, planes):
+    """One sub-block through the interpolation body at explicit positions (no reprojection).
+    pos: int32 [2, 4] = per list (luma x, y in 1/16, chroma x, y in 1/32); planes: (y, cb, cr) of
+    the one reference both lists read.  Returns (4x4 luma, 2x2 cb, 2x2 cr)."""
+    lib = load()
+    pos = np.ascontiguousarray(pos, dtype=np.int32)
+    y, cb, cr = (np.ascontiguousarray(a, dtype=np.int16) for a in planes)
+    oy = np.zeros((4, 4), dtype=np.int16)
+    ocb = np.zeros((2, 2), dtype=np.int16)
+    ocr = np.zeros((2, 2), dtype=np.int16)
+    lib.twin_mc_subblock(ctypes.addressof(params), int(use), int(bcw), int(hp), c_void_p(pos.ctypes.data),
+                         c_void_p(y.ctypes.data), c_void_p(cb.ctypes.data), c_void_p(cr.ctypes.data), y.shape[1],
+                         cb.shape[1], c_void_p(oy.ctypes.data), c_void_p(ocb.ctypes.data), c_void_p(ocr.ctypes.data))
+    return oy, ocb, ocr

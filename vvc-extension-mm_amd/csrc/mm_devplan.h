@@ -70,6 +70,7 @@ struct PicTables {
   int only_list;           // -1: normal prediction; 0/1: mm_pred_list of that list (other list ignored)
   int dmvr;                // MM_PUF_DMVR PUs allowed (mm_set_dmvr: the picture's DMVR enable)
   RefPool pool;            // the context's reference pool (device interior filters)
+  uint32_t pool_slot4[MAX_SLOTS / 4];  // pool slot of table slot s: byte s % 4 of word s / 4 (device)
 };
 
 // Offsets of everything k_plan_place produced; written by k_plan_place's first thread.
@@ -182,9 +183,12 @@ MM_HD void classify_pu(const mm_pu_desc& u, const PicTables& t, PuPlan* p) {
       p->code = MM_ERR_MODEL;
       return;
     }
-    int s = -1;
+    int s = -1, cam = -1;  // the table is read at uniform indices only (kernel argument: scalar loads)
     for (int k = 0; k < t.n_slots; k++)
-      if (t.poc[k] == u.ref_poc[l]) s = k;
+      if (t.poc[k] == u.ref_poc[l]) {
+        s = k;
+        cam = t.ged_cam[k];
+      }
     if (s < 0) {
       p->code = MM_ERR_NOREF;
       return;
@@ -192,11 +196,11 @@ MM_HD void classify_pu(const mm_pu_desc& u, const PicTables& t, PuPlan* p) {
     p->slot[l] = s;
     int ged = -1;
     if (m == GEODESIC_CAMPOSE) {
-      if (t.ged_cam[s] < 0) {
+      if (cam < 0) {
         p->code = MM_ERR_NOEPIPOLE;
         return;
       }
-      ged = t.ged_cam[s];
+      ged = cam;
     } else if (m >= GEODESIC_X && m <= GEODESIC_Z) {
       ged = m - GEODESIC_X;
     }

@@ -11,11 +11,11 @@
 //   3. parabolic sub-pel refinement from the 5 costs around the best offset unless it lies on the
 //      window border (xDMVRSubPixelErrorSurface :2157-2175, xSubPelErrorSrfc :1996-2048);
 //   4. the sub-PU is predicted as a bi PU at merge0 + mvd / merge1 - mvd (all components, addAvg).
-// Steps 1-3 run here (k_dmvr_setup_dev, then k_dmvr_search_dev: one workgroup per sub-PU, the
-// centre cost first, the other 24 offsets only when the centre does not end the search) inside
-// the picture's device-planned launch sequence: the planner (mm_devplan.h) places every sub-PU of an MM_PUF_DMVR PU as a bi PU
+// Steps 1-3 run here (k_dmvr_setup_dev, then k_dmvr_search_dev: one workgroup per sub-PU, all 25
+// offsets at once -- the early exit then only selects what the decision reads) inside the
+// picture's device-planned launch sequence: the planner (mm_devplan.h) places every sub-PU of an MM_PUF_DMVR PU as a bi PU
 // with its reprojection jobs and a SubPuDev record pointing at them, the search runs on the
-// records, and k_dmvr_decide writes the refined MVs into those jobs before k_setup reads them --
+// records, and the search writes the refined MVs into those jobs before k_setup reads them --
 // step 4 is then the ordinary setup / reprojection / interpolation of the picture.
 #pragma once
 #include "../../include/mm360.h"
@@ -53,12 +53,12 @@ MM_HD void dmvr_setup_thread(int t, const SeqConst& sc, const SubPuDev* sp, cons
 
 MM_HD int dmvr_setup_index(int s, int o, int l) { return (s * N_OFF + o) * 2 + l; }
 
-// Luma 4x4 sub-block e (Eigen column-major index over the sub-PU) at offset o: the reprojected
-// positions of both lists (1/16 pel) -- L0 at merge0 + offset, L1 at merge1 - offset, from the
-// (sub-PU, offset, list) setups b0 / b1 (reprojectMotionVectorSubblocks of the sub-PU at that MV,
+// Luma 4x4 sub-block e (Eigen column-major index over the sub-PU) of one list at offset o: its
+// reprojected position (1/16 pel) -- L0 at merge0 + offset, L1 at merge1 - offset, from the
+// (sub-PU, offset, list) setup b (reprojectMotionVectorSubblocks of the sub-PU at that MV,
 // InterPrediction.cpp:2510-2515, 2544-2549).
-MM_HD void dmvr_positions(const SeqConst& sc, const SubPuDev& u, const BlockSetup& b0, const BlockSetup& b1,
-                          const MpaCache& cache, int e, int32_t* fx, int32_t* fy) {
+MM_HD void dmvr_position(const SeqConst& sc, const SubPuDev& u, const BlockSetup& b, const MpaCache& cache, int e,
+                         int32_t* fx, int32_t* fy) {
   const int col = e / u.rows, row = e - col * u.rows;
   const float gx = (float)(u.x + 4 * col) + sc.off, gy = (float)(u.y + 4 * row) + sc.off;
   const bool mpa = u.model >= MPA_FRONT_BACK && u.model <= MPA_TOP_BOTTOM;
@@ -69,8 +69,22 @@ MM_HD void dmvr_positions(const SeqConst& sc, const SubPuDev& u, const BlockSetu
   }
   const bool packet = packet_lane(e, u.n);
   const GridSphere pg = grid_point(cache, u.model, (u.x >> 2) + col, (u.y >> 2) + row, packet);
-  reproject_element(sc, b0, gx, gy, packet, mpa, px, py, vip, 0, &fx[0], &fy[0], pg);
-  reproject_element(sc, b1, gx, gy, packet, mpa, px, py, vip, 0, &fx[1], &fy[1], pg);
+  reproject_element(sc, b, gx, gy, packet, mpa, px, py, vip, 0, fx, fy, pg);
+}
+
+// Item g of the picture's DMVR position array: (sub-PU si, offset o, sub-block e, list l) with
+// g = 2 * (u.elem_off + o * n + e) + l -- one reprojection per thread, k_reproj's footprint.
+MM_HD void dmvr_reproj_item(int g, int si, const SeqConst& sc, const SubPuDev* sp, const BlockSetup* setups,
+                            const MpaCache& cache, mm_int2* pos) {
+  const SubPuDev& u = sp[si];
+  const int local = (g >> 1) - u.elem_off, l = g & 1;
+  const int o = local / u.n, e = local - o * u.n;
+  int32_t fx, fy;
+  dmvr_position(sc, u, setups[dmvr_setup_index(si, o, l)], cache, e, &fx, &fy);
+  mm_int2 q;
+  q.x = fx;
+  q.y = fy;
+  pos[g] = q;
 }
 
 // xDMVRCost's share of one 4x4 sub-block: SAD of its rows 0 and 2 (the sub-PU's even rows, RdCost
@@ -187,7 +201,7 @@ inline void dmvr_search_host(int s, const SeqConst& sc, const Geometry& geo, con
     uint32_t sum = 0;
     for (int e = 0; e < u.n; e++) {
       int32_t fx[2], fy[2];
-      dmvr_positions(sc, u, setups[dmvr_setup_index(s, o, 0)], setups[dmvr_setup_index(s, o, 1)], cache, e, fx, fy);
+      for (int l = 0; l < 2; l++) dmvr_position(sc, u, setups[dmvr_setup_index(s, o, l)], cache, e, &fx[l], &fy[l]);
       int16_t p[2][16];
       for (int l = 0; l < 2; l++) {
         const int xPos = fx[l] >> 4, yPos = fy[l] >> 4, xFrac = fx[l] & 15, yFrac = fy[l] & 15;

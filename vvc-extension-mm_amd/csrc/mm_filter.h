@@ -19,6 +19,10 @@ struct RefPool {
   const char* base;
   uint32_t bytes;
   int cr_delta;
+  // every pool slot has the same layout: slot k's luma plane origin is base + k * pic_bytes + y0,
+  // its Cb origin base + k * pic_bytes + cb0 (device kernels derive RefDev offsets from slot numbers)
+  uint32_t pic_bytes, y0, cb0;
+  int stride_y, stride_c;
 };
 
 // m_lumaFilter[16][8] (InterpolationFilter.cpp:82-100)
@@ -186,9 +190,11 @@ MM_HD bool window_interior(int xPos, int yPos, int Wc, int Hc) {
 
 // Row segment of L = SBW + NT - 1 samples starting at x, read as dwords from the even index
 // below x (planes are 4-byte aligned, stride even).
+#if defined(__clang__)  // clang vector types (hipcc); the g++ builds of the CPU twin never load them
 typedef uint32_t u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
 typedef uint32_t u32x3_a4 __attribute__((ext_vector_type(3), aligned(4)));
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+#endif
 
 // ND dwords from a 4-byte aligned address as few wide loads as possible (global_load_dwordx4 /
 // x3 / x2 only need dword alignment on CDNA)

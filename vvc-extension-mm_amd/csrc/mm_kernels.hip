@@ -13,8 +13,9 @@
 //              addAvg / uni output (xWeightedAverage), written straight into the picture planes.
 // (k_setup / k_reproj also serve the parity API mm_reproject on a host-planned block list; the
 // _dev variants read their sizes from the device plan.)
-// Reference planes stay resident in HBM, unpadded; the edge-replication margin of the reference
-// is realised by address clamping (identical results, no padded copies).
+// Reference planes stay resident in HBM in one pool, each plane with edge-replicated margins wide
+// enough for every in-range window (plane_layout below), so k_mc, the MM-DMVR search and the ME
+// SAD kernel read windows without clamping; the host twin clamps addresses instead (same values).
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
@@ -354,11 +355,14 @@ __global__ void __launch_bounds__(256) k_setup_dev(SeqConst sc, const PlanMeta* 
                                                    BlockSetup* __restrict__ out) {
   static_assert(sizeof(BlockSetup) % 8 == 0, "BlockSetup image is copied in 8-byte words");
   __shared__ alignas(16) BlockSetup s_set[256];
+  __shared__ M3 s_ged[3 + MAX_SLOTS];  // indexed per lane: staged with scalar loads (stage_arg_words)
   const int n_jobs = meta->n_jobs;
   const int base = blockIdx.x * 256;
   if (base >= n_jobs) return;
+  stage_arg_words<sizeof(s_ged) / 4>(reinterpret_cast<const uint32_t*>(t.ged), reinterpret_cast<uint32_t*>(s_ged));
+  __syncthreads();
   const int i = base + threadIdx.x;
-  if (i < n_jobs) setup_job(jobs[i], sc, t.ged, &s_set[threadIdx.x]);
+  if (i < n_jobs) setup_job(jobs[i], sc, s_ged, &s_set[threadIdx.x]);
   __syncthreads();
   const int cnt = min(256, n_jobs - base);
   const int words = cnt * (int)(sizeof(BlockSetup) / 8);
@@ -403,13 +407,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   __shared__ PackedTaps s_taps;
   __shared__ RefDev s_ref[MAX_SLOTS];
   static_assert(sizeof(PackedTaps) % 16 == 0 && sizeof(PackedTaps) / 16 <= 256, "one 16-byte word per thread");
-  static_assert(sizeof(s_ref) % 8 == 0 && sizeof(s_ref) / 8 <= 256, "one 8-byte word per thread");
   const int first = b0 + (int)(blockIdx.x >> 3) * 256;
   if (first >= b1) return;  // whole workgroup past the band's end
   if (threadIdx.x < sizeof(PackedTaps) / 16)
     reinterpret_cast<uint4*>(&s_taps)[threadIdx.x] = reinterpret_cast<const uint4*>(&c_packed_taps)[threadIdx.x];
-  if (threadIdx.x < sizeof(s_ref) / 8)
-    reinterpret_cast<uint2*>(s_ref)[threadIdx.x] = reinterpret_cast<const uint2*>(t.ref)[threadIdx.x];
+  stage_ref_table<MAX_SLOTS>(t.pool_slot4, t.pool, s_ref);
   __syncthreads();
   const Taps taps{c_luma_taps, c_chroma_taps, &s_taps, t.pool};
   // s_ref: each lane looks its slots' pool offsets up in LDS; indexing the kernel-argument copy
@@ -445,9 +447,12 @@ using namespace mmme;
 
 __global__ void __launch_bounds__(256) k_me_setup(SeqConst sc, MeWindow w, const MeBlockDev* __restrict__ blocks,
                                                   int n_jobs, const PicTables t, BlockSetup* __restrict__ out) {
+  __shared__ M3 s_ged[3 + MAX_SLOTS];  // indexed per lane: staged with scalar loads (stage_arg_words)
+  stage_arg_words<sizeof(s_ged) / 4>(reinterpret_cast<const uint32_t*>(t.ged), reinterpret_cast<uint32_t*>(s_ged));
+  __syncthreads();
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_jobs) return;
-  me_setup_thread(i, sc, w, blocks, t.ged, out);
+  me_setup_thread(i, sc, w, blocks, s_ged, out);
 }
 
 // thread per (block, candidate, sub-block); the sub-block SADs of one candidate are summed
@@ -476,6 +481,9 @@ __global__ void __launch_bounds__(256) k_me_sad(SeqConst sc, Geometry geo, MeWin
                                                 int n_elems, const BlockSetup* __restrict__ setups, MpaCache cache,
                                                 const PicTables t, const int16_t* __restrict__ org, int org_stride,
                                                 uint32_t* __restrict__ sads) {
+  __shared__ RefDev s_ref[MAX_SLOTS];  // indexed per lane: rebuilt from scalar loads (stage_ref_table)
+  stage_ref_table<MAX_SLOTS>(t.pool_slot4, t.pool, s_ref);
+  __syncthreads();
   const int g = xcd_block() * blockDim.x + threadIdx.x;
   const int lane = __lane_id();
   if (g - lane >= n_elems) return;  // whole wave past the end
@@ -485,7 +493,7 @@ __global__ void __launch_bounds__(256) k_me_sad(SeqConst sc, Geometry geo, MeWin
   uint32_t v = 0;
   if (active) {
     const Taps taps{c_luma_taps, c_chroma_taps, &c_packed_taps, t.pool};
-    v = me_sad_thread(g, bi, sc, geo, taps, w, blocks, setups, cache, t.ref, org, org_stride, &idx);
+    v = me_sad_thread(g, bi, sc, geo, taps, w, blocks, setups, cache, s_ref, org, org_stride, &idx);
   }
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -510,156 +518,149 @@ constexpr int DMVR_GRID = 2048;  // workgroups of 256 of the grid-stride setup k
 __global__ void __launch_bounds__(256) k_dmvr_setup_dev(SeqConst sc, const PlanMeta* __restrict__ meta,
                                                         const SubPuDev* __restrict__ sp, const PicTables t,
                                                         BlockSetup* __restrict__ out) {
+  __shared__ M3 s_ged[3 + MAX_SLOTS];  // indexed per lane: staged with scalar loads (stage_arg_words)
+  stage_arg_words<sizeof(s_ged) / 4>(reinterpret_cast<const uint32_t*>(t.ged), reinterpret_cast<uint32_t*>(s_ged));
+  __syncthreads();
   const int n_jobs = meta->n_sub * N_OFF * 2;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n_jobs; i += gridDim.x * blockDim.x)
-    dmvr_setup_thread(i, sc, sp, t.ged, out);
+    dmvr_setup_thread(i, sc, sp, s_ged, out);
+}
+
+// thread per (sub-PU, offset, luma 4x4 sub-block, list): the reprojected position (mm_dmvr.h
+// dmvr_reproj_item), 8 bytes into the picture's DMVR position array.  One reprojection per thread
+// keeps this kernel at k_reproj's register footprint; the search below is load / LDS work.
+__global__ void __launch_bounds__(256) k_dmvr_reproj_dev(SeqConst sc, const PlanMeta* __restrict__ meta,
+                                                         const SubPuDev* __restrict__ sp, const int* __restrict__ off,
+                                                         const int* __restrict__ chunk,
+                                                         const BlockSetup* __restrict__ setups, MpaCache cache,
+                                                         mm_int2* __restrict__ pos) {
+  const int n_elems = meta->n_dmvr_elems, n_sub = meta->n_sub;
+  const int lane = __lane_id();
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, n_waves = (gridDim.x * blockDim.x) >> 6;
+  // wave w: list w & 1 of the 64 elements from 64 * (w >> 1) (wave_find_item wants lane-consecutive
+  // elements)
+  for (int w = wave; w < 2 * ((n_elems + 63) >> 6); w += n_waves) {
+    const int e = (w >> 1) * 64 + lane;
+    const int si = wave_find_item(off, chunk, e, n_sub);
+    if (e < n_elems) dmvr_reproj_item(2 * e + (w & 1), si, sc, sp, setups, cache, pos);
+  }
 }
 
 // The search of one sub-PU per workgroup iteration (xProcessDMVRProjected, InterPrediction.cpp:
-// 2488-2580), one thread per (non-centre offset, 4x4 sub-block):
-//   1. the centre cost (wave 0, one lane per sub-block, window rows straight from the pool); the
-//      search ends there when cost - cost/4 < dx*dy (:2520-2525) -- then nothing else is evaluated;
-//   2. both lists' reprojected positions of the 24 other offsets (the VALU-heavy part);
-//   3. the union of every offset's luma window, per list, staged once into LDS (16-byte loads): the
-//      24 x 16 windows of a list lie within about (dx + 11) x (dy + 11) samples, so each staged
+// 2488-2580), from the positions k_dmvr_reproj_dev wrote:
+//   1. the 25 offsets x n luma 4x4 sub-blocks x 2 lists positions into LDS (one 8-byte load per
+//      item), and per list the bounding box of the in-range windows;
+//   2. the union of every offset's luma window, per list, staged once into LDS (16-byte loads): the
+//      25 x n windows of a list lie within about (dx + 11) x (dy + 11) samples, so each staged
 //      sample serves ~50 window reads that would otherwise each be a global load; a union larger
 //      than the LDS window (strong warping, the ERP seam) reads the pool directly instead;
-//   4. rows 0 and 2 of both 14-bit predictions from LDS and their SAD, summed per offset over the
-//      16 lanes of its sub-blocks (xor shuffles inside the 16-lane segment);
-//   5. the decision (first strict minimum, error surface) and the refined MVs into the sub-PU's jobs.
-// Costs never leave the workgroup.
-constexpr int DMVR_SEARCH_WG = (N_OFF - 1) * 16;  // 384 threads: 24 offsets x 16 sub-blocks
-constexpr int DMVR_SEARCH_GRID = 1536;            // 6 workgroups per CU, grid-stride over the sub-PUs
-constexpr int DMVR_WIN_W = 64;                    // staged union window per list: samples x rows
+//   3. rows 0 and 2 of both 14-bit predictions per (offset, sub-block) and their SAD, summed per
+//      offset over its n sub-blocks (xor shuffles inside the n-lane segment);
+//   4. the decision (early exit on the centre cost, first strict minimum, error surface) and the
+//      refined MVs into the sub-PU's jobs.
+// All 25 costs are evaluated even when the centre ends the search (the decision then reads the
+// centre only).  Costs never leave the workgroup.
+constexpr int DMVR_SEARCH_WG = 256;
+constexpr int DMVR_SEARCH_GRID = 2048;  // 8 workgroups per CU, grid-stride over the sub-PUs
+[[maybe_unused]] constexpr int DMVR_MAX_ITEMS = N_OFF * 16 * 2;  // (offset, sub-block, list) items of a 16x16 sub-PU
+constexpr int DMVR_WIN_W = 64;                   // staged union window per list: samples x rows
 [[maybe_unused]] constexpr int DMVR_WIN_H = 48;
 [[maybe_unused]] constexpr int DMVR_WIN_STRIDE = DMVR_WIN_W / 2 + 1;  // dwords per LDS row: odd, so rows start on different banks
-static_assert(DMVR_SEARCH_WG == 384, "one thread per (non-centre offset, sub-block)");
 
-__device__ __forceinline__ uint32_t seg16_sum(uint32_t v) {  // sum over the 16-lane segment of this lane
-#pragma unroll
-  for (int d = 1; d < 16; d <<= 1) v += __shfl_xor(v, d);
-  return v;
-}
-
-__global__ void __launch_bounds__(DMVR_SEARCH_WG) k_dmvr_search_dev(SeqConst sc, Geometry geo,
-                                                                   const PlanMeta* __restrict__ meta,
+__global__ void __launch_bounds__(DMVR_SEARCH_WG) k_dmvr_search_dev(Geometry geo, const PlanMeta* __restrict__ meta,
                                                                    const SubPuDev* __restrict__ sp,
-                                                                   const BlockSetup* __restrict__ setups, MpaCache cache,
-                                                                   const PicTables t, JobDev* __restrict__ jobs,
-                                                                   int32_t* __restrict__ mvd) {
+                                                                   const mm_int2* __restrict__ pos, const PicTables t,
+                                                                   JobDev* __restrict__ jobs, int32_t* __restrict__ mvd) {
 #if defined(__HIP_DEVICE_COMPILE__)  // device-only filter paths (mm_filter.h predict_rows02, PtrRows, LdsRows)
   __shared__ PackedTaps s_taps;
   __shared__ uint32_t s_win[2][DMVR_WIN_H * DMVR_WIN_STRIDE];
-  __shared__ int s_box[2][4];  // per list: min / max of the in-range xPos, yPos
+  __shared__ mm_int2 s_pos[DMVR_MAX_ITEMS];  // item 2 * (o * n + e) + l
+  __shared__ int s_box[2][4];                // per list: min / max of the in-range xPos, yPos
   __shared__ uint32_t s_cost[N_OFF];
-  __shared__ RefDev s_ref[MAX_SLOTS];  // looked up by the sub-PU's slots (indexing the kernel argument would copy it to scratch)
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  static_assert(sizeof(PackedTaps) % 16 == 0 && sizeof(PackedTaps) / 16 <= DMVR_SEARCH_WG, "one 16-byte word per thread");
   if (tid < sizeof(PackedTaps) / 16)
     reinterpret_cast<uint4*>(&s_taps)[tid] = reinterpret_cast<const uint4*>(&c_packed_taps)[tid];
-  static_assert(sizeof(s_ref) % 8 == 0 && sizeof(s_ref) / 8 <= DMVR_SEARCH_WG, "one 8-byte word per thread");
-  if (tid < sizeof(s_ref) / 8) reinterpret_cast<uint2*>(s_ref)[tid] = reinterpret_cast<const uint2*>(t.ref)[tid];
   const int n_sub = meta->n_sub;
   const RefPool pool = t.pool;
+  // items alternate lists and the stride is even, so every item of a thread has the list tid & 1
   for (int s = blockIdx.x; s < n_sub; s += gridDim.x) {
     const SubPuDev u = sp[s];
-    const uint32_t off_y[2] = {s_ref[u.slot[0]].off_y, s_ref[u.slot[1]].off_y};
-    const int stride_y[2] = {s_ref[u.slot[0]].stride_y, s_ref[u.slot[1]].stride_y};
+    const int n = u.n, n_items = 2 * N_OFF * n, log2n = 31 - __clz(n);  // n: 8 or 16
+    // the sub-PU's slots are uniform: scalar loads of the kernel argument's table
+    const int slot0 = __builtin_amdgcn_readfirstlane(u.slot[0]), slot1 = __builtin_amdgcn_readfirstlane(u.slot[1]);
+    const uint32_t off_y[2] = {t.ref[slot0].off_y, t.ref[slot1].off_y};
+    const int stride_y[2] = {t.ref[slot0].stride_y, t.ref[slot1].stride_y};
     if (tid < 8) (&s_box[0][0])[tid] = (tid & 1) ? INT_MIN : INT_MAX;
-    __syncthreads();  // s_taps staged; the previous sub-PU's LDS reads are done
-    // 1. centre cost
-    if (tid < 64) {
-      uint32_t v = 0;
-      if (tid < u.n) {
-        int32_t fx[2], fy[2];
-        dmvr_positions(sc, u, setups[dmvr_setup_index(s, 12, 0)], setups[dmvr_setup_index(s, 12, 1)], cache, tid, fx, fy);
-        int16_t p[2][8];
-#pragma unroll
-        for (int l = 0; l < 2; l++) {
-          const int xPos = fx[l] >> 4, yPos = fy[l] >> 4;
-          if (sb_out_of_range(xPos, yPos, geo.W, geo.H, geo.maxCUw, geo.maxCUh, 4, 4)) {
-#pragma unroll
-            for (int i = 0; i < 8; i++) p[l][i] = 0;
-          } else {
-            const int x0 = (xPos - 3) & ~1;
-            const PtrRows rows{pool.base + off_y[l] + (long)((yPos - 3) * stride_y[l] + x0) * 2, stride_y[l] * 2};
-            predict_rows02(rows, s_taps.lh[fx[l] & 15][(xPos - 3) & 1], s_taps.lv[fy[l] & 15], geo.bd, p[l]);
-          }
-        }
-        v = dmvr_sad_rows02(p[0], p[1]);
+    __syncthreads();  // s_taps staged; the previous sub-PU's LDS reads and decision are done
+    // 1. positions of the (offset, sub-block, list) items and the in-range box of this thread's list
+    int xmin = INT_MAX, xmax = INT_MIN, ymin = INT_MAX, ymax = INT_MIN;
+    const mm_int2* src_pos = pos + 2 * (long)u.elem_off;
+    for (int i = tid; i < n_items; i += DMVR_SEARCH_WG) {
+      const mm_int2 q = src_pos[i];
+      s_pos[i] = q;
+      const int xPos = q.x >> 4, yPos = q.y >> 4;
+      if (!sb_out_of_range(xPos, yPos, geo.W, geo.H, geo.maxCUw, geo.maxCUh, 4, 4)) {
+        xmin = min(xmin, xPos);
+        xmax = max(xmax, xPos);
+        ymin = min(ymin, yPos);
+        ymax = max(ymax, yPos);
       }
-      v = seg16_sum(v);
-      if (tid == 0) s_cost[12] = v;
+    }
+#pragma unroll
+    for (int d = 2; d < 64; d <<= 1) {  // over the lanes of the same list (same parity)
+      xmin = min(xmin, __shfl_xor(xmin, d));
+      xmax = max(xmax, __shfl_xor(xmax, d));
+      ymin = min(ymin, __shfl_xor(ymin, d));
+      ymax = max(ymax, __shfl_xor(ymax, d));
+    }
+    if (lane < 2 && xmin <= xmax) {
+      atomicMin(&s_box[lane][0], xmin);
+      atomicMax(&s_box[lane][1], xmax);
+      atomicMin(&s_box[lane][2], ymin);
+      atomicMax(&s_box[lane][3], ymax);
     }
     __syncthreads();
-    const uint32_t c12 = s_cost[12];
-    const bool early = c12 - (c12 >> 2) < (uint32_t)(u.w * u.h);  // notZeroCost = false (:2520-2525)
-    if (!early) {
-      // 2. positions of the other 24 offsets
-      const int oo = tid >> 4, e = tid & 15, o = oo < 12 ? oo : oo + 1;
-      const bool valid = e < u.n;
-      int32_t fx[2] = {0, 0}, fy[2] = {0, 0};
-      bool inr[2] = {false, false};
-      if (valid) {
-        dmvr_positions(sc, u, setups[dmvr_setup_index(s, o, 0)], setups[dmvr_setup_index(s, o, 1)], cache, e, fx, fy);
+    // 2. stage the union windows: columns [bx0, bx0 + 8 cw), rows [by0, by0 + rows)
+    int bx0[2], by0[2];
+    bool staged[2];
 #pragma unroll
-        for (int l = 0; l < 2; l++)
-          inr[l] = !sb_out_of_range(fx[l] >> 4, fy[l] >> 4, geo.W, geo.H, geo.maxCUw, geo.maxCUh, 4, 4);
-      }
-#pragma unroll
-      for (int l = 0; l < 2; l++) {  // union box of the in-range windows: wave min / max, then LDS atomics
-        int xmin = inr[l] ? (fx[l] >> 4) : INT_MAX, xmax = inr[l] ? (fx[l] >> 4) : INT_MIN;
-        int ymin = inr[l] ? (fy[l] >> 4) : INT_MAX, ymax = inr[l] ? (fy[l] >> 4) : INT_MIN;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-          xmin = min(xmin, __shfl_xor(xmin, d));
-          xmax = max(xmax, __shfl_xor(xmax, d));
-          ymin = min(ymin, __shfl_xor(ymin, d));
-          ymax = max(ymax, __shfl_xor(ymax, d));
-        }
-        if ((tid & 63) == 0 && xmin <= xmax) {
-          atomicMin(&s_box[l][0], xmin);
-          atomicMax(&s_box[l][1], xmax);
-          atomicMin(&s_box[l][2], ymin);
-          atomicMax(&s_box[l][3], ymax);
+    for (int l = 0; l < 2; l++) {
+      const int bxmin = s_box[l][0], bxmax = s_box[l][1], bymin = s_box[l][2], bymax = s_box[l][3];
+      bx0[l] = (bxmin - 3) & ~1;
+      by0[l] = bymin - 3;
+      const int cw = (bxmax + 9 - bx0[l] + 7) >> 3, rows = bymax - bymin + 11;  // 16-byte chunks per row, rows
+      staged[l] = bxmin <= bxmax && cw * 8 <= DMVR_WIN_W && rows <= DMVR_WIN_H;
+      if (staged[l]) {
+        const char* src = pool.base + off_y[l] + (long)(by0[l] * stride_y[l] + bx0[l]) * 2;
+        for (int k = tid; k < rows * cw; k += DMVR_SEARCH_WG) {
+          const int r = k / cw, c = k - r * cw;
+          typedef uint32_t u4a4 __attribute__((ext_vector_type(4), aligned(4)));
+          const u4a4 q = *reinterpret_cast<const u4a4*>(src + ((long)r * stride_y[l] + 8 * c) * 2);
+          uint32_t* d = &s_win[l][r * DMVR_WIN_STRIDE + 4 * c];
+          d[0] = q.x;
+          d[1] = q.y;
+          d[2] = q.z;
+          d[3] = q.w;
         }
       }
-      __syncthreads();
-      // 3. stage the union windows: columns [bx0, bx0 + 8 cw), rows [by0, by0 + rows)
-      int bx0[2], by0[2];
-      bool staged[2];
-#pragma unroll
-      for (int l = 0; l < 2; l++) {
-        const int xmin = s_box[l][0], xmax = s_box[l][1], ymin = s_box[l][2], ymax = s_box[l][3];
-        bx0[l] = (xmin - 3) & ~1;
-        by0[l] = ymin - 3;
-        const int cw = (xmax + 9 - bx0[l] + 7) >> 3, rows = ymax - ymin + 11;  // 16-byte chunks per row, rows
-        staged[l] = xmin <= xmax && cw * 8 <= DMVR_WIN_W && rows <= DMVR_WIN_H;
-        if (staged[l]) {
-          const char* src = pool.base + off_y[l] + (long)(by0[l] * stride_y[l] + bx0[l]) * 2;
-          for (int k = tid; k < rows * cw; k += DMVR_SEARCH_WG) {
-            const int r = k / cw, c = k - r * cw;
-            typedef uint32_t u4a4 __attribute__((ext_vector_type(4), aligned(4)));
-            const u4a4 q = *reinterpret_cast<const u4a4*>(src + ((long)r * stride_y[l] + 8 * c) * 2);
-            uint32_t* d = &s_win[l][r * DMVR_WIN_STRIDE + 4 * c];
-            d[0] = q.x;
-            d[1] = q.y;
-            d[2] = q.z;
-            d[3] = q.w;
-          }
-        }
-      }
-      __syncthreads();
-      // 4. rows 0 and 2 of both predictions, SAD per offset
+    }
+    __syncthreads();
+    // 3. rows 0 and 2 of both predictions per (offset, sub-block), SAD per offset
+#pragma unroll 1
+    for (int base = 0; base < N_OFF * 16; base += DMVR_SEARCH_WG) {  // uniform trip count (shuffles below)
+      const int oe = base + tid;
       uint32_t v = 0;
-      if (valid) {
+      if (oe < N_OFF * n) {
         int16_t p[2][8];
 #pragma unroll
         for (int l = 0; l < 2; l++) {
-          const int xPos = fx[l] >> 4, yPos = fy[l] >> 4;
-          const uint32_t* ht = s_taps.lh[fx[l] & 15][(xPos - 3) & 1];
-          const uint32_t* vt = s_taps.lv[fy[l] & 15];
+          const mm_int2 q = s_pos[2 * oe + l];
+          const int xPos = q.x >> 4, yPos = q.y >> 4;
+          const uint32_t* ht = s_taps.lh[q.x & 15][(xPos - 3) & 1];
+          const uint32_t* vt = s_taps.lv[q.y & 15];
           const int x0 = (xPos - 3) & ~1;
-          if (!inr[l]) {
+          if (sb_out_of_range(xPos, yPos, geo.W, geo.H, geo.maxCUw, geo.maxCUh, 4, 4)) {
 #pragma unroll
             for (int i = 0; i < 8; i++) p[l][i] = 0;
           } else if (staged[l]) {
@@ -672,11 +673,11 @@ __global__ void __launch_bounds__(DMVR_SEARCH_WG) k_dmvr_search_dev(SeqConst sc,
         }
         v = dmvr_sad_rows02(p[0], p[1]);
       }
-      v = seg16_sum(v);
-      if (e == 0) s_cost[o] = v;
-      __syncthreads();
+      for (int d = 1; d < n; d <<= 1) v += __shfl_xor(v, d);  // n-lane segments (n divides 64)
+      if (oe < N_OFF * n && (oe & (n - 1)) == 0) s_cost[oe >> log2n] = v;
     }
-    // 5. the decision (the early exit reads only the centre) and the refined MVs
+    __syncthreads();
+    // 4. the decision and the refined MVs
     if (tid == 0) {
       int tdx, tdy;
       dmvr_decide(u, s_cost, &tdx, &tdy);
@@ -830,7 +831,13 @@ struct DevBuf {
   hipError_t ensure(size_t n, bool* fresh = nullptr) {
     if (fresh) *fresh = false;
     if (n <= cap && p) return hipSuccess;
-    if (p) (void)hipFree(p);
+    // Growing replaces a buffer that work still queued on any of the context's streams may use
+    // (the host runs pictures ahead of the GPU): drain the device first.  Buffers only grow, so
+    // this happens a few times per context.
+    if (p) {
+      (void)hipDeviceSynchronize();
+      (void)hipFree(p);
+    }
     p = nullptr;
     cap = 0;
     size_t want = std::max<size_t>(n, 1);
@@ -952,6 +959,7 @@ struct mm_ctx {
   bool dmvr = false;
   DevBuf<int> d_dmvr_mvd;
   DevBuf<BlockSetup> d_dmvr_setup;
+  DevBuf<mm_int2> d_dmvr_pos;  // both lists' reprojected positions per (sub-PU, offset, sub-block)
   // MM-MVP: the device copy of the epipole list (refreshed when its version moves, staged through a
   // pinned buffer on the context stream), the host-buffer API's query / result buffers and the
   // deferred status words (ping-pong: a call's block 0 zeroes the next call's word)
@@ -1194,6 +1202,7 @@ int mm_destroy(mm_ctx* c) {
   c->d_me_blocks.release();
   c->d_dmvr_mvd.release();
   c->d_dmvr_setup.release();
+  c->d_dmvr_pos.release();
   c->d_mvp_q.release();
   c->d_mvp_out.release();
   c->d_mvp_status.release();
@@ -1385,8 +1394,34 @@ static int take_pool_slot(mm_ctx* c, int* slot) {
 }
 
 static RefPool pool_of(const mm_ctx* c) {
-  const int cr_delta = c->geo.chroma ? (int)chroma_layout(c).bytes : 0;
-  return RefPool{c->pool, (uint32_t)((size_t)c->pool_cap * c->pic_bytes), cr_delta};
+  const PlaneLayout ly = luma_layout(c), lc = chroma_layout(c);
+  RefPool p{};
+  p.base = c->pool;
+  p.bytes = (uint32_t)((size_t)c->pool_cap * c->pic_bytes);
+  p.cr_delta = c->geo.chroma ? (int)lc.bytes : 0;
+  p.pic_bytes = (uint32_t)c->pic_bytes;
+  p.y0 = (uint32_t)(2 * ((size_t)ly.my * ly.stride + ly.mx));
+  p.cb0 = c->geo.chroma ? (uint32_t)(ly.bytes + 2 * ((size_t)lc.my * lc.stride + lc.mx)) : 0u;
+  p.stride_y = ly.stride;
+  p.stride_c = lc.stride;
+  return p;
+}
+
+// A picture's tables for the device: the pool and, per table slot, its pool slot (packed bytes;
+// stage_ref_table rebuilds the RefDev offsets from them), checked against the host offsets.
+static int device_tables(mm_ctx* c, PicTables* t) {
+  t->pool = pool_of(c);
+  for (int k = 0; k < MAX_SLOTS / 4; k++) t->pool_slot4[k] = 0u;
+  for (int s = 0; s < t->n_slots; s++) {
+    const RefDev& r = t->ref[s];
+    const uint32_t ps = (r.off_y - t->pool.y0) / t->pool.pic_bytes;
+    if (ps > 255u || ps * t->pool.pic_bytes + t->pool.y0 != r.off_y ||
+        (c->geo.chroma && ps * t->pool.pic_bytes + t->pool.cb0 != r.off_cb) || r.stride_y != t->pool.stride_y ||
+        (c->geo.chroma && r.stride_c != t->pool.stride_c))
+      return fail(c, MM_ERR_HIP, "reference outside the pool layout");
+    t->pool_slot4[s >> 2] |= ps << (8 * (s & 3));
+  }
+  return MM_OK;
 }
 
 // Reference slots of a picture: every resident reference, POC order, with its pool offsets
@@ -1482,6 +1517,7 @@ static int ensure_slot_buffers(mm_ctx* c, PlanSlot& S, int n, bool dmvr) {
     HIPCHK(c, S.dmvr_chunk.ensure((size_t)k.dmvr_elems / 64 + 1));
     HIPCHK(c, c->d_dmvr_setup.ensure((size_t)k.subs * N_OFF * 2));
     HIPCHK(c, c->d_dmvr_mvd.ensure(2 * (size_t)k.subs));
+    HIPCHK(c, c->d_dmvr_pos.ensure(2 * (size_t)k.dmvr_elems));
     S.dmvr_ensured = true;
   }
   bool fresh_jobs = false;
@@ -1549,8 +1585,11 @@ static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables
     }
     const int gd = (int)std::min<long>(DMVR_GRID, ((long)k.subs * N_OFF * 2 + 255) / 256 + 1);
     hipLaunchKernelGGL(k_dmvr_setup_dev, dim3(gd), dim3(256), 0, st, c->sc, S.meta.p, S.dmvr_sub.p, t, c->d_dmvr_setup.p);
+    const int gc = (int)std::min<long>(DMVR_GRID, ((long)k.dmvr_elems * 2 + 255) / 256 + 1);
+    hipLaunchKernelGGL(k_dmvr_reproj_dev, dim3(gc), dim3(256), 0, st, c->sc, S.meta.p, S.dmvr_sub.p, S.dmvr_off.p,
+                       S.dmvr_chunk.p, c->d_dmvr_setup.p, make_cache(c), c->d_dmvr_pos.p);
     hipLaunchKernelGGL(k_dmvr_search_dev, dim3(std::max(1, std::min(DMVR_SEARCH_GRID, k.subs))), dim3(DMVR_SEARCH_WG),
-                       0, st, c->sc, geo, S.meta.p, S.dmvr_sub.p, c->d_dmvr_setup.p, make_cache(c), t, S.jobs.p,
+                       0, st, geo, S.meta.p, S.dmvr_sub.p, c->d_dmvr_pos.p, t, S.jobs.p,
                        want_mvd ? c->d_dmvr_mvd.p : nullptr);
   }
   if (back && KERNEL_EVENTS) {  // plan-ahead: ev_plan completes with k_setup_dev
@@ -1613,7 +1652,7 @@ static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, in
   std::string err;
   int rc = build_pic_tables(seq_info(c->prm), c->epipoles, cur_poc, refs, &t, &err);
   if (rc) return fail(c, rc, err);
-  t.pool = pool_of(c);
+  RCCHK(device_tables(c, &t));
   t.only_list = only_list;
   t.dmvr = dmvr ? 1 : 0;
   Geometry geo = c->geo;
@@ -1825,7 +1864,7 @@ int mm_sad_window(mm_ctx* c, int cur_poc, const mm_me_block* blocks, int n, int 
   std::string err;
   int rc = build_pic_tables(seq_info(c->prm), c->epipoles, cur_poc, refs, &t, &err);
   if (rc) return fail(c, rc, err);
-  t.pool = pool_of(c);
+  RCCHK(device_tables(c, &t));
   MeWindow w;
   w.range = range;
   w.step = step;

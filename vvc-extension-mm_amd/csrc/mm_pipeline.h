@@ -4,6 +4,7 @@
 // used by the CPU test suite (tests/native/host_twin.cpp) loops over the same bodies, so the
 // device logic is exercised bit-for-bit on the host before it ever reaches a GPU.
 #pragma once
+#include <cstddef>
 #include "mm_filter.h"
 #include "mm_models.h"
 
@@ -208,6 +209,51 @@ MM_HD int find_item(const int* offsets, const int* chunk_start, int g, int n_ite
 }
 
 #if defined(__HIP__)
+// Kernel arguments are read with uniform (scalar) loads only.  Per-lane (vector) loads of kernel-
+// argument memory returned stale words on MI355X when launches were queued back to back -- the
+// MM-DMVR search's per-lane copy of PicTables::ref faulted on another launch's words
+// (profiles/r04_kernarg_fault.txt) -- so a table a kernel indexes per lane is copied into LDS by
+// wave 0: lane k of each 64-word chunk selects word k among the chunk's scalar loads.  The caller
+// synchronises the workgroup before reading `lds`.
+template <int NW>
+__device__ __forceinline__ void stage_arg_words(const uint32_t* arg, uint32_t* lds) {
+  if (threadIdx.x >= 64) return;
+  const int lane = threadIdx.x;
+#pragma unroll
+  for (int c = 0; c < NW; c += 64) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int k = 0; k < 64; k++) {
+      if (c + k < NW) {
+        const uint32_t w = arg[c + k];  // uniform address: a scalar load
+        v = lane == k ? w : v;
+      }
+    }
+    if (c + lane < NW) lds[c + lane] = v;
+  }
+}
+// The device fields of a picture's reference table (RefDev stride_y, stride_c, off_y, off_cb; the
+// host plane pointers are not used on the device) for NS slots, rebuilt in LDS from the packed
+// pool-slot numbers and the pool's uniform layout: four scalar loads, a few VALU ops in lanes 0..NS-1.
+template <int NS>
+__device__ __forceinline__ void stage_ref_table(const uint32_t* pool_slot4, const RefPool& pool, RefDev* lds) {
+  static_assert(NS % 4 == 0 && NS <= 64, "four slots per packed word");
+  if (threadIdx.x >= NS) return;
+  const int lane = threadIdx.x;
+  uint32_t w = 0;
+#pragma unroll
+  for (int k = 0; k < NS / 4; k++) {
+    const uint32_t v = pool_slot4[k];  // uniform address: a scalar load
+    w = (lane >> 2) == k ? v : w;
+  }
+  const uint32_t ps = (w >> (8 * (lane & 3))) & 255u;
+  RefDev& r = lds[lane];
+  r.stride_y = pool.stride_y;
+  r.stride_c = pool.stride_c;
+  r.off_y = ps * pool.pic_bytes + pool.y0;
+  r.off_cb = ps * pool.pic_bytes + pool.cb0;
+}
+
 // The same lookup for a whole wavefront whose lanes hold g = g0 + lane (g0 % 64 == 0): one
 // uniform chunk_start load, one coalesced load of the next 64 item offsets, and a 6-step binary
 // search over them with cross-lane reads -- instead of a chain of dependent loads per lane.
@@ -384,7 +430,10 @@ MM_HD int16_t weighted_avg(int p0, int p1, int w0, int w1, int bd) {
 // V pass's offset is a multiple of 2^6, so its single shift equals the 14-bit shift followed by
 // this one; tests/test_filter_identity.py).  So bi and uni sub-blocks share one body and a wave may
 // hold both (k_mc's waves follow the picture's spatial order, not PU classes); a list no lane of
-// the wave uses is skipped as a whole.
+// the wave uses is skipped as a whole.  A sub-block whose window lies out of range is zero in the
+// reference at the precision the list is predicted at (InterPrediction.cpp:780-783): the 14-bit
+// intermediate for bi and HP, the final samples for uni -- so a uni one is filled with
+// -IF_INTERNAL_OFFS, which weighted_avg(., *, 8, 0) maps to 0 (tests/test_twin.py).
 // HP (mm_pred_list hp = 1): every sub-block uses one list and keeps its 14-bit prediction.
 // The 24 bytes of one sub-block's record, loaded by mc_rec_load (the positions of both lists
 // unconditionally: the arrays are zeroed at allocation, and a wave of the class-agnostic
@@ -436,6 +485,7 @@ MM_HD void mc_rec_impl(int g, const McIn& in, const Geometry& geo, const Taps& t
   // bi: (w0, w1) of the BCW index; uni: the list's prediction with weight 8 (see above)
   const int w1b = bcw_w1((meta.y >> 8) & 7);
   const int wa = bi ? 8 - w1b : 8, wb = bi ? w1b : 0;
+  const int16_t oor = (HP || bi) ? 0 : (int16_t)-IF_INTERNAL_OFFS;  // out-of-range fill (see above)
   if (geo.store & 1) {
     int16_t pl[2][16];
 #pragma unroll
@@ -446,7 +496,7 @@ MM_HD void mc_rec_impl(int g, const McIn& in, const Geometry& geo, const Taps& t
       const int xPos = fx >> 4, yPos = fy >> 4, xFrac = fx & 15, yFrac = fy & 15;
       const RefDev r = refs[slot[l]];
       if (sb_out_of_range(xPos, yPos, geo.W, geo.H, geo.maxCUw, geo.maxCUh, 4, 4)) {
-        for (int i = 0; i < 16; i++) pl[l][i] = 0;
+        for (int i = 0; i < 16; i++) pl[l][i] = oor;
 #if defined(__HIP_DEVICE_COMPILE__)
       } else if (geo.padded || window_interior<8, 4, 4>(xPos, yPos, geo.W, geo.H)) {
         predict_subblock_pool<8, 4, 4>(taps.pool, r.off_y, 0, r.stride_y, xPos, yPos, taps.packed->lh[xFrac][(xPos - 3) & 1],
@@ -484,7 +534,7 @@ MM_HD void mc_rec_impl(int g, const McIn& in, const Geometry& geo, const Taps& t
     const int xPos = fx >> 5, yPos = fy >> 5, xFrac = fx & 31, yFrac = fy & 31;
     const RefDev r = refs[slot[l]];
     if (sb_out_of_range(xPos, yPos, geo.Wc, geo.Hc, geo.maxCUwc, geo.maxCUhc, 2, 2)) {
-      for (int i = 0; i < 4; i++) pcb[l][i] = pcr[l][i] = 0;
+      for (int i = 0; i < 4; i++) pcb[l][i] = pcr[l][i] = oor;
 #if defined(__HIP_DEVICE_COMPILE__)
     } else if (geo.padded || window_interior<4, 2, 2>(xPos, yPos, geo.Wc, geo.Hc)) {
       const uint32_t* ht = taps.packed->ch[xFrac][(xPos - 1) & 1];
