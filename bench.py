@@ -287,6 +287,26 @@ def bench_pictures(args, cfg, params, rank, world, local, dist):
     return None
 
 
+def dmvr_record(args, cfg, params, share=0.3, steps=12, warmup=3):
+    """C3 with MM-DMVR beside the headline: the same rotating pictures with
+    `share` of the DMVR-eligible bi leaves flagged MM_PUF_DMVR (merge / mvRefine PUs), so that each
+    picture runs the centre costs, the survivors' 24-offset search and the refined prediction inside
+    its own launch sequence (mm_set_dmvr).  Timed like the headline (plan-ahead as set); the timed
+    outputs of every picture are checked against the oracle (its serial DMVR restatement)."""
+    a = argparse.Namespace(**vars(args))
+    a.dmvr_share, a.steps, a.warmup, a.kernel_steps = share, steps, warmup, 2
+    a.no_mvp, a.cpu_seconds, a.uniform_model, a.coherent_mv = True, 0.5, None, False
+    line = bench_pictures(a, cfg, params, 0, 1, 0, None)
+    cpu = line["cpu_baseline"] or {}
+    return {"workload": line["config"]["workload"], "share": share, "value": line["value"], "unit": "Mpixels/s",
+            "ms_per_picture": line["ms_per_step"], "steps": steps, "stages_ms": line["stages_ms"],
+            "bit_exact": line["bit_exact"], "mismatching_samples": line["mismatching_samples"],
+            "bit_exact_sample": f"the {min(a.pictures, steps)} timed pictures vs the oracle",
+            "cpu_all_cores_mpix_s": (cpu.get("all_cores") or {}).get("value"),
+            "note": "stages_ms.setup holds the DMVR kernels (setups, centre costs, survivors' positions and "
+                    "search) and k_setup_dev; not part of value"}
+
+
 def mvp_per_picture(ctx, cfg, n_pus, reps=10):
     """MM-MVP (mm_mvp_convert_device) beside the C3 number, outside its timed
     region: one conversion per PU and list (2 x PUs queries, the seeded query mix tiled), queries
@@ -671,6 +691,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-mvp", action="store_true", help="C3: skip the MM-MVP figure beside the line")
     ap.add_argument("--no-c5", action="store_true", help="C3: skip the C5 (encoder ME) sub-record beside the line")
+    ap.add_argument("--no-dmvr", action="store_true", help="C3: skip the MM-DMVR sub-record beside the line")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="length of the one-thread CPU baseline sample")
     ap.add_argument("--kernel-steps", type=int, default=8, help="extra steps timed per launch with HIP events")
     ap.add_argument("--lib", default=None, help="alternative build of libmm360.so (A/B experiments)")
@@ -720,6 +741,8 @@ def main():
     else:
         line = bench_pictures(args, cfg, params, rank, world, local, dist)
         if line is not None:
+            if args.config == "C3" and world == 1 and args.dmvr_share == 0 and not args.no_dmvr:
+                line["dmvr"] = dmvr_record(args, cfg, params)
             if args.config == "C3" and world == 1 and not args.no_c5:
                 line["c5"] = c5_record(args)
             print(json.dumps(line), flush=True)

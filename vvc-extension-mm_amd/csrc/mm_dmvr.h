@@ -11,9 +11,11 @@
 //   3. parabolic sub-pel refinement from the 5 costs around the best offset unless it lies on the
 //      window border (xDMVRSubPixelErrorSurface :2157-2175, xSubPelErrorSrfc :1996-2048);
 //   4. the sub-PU is predicted as a bi PU at merge0 + mvd / merge1 - mvd (all components, addAvg).
-// Steps 1-3 run here (k_dmvr_setup_dev, then k_dmvr_search_dev: one workgroup per sub-PU, all 25
-// offsets at once -- the early exit then only selects what the decision reads) inside the
-// picture's device-planned launch sequence: the planner (mm_devplan.h) places every sub-PU of an MM_PUF_DMVR PU as a bi PU
+// Steps 1-3 run here inside the picture's device-planned launch sequence (mm_kernels.hip): the
+// per-offset block setups, the centre cost of every sub-PU (k_dmvr_centre_dev; a sub-PU whose
+// centre ends the search keeps its merge MVs), then for the surviving sub-PUs only -- compacted
+// into a list -- the 24 other offsets' positions and the search (k_dmvr_reproj_dev,
+// k_dmvr_search_dev): the planner (mm_devplan.h) places every sub-PU of an MM_PUF_DMVR PU as a bi PU
 // with its reprojection jobs and a SubPuDev record pointing at them, the search runs on the
 // records, and the search writes the refined MVs into those jobs before k_setup reads them --
 // step 4 is then the ordinary setup / reprojection / interpolation of the picture.
@@ -72,19 +74,59 @@ MM_HD void dmvr_position(const SeqConst& sc, const SubPuDev& u, const BlockSetup
   reproject_element(sc, b, gx, gy, packet, mpa, px, py, vip, 0, fx, fy, pg);
 }
 
-// Item g of the picture's DMVR position array: (sub-PU si, offset o, sub-block e, list l) with
-// g = 2 * (u.elem_off + o * n + e) + l -- one reprojection per thread, k_reproj's footprint.
-MM_HD void dmvr_reproj_item(int g, int si, const SeqConst& sc, const SubPuDev* sp, const BlockSetup* setups,
-                            const MpaCache& cache, mm_int2* pos) {
-  const SubPuDev& u = sp[si];
-  const int local = (g >> 1) - u.elem_off, l = g & 1;
-  const int o = local / u.n, e = local - o * u.n;
-  int32_t fx, fy;
-  dmvr_position(sc, u, setups[dmvr_setup_index(si, o, l)], cache, e, &fx, &fy);
-  mm_int2 q;
-  q.x = fx;
-  q.y = fy;
-  pos[g] = q;
+// The 24 non-centre offsets (the centre is evaluated first, for every sub-PU): offset index o of
+// the k-th non-centre offset.
+MM_HD int dmvr_outer_offset(int k) { return k < N_OFF / 2 ? k : k + 1; }
+
+// Luma 4x4 sub-block e of list l at n_offs offsets (offset index offs(j) for the j-th): its
+// reprojected positions (1/16 pel), out(j, fx, fy).  The element's grid terms and the MV-independent head of its
+// model (motion_head: TAN's tangent-plane coordinates, GED's rotated spherical coordinates) are
+// computed once, the tail per offset: the same operations as dmvr_position per offset.
+template <class Offs, class Out>
+MM_HD void dmvr_positions_offsets(const SeqConst& sc, const SubPuDev& u, const BlockSetup* setups, int s, int l, int e,
+                                  const MpaCache& cache, Offs offs, int n_offs, Out out) {
+  const int col = e / u.rows, row = e - col * u.rows;
+  const float gx = (float)(u.x + 4 * col) + sc.off, gy = (float)(u.y + 4 * row) + sc.off;
+  const bool mpa = u.model >= MPA_FRONT_BACK && u.model <= MPA_TOP_BOTTOM;
+  float px = 0.0f, py = 0.0f;
+  bool vip = false;
+  if (mpa) {
+    mpa_lookup(cache, u.model, (u.x >> 2) + col, (u.y >> 2) + row, &px, &py, &vip);
+  }
+  const bool packet = packet_lane(e, u.n);
+  const Math m{packet};
+  const GridSphere pg = grid_point(cache, u.model, (u.x >> 2) + col, (u.y >> 2) + row, packet);
+  MotionHead h{};
+  bool have_head = false;
+  for (int j = 0; j < n_offs; j++) {
+    const BlockSetup& b = setups[dmvr_setup_index(s, offs(j), l)];
+    if (!have_head && !b.identity) {  // a zero-MV setup is the identity and carries no TAN terms
+      h = motion_head(sc, b, gx, gy, m, pg);
+      have_head = true;
+    }
+    float mx, my;
+    motion_tail(sc, b, h, gx, gy, m, mpa, px, py, vip, &mx, &my);
+    int32_t fx, fy;
+    reproject_finish(sc, gx, gy, mx, my, packet, 0, &fx, &fy);
+    out(j, fx, fy);
+  }
+}
+
+// Thread (survivor k, sub-block e, list l) of k_dmvr_reproj_dev: the positions of its 24 non-centre
+// offsets into the survivor's items surv_base[k] + 2 * (j * n + e) + l.
+MM_HD void dmvr_reproj_thread(int k, int e, int l, const int* surv_s, const int* surv_base, const SeqConst& sc,
+                              const SubPuDev* sp, const BlockSetup* setups, const MpaCache& cache, mm_int2* pos) {
+  const int s = surv_s[k];
+  const SubPuDev& u = sp[s];
+  if (e >= u.n) return;
+  mm_int2* dst = pos + surv_base[k] + 2 * e + l;
+  const int stride = 2 * u.n;
+  dmvr_positions_offsets(sc, u, setups, s, l, e, cache, dmvr_outer_offset, N_OFF - 1, [&](int j, int32_t fx, int32_t fy) {
+    mm_int2 q;
+    q.x = fx;
+    q.y = fy;
+    dst[(long)j * stride] = q;
+  });
 }
 
 // xDMVRCost's share of one 4x4 sub-block: SAD of its rows 0 and 2 (the sub-PU's even rows, RdCost
@@ -197,11 +239,27 @@ inline void dmvr_search_host(int s, const SeqConst& sc, const Geometry& geo, con
   const SubPuDev& u = sp[s];
   uint32_t cost[N_OFF];
   for (int i = 0; i < N_OFF; i++) cost[i] = 0;
+  // every offset's positions, as the device computes them (centre: dmvr_position; the 24 others:
+  // dmvr_positions_offsets, head once per element)
+  int32_t pos[N_OFF][16][2][2];
+  for (int e = 0; e < u.n; e++)
+    for (int l = 0; l < 2; l++) {
+      dmvr_position(sc, u, setups[dmvr_setup_index(s, N_OFF / 2, l)], cache, e, &pos[N_OFF / 2][e][l][0],
+                    &pos[N_OFF / 2][e][l][1]);
+      dmvr_positions_offsets(sc, u, setups, s, l, e, cache, dmvr_outer_offset, N_OFF - 1,
+                             [&](int j, int32_t fx, int32_t fy) {
+                               pos[dmvr_outer_offset(j)][e][l][0] = fx;
+                               pos[dmvr_outer_offset(j)][e][l][1] = fy;
+                             });
+    }
   auto eval = [&](int o) {
     uint32_t sum = 0;
     for (int e = 0; e < u.n; e++) {
       int32_t fx[2], fy[2];
-      for (int l = 0; l < 2; l++) dmvr_position(sc, u, setups[dmvr_setup_index(s, o, l)], cache, e, &fx[l], &fy[l]);
+      for (int l = 0; l < 2; l++) {
+        fx[l] = pos[o][e][l][0];
+        fy[l] = pos[o][e][l][1];
+      }
       int16_t p[2][16];
       for (int l = 0; l < 2; l++) {
         const int xPos = fx[l] >> 4, yPos = fy[l] >> 4, xFrac = fx[l] & 15, yFrac = fy[l] & 15;

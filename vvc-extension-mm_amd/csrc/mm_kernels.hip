@@ -514,6 +514,16 @@ __global__ void __launch_bounds__(256) k_me_sad(SeqConst sc, Geometry geo, MeWin
 using namespace mmdmvr;
 constexpr int DMVR_GRID = 2048;  // workgroups of 256 of the grid-stride setup kernel
 
+// The picture's DMVR survivors (sub-PUs whose centre cost does not end the search) and their items
+struct DmvrWork {
+  unsigned long long* count;  // (survivors << 32) | position items (k_dmvr_compact_dev)
+  uint32_t* ccost;            // centre cost (xDMVRCost at the merge MVs) per sub-PU
+  int* sitems;                // position items of sub-PU s: 2 x 24 x n if it survived, else 0
+  int* surv_s;                // sub-PU of survivor k
+  int* surv_base;             // first position item of survivor k
+  int* surv_chunk;            // survivor holding position item 64 c (wave_find_item hints)
+};
+
 // thread per (sub-PU, offset, list) setup
 __global__ void __launch_bounds__(256) k_dmvr_setup_dev(SeqConst sc, const PlanMeta* __restrict__ meta,
                                                         const SubPuDev* __restrict__ sp, const PicTables t,
@@ -526,76 +536,174 @@ __global__ void __launch_bounds__(256) k_dmvr_setup_dev(SeqConst sc, const PlanM
     dmvr_setup_thread(i, sc, sp, s_ged, out);
 }
 
-// thread per (sub-PU, offset, luma 4x4 sub-block, list): the reprojected position (mm_dmvr.h
-// dmvr_reproj_item), 8 bytes into the picture's DMVR position array.  One reprojection per thread
-// keeps this kernel at k_reproj's register footprint; the search below is load / LDS work.
-__global__ void __launch_bounds__(256) k_dmvr_reproj_dev(SeqConst sc, const PlanMeta* __restrict__ meta,
-                                                         const SubPuDev* __restrict__ sp, const int* __restrict__ off,
-                                                         const int* __restrict__ chunk,
+// The centre cost of every sub-PU (InterPrediction.cpp:2510-2525): one wave per sub-PU, lane
+// 2 e + l list l of luma 4x4 sub-block e -- its position at the merge MV and rows 0 and 2 of its
+// 14-bit prediction; the L0 lane takes its partner's L1 rows by shuffle for the SAD, summed over
+// the wave.  minCost = cost - cost/4 < dx*dy ends the search: the sub-PU keeps its merge MVs
+// (dmvr_apply with a zero delta).  Otherwise it needs 2 x 24 x n position items (sitems), which
+// k_dmvr_compact_dev turns into the survivor list.
+__global__ void __launch_bounds__(256) k_dmvr_centre_dev(SeqConst sc, Geometry geo, const PlanMeta* __restrict__ meta,
+                                                         const SubPuDev* __restrict__ sp,
                                                          const BlockSetup* __restrict__ setups, MpaCache cache,
-                                                         mm_int2* __restrict__ pos) {
-  const int n_elems = meta->n_dmvr_elems, n_sub = meta->n_sub;
-  const int lane = __lane_id();
-  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, n_waves = (gridDim.x * blockDim.x) >> 6;
-  // wave w: list w & 1 of the 64 elements from 64 * (w >> 1) (wave_find_item wants lane-consecutive
-  // elements)
-  for (int w = wave; w < 2 * ((n_elems + 63) >> 6); w += n_waves) {
-    const int e = (w >> 1) * 64 + lane;
-    const int si = wave_find_item(off, chunk, e, n_sub);
-    if (e < n_elems) dmvr_reproj_item(2 * e + (w & 1), si, sc, sp, setups, cache, pos);
+                                                         const PicTables t, DmvrWork w, JobDev* __restrict__ jobs,
+                                                         int32_t* __restrict__ mvd) {
+#if defined(__HIP_DEVICE_COMPILE__)  // device-only filter paths (mm_filter.h predict_rows02, PtrRows)
+  __shared__ PackedTaps s_taps;
+  __shared__ RefDev s_ref[MAX_SLOTS];  // indexed per lane: rebuilt from scalar loads (stage_ref_table)
+  const int tid = threadIdx.x;
+  if (tid < sizeof(PackedTaps) / 16)
+    reinterpret_cast<uint4*>(&s_taps)[tid] = reinterpret_cast<const uint4*>(&c_packed_taps)[tid];
+  stage_ref_table<MAX_SLOTS>(t.pool_slot4, t.pool, s_ref);
+  __syncthreads();
+  const int n_sub = meta->n_sub;
+  const RefPool pool = t.pool;
+  for (int base = blockIdx.x * 256; base < n_sub * 64; base += gridDim.x * 256) {  // uniform trip count
+    // one sub-PU per wave (its model and slots uniform: scalar loads of the record)
+    const int g = base + tid, s = __builtin_amdgcn_readfirstlane(g >> 6), e = (g >> 1) & 31, l = g & 1;
+    int16_t p[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    SubPuDev u;
+    if (s < n_sub) u = sp[s];
+    if (s < n_sub && e < u.n) {
+      int32_t fx, fy;
+      dmvr_position(sc, u, setups[dmvr_setup_index(s, N_OFF / 2, l)], cache, e, &fx, &fy);
+      const int xPos = fx >> 4, yPos = fy >> 4;
+      if (!sb_out_of_range(xPos, yPos, geo.W, geo.H, geo.maxCUw, geo.maxCUh, 4, 4)) {
+        const RefDev& r = s_ref[l ? u.slot[1] : u.slot[0]];
+        const int x0 = (xPos - 3) & ~1;
+        const PtrRows rows{pool.base + r.off_y + (long)((yPos - 3) * r.stride_y + x0) * 2, r.stride_y * 2};
+        predict_rows02(rows, s_taps.lh[fx & 15][(xPos - 3) & 1], s_taps.lv[fy & 15], geo.bd, p);
+      }
+    }
+    uint32_t v = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t mine = (uint32_t)(uint16_t)p[2 * j] | ((uint32_t)(uint16_t)p[2 * j + 1] << 16);
+      const uint32_t other = __shfl_xor(mine, 1);
+      v += (uint32_t)abs((int)(int16_t)(mine & 0xffffu) - (int)(int16_t)(other & 0xffffu)) +
+           (uint32_t)abs((int)(int16_t)(mine >> 16) - (int)(int16_t)(other >> 16));
+    }
+    v = l ? 0u : v;  // each pair counted once
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) v += __shfl_xor(v, d);
+    if (s < n_sub && (g & 63) == 0) {
+      w.ccost[s] = v;
+      const bool survives = v - (v >> 2) >= (uint32_t)(u.w * u.h);
+      w.sitems[s] = survives ? 2 * (N_OFF - 1) * u.n : 0;
+      if (!survives) dmvr_apply(s, u, 0, 0, jobs, mvd);  // notZeroCost = false: no refinement (:2520-2525)
+    }
   }
+#endif
 }
 
-// The search of one sub-PU per workgroup iteration (xProcessDMVRProjected, InterPrediction.cpp:
-// 2488-2580), from the positions k_dmvr_reproj_dev wrote:
-//   1. the 25 offsets x n luma 4x4 sub-blocks x 2 lists positions into LDS (one 8-byte load per
-//      item), and per list the bounding box of the in-range windows;
+// The survivor list in sub-PU order (one workgroup): an exclusive scan of sitems gives each
+// surviving sub-PU its item base and survivor index; count = (survivors << 32) | items.  (A single
+// atomic counter appended by the centre kernel serialised ~14 K device-scope atomics.)
+constexpr int DMVR_COMPACT_WG = 1024;
+__global__ void __launch_bounds__(DMVR_COMPACT_WG) k_dmvr_compact_dev(const PlanMeta* __restrict__ meta, DmvrWork w) {
+  __shared__ int s_items[DMVR_COMPACT_WG / 64], s_surv[DMVR_COMPACT_WG / 64];
+  const int n_sub = meta->n_sub, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int per = (n_sub + DMVR_COMPACT_WG - 1) / DMVR_COMPACT_WG;  // consecutive sub-PUs per thread
+  const int s0 = min(n_sub, tid * per), s1 = min(n_sub, s0 + per);
+  int items = 0, surv = 0;
+  for (int s = s0; s < s1; s++) {
+    const int it = w.sitems[s];
+    items += it;
+    surv += it ? 1 : 0;
+  }
+  // exclusive scan: inside the wave, then over the waves
+  int ie = items, se = surv;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int a = __shfl_up(ie, d), b = __shfl_up(se, d);
+    if (lane >= d) {
+      ie += a;
+      se += b;
+    }
+  }
+  if (lane == 63) {
+    s_items[wave] = ie;
+    s_surv[wave] = se;
+  }
+  __syncthreads();
+  int ib = ie - items, kb = se - surv;
+  for (int v = 0; v < wave; v++) {
+    ib += s_items[v];
+    kb += s_surv[v];
+  }
+  for (int s = s0; s < s1; s++) {
+    const int it = w.sitems[s];
+    if (!it) continue;
+    w.surv_s[kb] = s;
+    w.surv_base[kb] = ib;
+    write_chunks(w.surv_chunk, kb, ib, it);
+    ib += it;
+    kb++;
+  }
+  if (tid == DMVR_COMPACT_WG - 1) *w.count = ((unsigned long long)kb << 32) | (unsigned long long)(unsigned)ib;
+}
+
+// thread per (survivor, luma 4x4 sub-block, list), 32 per survivor (mm_dmvr.h dmvr_reproj_thread):
+// the positions of its 24 non-centre offsets -- the element's grid terms and its model's
+// MV-independent head once, the tail per offset -- 8 bytes each into the survivor's items.
+__global__ void __launch_bounds__(256) k_dmvr_reproj_dev(SeqConst sc, const SubPuDev* __restrict__ sp,
+                                                         const BlockSetup* __restrict__ setups, MpaCache cache,
+                                                         DmvrWork w, mm_int2* __restrict__ pos) {
+  const int n_surv = (int)(*w.count >> 32);
+  for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < n_surv * 32; g += gridDim.x * blockDim.x)
+    dmvr_reproj_thread(g >> 5, (g >> 1) & 15, g & 1, w.surv_s, w.surv_base, sc, sp, setups, cache, pos);
+}
+
+// The search of one surviving sub-PU per workgroup iteration (xProcessDMVRProjected,
+// InterPrediction.cpp:2526-2580), from the positions k_dmvr_reproj_dev wrote:
+//   1. the 24 non-centre offsets x n luma 4x4 sub-blocks x 2 lists positions into LDS (one 8-byte
+//      load per item), and per list the bounding box of the in-range windows;
 //   2. the union of every offset's luma window, per list, staged once into LDS (16-byte loads): the
-//      25 x n windows of a list lie within about (dx + 11) x (dy + 11) samples, so each staged
+//      24 x n windows of a list lie within about (dx + 11) x (dy + 11) samples, so each staged
 //      sample serves ~50 window reads that would otherwise each be a global load; a union larger
 //      than the LDS window (strong warping, the ERP seam) reads the pool directly instead;
 //   3. rows 0 and 2 of both 14-bit predictions per (offset, sub-block) and their SAD, summed per
 //      offset over its n sub-blocks (xor shuffles inside the n-lane segment);
-//   4. the decision (early exit on the centre cost, first strict minimum, error surface) and the
-//      refined MVs into the sub-PU's jobs.
-// All 25 costs are evaluated even when the centre ends the search (the decision then reads the
-// centre only).  Costs never leave the workgroup.
+//   4. the decision (the centre cost from k_dmvr_centre_dev, first strict minimum, error surface)
+//      and the refined MVs into the sub-PU's jobs.
+// Costs never leave the workgroup.
 constexpr int DMVR_SEARCH_WG = 256;
-constexpr int DMVR_SEARCH_GRID = 2048;  // 8 workgroups per CU, grid-stride over the sub-PUs
-[[maybe_unused]] constexpr int DMVR_MAX_ITEMS = N_OFF * 16 * 2;  // (offset, sub-block, list) items of a 16x16 sub-PU
+constexpr int DMVR_SEARCH_GRID = 2048;  // 8 workgroups per CU, grid-stride over the survivors
+[[maybe_unused]] constexpr int DMVR_MAX_ITEMS = (N_OFF - 1) * 16 * 2;  // position items of a 16x16 sub-PU
 constexpr int DMVR_WIN_W = 64;                   // staged union window per list: samples x rows
 [[maybe_unused]] constexpr int DMVR_WIN_H = 48;
 [[maybe_unused]] constexpr int DMVR_WIN_STRIDE = DMVR_WIN_W / 2 + 1;  // dwords per LDS row: odd, so rows start on different banks
 
-__global__ void __launch_bounds__(DMVR_SEARCH_WG) k_dmvr_search_dev(Geometry geo, const PlanMeta* __restrict__ meta,
-                                                                   const SubPuDev* __restrict__ sp,
+__global__ void __launch_bounds__(DMVR_SEARCH_WG) k_dmvr_search_dev(Geometry geo, const SubPuDev* __restrict__ sp,
                                                                    const mm_int2* __restrict__ pos, const PicTables t,
-                                                                   JobDev* __restrict__ jobs, int32_t* __restrict__ mvd) {
+                                                                   DmvrWork w, JobDev* __restrict__ jobs,
+                                                                   int32_t* __restrict__ mvd) {
 #if defined(__HIP_DEVICE_COMPILE__)  // device-only filter paths (mm_filter.h predict_rows02, PtrRows, LdsRows)
   __shared__ PackedTaps s_taps;
   __shared__ uint32_t s_win[2][DMVR_WIN_H * DMVR_WIN_STRIDE];
-  __shared__ mm_int2 s_pos[DMVR_MAX_ITEMS];  // item 2 * (o * n + e) + l
+  __shared__ mm_int2 s_pos[DMVR_MAX_ITEMS];  // item 2 * (j * n + e) + l
   __shared__ int s_box[2][4];                // per list: min / max of the in-range xPos, yPos
   __shared__ uint32_t s_cost[N_OFF];
   const int tid = threadIdx.x, lane = tid & 63;
   static_assert(sizeof(PackedTaps) % 16 == 0 && sizeof(PackedTaps) / 16 <= DMVR_SEARCH_WG, "one 16-byte word per thread");
   if (tid < sizeof(PackedTaps) / 16)
     reinterpret_cast<uint4*>(&s_taps)[tid] = reinterpret_cast<const uint4*>(&c_packed_taps)[tid];
-  const int n_sub = meta->n_sub;
+  const int n_surv = (int)(*w.count >> 32);
   const RefPool pool = t.pool;
   // items alternate lists and the stride is even, so every item of a thread has the list tid & 1
-  for (int s = blockIdx.x; s < n_sub; s += gridDim.x) {
+  for (int k = blockIdx.x; k < n_surv; k += gridDim.x) {
+    const int s = w.surv_s[k];
     const SubPuDev u = sp[s];
-    const int n = u.n, n_items = 2 * N_OFF * n, log2n = 31 - __clz(n);  // n: 8 or 16
+    const int n = u.n, n_items = 2 * (N_OFF - 1) * n, log2n = 31 - __clz(n);  // n: 8 or 16
     // the sub-PU's slots are uniform: scalar loads of the kernel argument's table
     const int slot0 = __builtin_amdgcn_readfirstlane(u.slot[0]), slot1 = __builtin_amdgcn_readfirstlane(u.slot[1]);
     const uint32_t off_y[2] = {t.ref[slot0].off_y, t.ref[slot1].off_y};
     const int stride_y[2] = {t.ref[slot0].stride_y, t.ref[slot1].stride_y};
     if (tid < 8) (&s_box[0][0])[tid] = (tid & 1) ? INT_MIN : INT_MAX;
+    if (tid == 0) s_cost[N_OFF / 2] = w.ccost[s];
     __syncthreads();  // s_taps staged; the previous sub-PU's LDS reads and decision are done
     // 1. positions of the (offset, sub-block, list) items and the in-range box of this thread's list
     int xmin = INT_MAX, xmax = INT_MIN, ymin = INT_MAX, ymax = INT_MIN;
-    const mm_int2* src_pos = pos + 2 * (long)u.elem_off;
+    const mm_int2* src_pos = pos + w.surv_base[k];
     for (int i = tid; i < n_items; i += DMVR_SEARCH_WG) {
       const mm_int2 q = src_pos[i];
       s_pos[i] = q;
@@ -648,10 +756,10 @@ __global__ void __launch_bounds__(DMVR_SEARCH_WG) k_dmvr_search_dev(Geometry geo
     __syncthreads();
     // 3. rows 0 and 2 of both predictions per (offset, sub-block), SAD per offset
 #pragma unroll 1
-    for (int base = 0; base < N_OFF * 16; base += DMVR_SEARCH_WG) {  // uniform trip count (shuffles below)
+    for (int base = 0; base < (N_OFF - 1) * 16; base += DMVR_SEARCH_WG) {  // uniform trip count (shuffles below)
       const int oe = base + tid;
       uint32_t v = 0;
-      if (oe < N_OFF * n) {
+      if (oe < (N_OFF - 1) * n) {
         int16_t p[2][8];
 #pragma unroll
         for (int l = 0; l < 2; l++) {
@@ -674,7 +782,7 @@ __global__ void __launch_bounds__(DMVR_SEARCH_WG) k_dmvr_search_dev(Geometry geo
         v = dmvr_sad_rows02(p[0], p[1]);
       }
       for (int d = 1; d < n; d <<= 1) v += __shfl_xor(v, d);  // n-lane segments (n divides 64)
-      if (oe < N_OFF * n && (oe & (n - 1)) == 0) s_cost[oe >> log2n] = v;
+      if (oe < (N_OFF - 1) * n && (oe & (n - 1)) == 0) s_cost[dmvr_outer_offset(oe >> log2n)] = v;
     }
     __syncthreads();
     // 4. the decision and the refined MVs
@@ -959,7 +1067,10 @@ struct mm_ctx {
   bool dmvr = false;
   DevBuf<int> d_dmvr_mvd;
   DevBuf<BlockSetup> d_dmvr_setup;
-  DevBuf<mm_int2> d_dmvr_pos;  // both lists' reprojected positions per (sub-PU, offset, sub-block)
+  DevBuf<mm_int2> d_dmvr_pos;  // both lists' reprojected positions per (survivor, offset, sub-block)
+  DevBuf<unsigned long long> d_dmvr_count;  // DmvrWork (k_dmvr_centre_dev's survivor list)
+  DevBuf<uint32_t> d_dmvr_ccost;
+  DevBuf<int> d_dmvr_sitems, d_dmvr_surv_s, d_dmvr_surv_base, d_dmvr_surv_chunk;
   // MM-MVP: the device copy of the epipole list (refreshed when its version moves, staged through a
   // pinned buffer on the context stream), the host-buffer API's query / result buffers and the
   // deferred status words (ping-pong: a call's block 0 zeroes the next call's word)
@@ -1203,6 +1314,12 @@ int mm_destroy(mm_ctx* c) {
   c->d_dmvr_mvd.release();
   c->d_dmvr_setup.release();
   c->d_dmvr_pos.release();
+  c->d_dmvr_count.release();
+  c->d_dmvr_ccost.release();
+  c->d_dmvr_sitems.release();
+  c->d_dmvr_surv_s.release();
+  c->d_dmvr_surv_base.release();
+  c->d_dmvr_surv_chunk.release();
   c->d_mvp_q.release();
   c->d_mvp_out.release();
   c->d_mvp_status.release();
@@ -1518,6 +1635,12 @@ static int ensure_slot_buffers(mm_ctx* c, PlanSlot& S, int n, bool dmvr) {
     HIPCHK(c, c->d_dmvr_setup.ensure((size_t)k.subs * N_OFF * 2));
     HIPCHK(c, c->d_dmvr_mvd.ensure(2 * (size_t)k.subs));
     HIPCHK(c, c->d_dmvr_pos.ensure(2 * (size_t)k.dmvr_elems));
+    HIPCHK(c, c->d_dmvr_count.ensure(1));
+    HIPCHK(c, c->d_dmvr_ccost.ensure(k.subs));
+    HIPCHK(c, c->d_dmvr_sitems.ensure(k.subs));
+    HIPCHK(c, c->d_dmvr_surv_s.ensure(k.subs));
+    HIPCHK(c, c->d_dmvr_surv_base.ensure(k.subs));
+    HIPCHK(c, c->d_dmvr_surv_chunk.ensure(2 * (size_t)k.dmvr_elems / 64 + 1));
     S.dmvr_ensured = true;
   }
   bool fresh_jobs = false;
@@ -1584,13 +1707,19 @@ static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables
       back = false;
     }
     const int gd = (int)std::min<long>(DMVR_GRID, ((long)k.subs * N_OFF * 2 + 255) / 256 + 1);
+    const DmvrWork dw{c->d_dmvr_count.p, c->d_dmvr_ccost.p, c->d_dmvr_sitems.p, c->d_dmvr_surv_s.p,
+                      c->d_dmvr_surv_base.p, c->d_dmvr_surv_chunk.p};
+    int32_t* mvd = want_mvd ? c->d_dmvr_mvd.p : nullptr;
     hipLaunchKernelGGL(k_dmvr_setup_dev, dim3(gd), dim3(256), 0, st, c->sc, S.meta.p, S.dmvr_sub.p, t, c->d_dmvr_setup.p);
-    const int gc = (int)std::min<long>(DMVR_GRID, ((long)k.dmvr_elems * 2 + 255) / 256 + 1);
-    hipLaunchKernelGGL(k_dmvr_reproj_dev, dim3(gc), dim3(256), 0, st, c->sc, S.meta.p, S.dmvr_sub.p, S.dmvr_off.p,
-                       S.dmvr_chunk.p, c->d_dmvr_setup.p, make_cache(c), c->d_dmvr_pos.p);
+    const int gcen = (int)std::min<long>(DMVR_GRID, ((long)k.subs * 64 + 255) / 256);
+    hipLaunchKernelGGL(k_dmvr_centre_dev, dim3(std::max(1, gcen)), dim3(256), 0, st, c->sc, geo, S.meta.p, S.dmvr_sub.p,
+                       c->d_dmvr_setup.p, make_cache(c), t, dw, S.jobs.p, mvd);
+    hipLaunchKernelGGL(k_dmvr_compact_dev, dim3(1), dim3(DMVR_COMPACT_WG), 0, st, S.meta.p, dw);
+    const int gc = (int)std::min<long>(DMVR_GRID, ((long)k.subs * 32 + 255) / 256);
+    hipLaunchKernelGGL(k_dmvr_reproj_dev, dim3(gc), dim3(256), 0, st, c->sc, S.dmvr_sub.p, c->d_dmvr_setup.p,
+                       make_cache(c), dw, c->d_dmvr_pos.p);
     hipLaunchKernelGGL(k_dmvr_search_dev, dim3(std::max(1, std::min(DMVR_SEARCH_GRID, k.subs))), dim3(DMVR_SEARCH_WG),
-                       0, st, geo, S.meta.p, S.dmvr_sub.p, c->d_dmvr_pos.p, t, S.jobs.p,
-                       want_mvd ? c->d_dmvr_mvd.p : nullptr);
+                       0, st, geo, S.dmvr_sub.p, c->d_dmvr_pos.p, t, dw, S.jobs.p, mvd);
   }
   if (back && KERNEL_EVENTS) {  // plan-ahead: ev_plan completes with k_setup_dev
     hipExtLaunchKernelGGL(k_setup_dev, dim3(gs), dim3(256), 0, st, nullptr, c->ev_plan, 0, c->sc, S.meta.p, S.jobs.p, t,

@@ -384,10 +384,50 @@ MM_HD void tan_grid_entry(V3 p, Math m, float* alpha, float* se, float* ce) {
   *se = m.sin(eps);
   *ce = m.cos(eps);
 }
-MM_HD void model_motion_element(const SeqConst& s, const BlockSetup& b, float gx, float gy, bool packet,
-                                bool mpa_cached, float pers_x, float pers_y, bool pers_vip, float* omx, float* omy,
-                                GridSphere grid = no_grid()) {
-  const Math m{packet};
+// model_motion_element in two parts.  The head is what does not depend on the block's MV: the
+// element's sphere point and, for TAN, the tangent-plane coordinates (xP, yP) of the element about the
+// block centre (the setup's sE, cE, alphaC come from the centre only), for GED the spherical
+// coordinates of the rotated point (the setup's rotation M is the epipole's or the axis', whatever
+// the MV).  A block searched over many MVs (MM-DMVR's offsets) computes the head once per element and
+// the tail per MV; model_motion_element is head + tail, so both give the same bits.  The head needs
+// a setup that is not the zero-MV identity (TAN leaves sE, cE, alphaC unset there).
+struct MotionHead {
+  V3 p;           // toSphere(grid) of TAN / 3DT / ROT / GED
+  V3 ged_sp;      // GED: cart_to_sph(M p)
+  float xP, yP;   // TAN: tangent-plane coordinates
+  float se, ce;   // TAN: the element's sin / cos of its elevation complement
+};
+MM_HD MotionHead motion_head(const SeqConst& s, const BlockSetup& b, float gx, float gy, const Math& m,
+                             const GridSphere& grid) {
+  MotionHead h;
+  h.p = {0.0f, 0.0f, 0.0f};
+  h.ged_sp = {0.0f, 0.0f, 0.0f};
+  h.xP = h.yP = h.se = h.ce = 0.0f;
+  const bool mpa = b.model >= MPA_FRONT_BACK && b.model <= MPA_TOP_BOTTOM;
+  if (b.model == CLASSIC || b.identity || b.model >= NUM_MODELS || mpa) return h;
+  if (!grid.tan_valid) h.p = grid.valid ? grid.p : erp_to_sphere(gx, gy, s, m);
+  if (b.model == TANGENTIAL) {  // TangentialMotionModel.cpp:8-48, up to the MV
+    float alpha;
+    if (grid.tan_valid) {
+      alpha = grid.alpha;
+      h.se = grid.se;
+      h.ce = grid.ce;
+    } else {
+      tan_grid_entry(h.p, m, &alpha, &h.se, &h.ce);
+    }
+    const float sE = tan_sE(b), cE = tan_cE(b), alphaC = tan_alphaC(b);
+    float dA = alpha - alphaC;
+    float cdA = m.cos(dA);
+    float cosPsi = sE * h.se + (cE * h.ce) * cdA;
+    h.yP = (h.se * cE - (sE * h.ce) * cdA) / cosPsi;
+    h.xP = (m.sin(dA) * h.ce) / cosPsi;
+  } else if (b.model >= GEODESIC_X) {  // GeodesicMotionModel.cpp:101-176, up to the MV
+    h.ged_sp = cart_to_sph(mat_vec(b.M, h.p), m, true);
+  }
+  return h;
+}
+MM_HD void motion_tail(const SeqConst& s, const BlockSetup& b, const MotionHead& h, float gx, float gy, const Math& m,
+                       bool mpa_cached, float pers_x, float pers_y, bool pers_vip, float* omx, float* omy) {
   if (b.model == CLASSIC) {
     *omx = gx + b.mvx;
     *omy = gy + b.mvy;
@@ -400,9 +440,6 @@ MM_HD void model_motion_element(const SeqConst& s, const BlockSetup& b, float gx
   }
   // Every model ends in EquirectangularProjection::fromSphere of a moved sphere point q; the
   // switch computes q and the shared tail projects it (one copy of the acosf/atan2f code).
-  const bool mpa = b.model >= MPA_FRONT_BACK && b.model <= MPA_TOP_BOTTOM;
-  V3 p = {0.0f, 0.0f, 0.0f};  // toSphere(grid) of TAN / 3DT / ROT / GED
-  if (!mpa && !grid.tan_valid) p = grid.valid ? grid.p : erp_to_sphere(gx, gy, s, m);
   V3 q;
   switch (b.model) {
     case MPA_FRONT_BACK:
@@ -429,23 +466,10 @@ MM_HD void model_motion_element(const SeqConst& s, const BlockSetup& b, float gx
       else
         q = {c.z, c.y, -c.x};
     } break;
-    case TANGENTIAL: {  // TangentialMotionModel.cpp:8-48
-      float alpha, se, ce;
-      if (grid.tan_valid) {
-        alpha = grid.alpha;
-        se = grid.se;
-        ce = grid.ce;
-      } else {
-        tan_grid_entry(p, m, &alpha, &se, &ce);
-      }
+    case TANGENTIAL: {  // TangentialMotionModel.cpp:8-48, from the MV on
       const float sE = tan_sE(b), cE = tan_cE(b), alphaC = tan_alphaC(b);
-      float dA = alpha - alphaC;
-      float cdA = m.cos(dA);
-      float cosPsi = sE * se + (cE * ce) * cdA;
-      float yP = (se * cE - (sE * ce) * cdA) / cosPsi;
-      float xP = (m.sin(dA) * ce) / cosPsi;
-      float yM = yP - b.mvy * s.res;
-      float xM = xP - b.mvx * s.res;
+      float yM = h.yP - b.mvy * s.res;
+      float xM = h.xP - b.mvx * s.res;
       float rho = m.sqrt(xM * xM + yM * yM);
       float eta = g_atanf(rho);
       float gamma = (rho * cE) * m.cos(eta) - (yM * sE) * m.sin(eta);
@@ -454,14 +478,13 @@ MM_HD void model_motion_element(const SeqConst& s, const BlockSetup& b, float gx
       q = sph_to_cart(1.0f, PI_2_F - epsM, alphaM, m);
     } break;
     case THREE_D_TRANSLATIONAL:  // ThreeDTranslationalMotionModel.cpp:7-24
-      q = {p.x + b.M.m[0], p.y + b.M.m[1], p.z + b.M.m[2]};  // 3D motion vector
+      q = {h.p.x + b.M.m[0], h.p.y + b.M.m[1], h.p.z + b.M.m[2]};  // 3D motion vector
       break;
     case ROTATIONAL:  // RotationalMotionModel.cpp:66-77
-      q = mat_vec(b.M, p);
+      q = mat_vec(b.M, h.p);
       break;
-    default: {  // GEODESIC_X/Y/Z/CAMPOSE, GeodesicMotionModel.cpp:101-176
-      V3 r = mat_vec(b.M, p);
-      V3 sp = cart_to_sph(r, m, true);
+    default: {  // GEODESIC_X/Y/Z/CAMPOSE, GeodesicMotionModel.cpp:101-176, from the MV on
+      const V3 sp = h.ged_sp;
       float th;
       if (s.ged_flavor == 1)
         th = sp.y + g_atanf(g_sinf(sp.y) / (b.k - g_cosf(sp.y)));
@@ -474,13 +497,26 @@ MM_HD void model_motion_element(const SeqConst& s, const BlockSetup& b, float gx
   }
   erp_from_sphere(q, s, m, true, omx, omy);
 }
+MM_HD void model_motion_element(const SeqConst& s, const BlockSetup& b, float gx, float gy, bool packet,
+                                bool mpa_cached, float pers_x, float pers_y, bool pers_vip, float* omx, float* omy,
+                                GridSphere grid = no_grid()) {
+  const Math m{packet};
+  motion_tail(s, b, motion_head(s, b, gx, gy, m, grid), gx, gy, m, mpa_cached, pers_x, pers_y, pers_vip, omx, omy);
+}
+
+// NaN -> unmoved (MVReprojection.cpp:151-154), remove offset, rescale, round to fixed point
+MM_HD void reproject_finish(const SeqConst& s, float gx, float gy, float mx, float my, bool packet, int chroma_shift,
+                            int32_t* fx, int32_t* fy);
 
 MM_HD void reproject_element(const SeqConst& s, const BlockSetup& b, float gx, float gy, bool packet,
                              bool mpa_cached, float pers_x, float pers_y, bool pers_vip,
                              int chroma_shift, int32_t* fx, int32_t* fy, GridSphere grid = no_grid()) {
   float mx, my;
   model_motion_element(s, b, gx, gy, packet, mpa_cached, pers_x, pers_y, pers_vip, &mx, &my, grid);
-  // NaN -> unmoved (MVReprojection.cpp:151-154), remove offset, rescale, round to fixed point
+  reproject_finish(s, gx, gy, mx, my, packet, chroma_shift, fx, fy);
+}
+MM_HD void reproject_finish(const SeqConst& s, float gx, float gy, float mx, float my, bool packet, int chroma_shift,
+                            int32_t* fx, int32_t* fy) {
   if (isnanf_(mx) || isnanf_(my)) {
     mx = gx;
     my = gy;
