@@ -51,16 +51,18 @@ RED_DEVICE = ["cuda"]  # where the timing reductions run: "cpu" under the gloo r
 
 def measured_traffic(args, config):
     """HBM bytes per k_mc_dev launch from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes
-    (profiles/r03_traffic.json, tools/traffic_json.py), only when that profile was taken with
+    (profiles/r0N_traffic.json, tools/traffic_json.py), only when that profile was taken with
     this very library (sha256) and the same workload; else None."""
+    import glob
     import hashlib
-    path = os.path.join(ROOT, "profiles", "r03_traffic.json")
-    if config != "C3" or args.uniform_model is not None or args.coherent_mv or not os.path.exists(path):
+    if config != "C3" or args.uniform_model is not None or args.coherent_mv or args.dmvr_share > 0:
         return None
-    d = json.load(open(path))
     sha = hashlib.sha256(open(mm360.LIB_PATH, "rb").read()).hexdigest()
-    ok = d.get("lib_sha256") == sha and d.get("pictures") == args.pictures
-    return d["traffic_bytes_per_launch"] if ok else None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")), reverse=True):
+        d = json.load(open(path))
+        if d.get("lib_sha256") == sha and d.get("pictures") == args.pictures:
+            return d["traffic_bytes_per_launch"]
+    return None
 
 
 def host_info(threads):
@@ -342,11 +344,14 @@ def mvp_per_picture(ctx, cfg, n_pus, reps=10):
 
 
 def mvp_in_loop(args, ctx, cfg, pictures, d_pus, outs, area):
-    """C3 with MM-MVP in the decode loop: picture t+1's conversions (one per PU and list, one
-    batch) run on their own stream (mm_set_mvp_stream) while picture t is predicted on the context
-    stream, and picture t's prediction -- planning included, so plan-ahead is off here -- waits for
-    its own conversions (an event): a decoder that derives the next picture's MVs while the
-    current one is motion-compensated.  Also the latency of one CTU row's and one CTU's batch
+    """C3 with MM-MVP in the decode loop: a picture's conversions (one per PU and list, one batch)
+    run on their own stream (mm_set_mvp_stream), two pictures ahead, while earlier pictures are
+    predicted on the context stream; a picture's PU list depends on its conversions, so before its
+    prediction call is issued the host waits for them (the plan-ahead contract: a call's list is
+    complete when the call is issued; the conversions finished during the previous picture, so the
+    wait returns at once): a decoder that derives the next pictures' MVs while the current one is
+    motion-compensated.  With plan-ahead off, the prediction waits for its conversions on the
+    device instead (an event) and they run one picture ahead.  Also the latency of one CTU row's and one CTU's batch
     (merge lists that chain, UnitTools.cpp:2269-2302, convert in dependent batches): device time of
     the call and host wall time of the synchronous host-buffer call."""
     P_ = len(pictures)
@@ -355,7 +360,8 @@ def mvp_in_loop(args, ctx, cfg, pictures, d_pus, outs, area):
     d_q = [mm360.queries_to_device(q) for q in qs]
     d_o = [torch.zeros((len(q), 2), dtype=torch.int32, device="cuda") for q in qs]
     side = torch.cuda.Stream()
-    ctx.set_plan_ahead(False)
+    ahead = 2 if args.plan_ahead else 1
+    ctx.set_plan_ahead(bool(args.plan_ahead))
     ctx.set_call_timing(False)
     ctx.set_mvp_stream(side.cuda_stream)
     ready = [torch.cuda.Event() for _ in range(P_)]
@@ -368,9 +374,13 @@ def mvp_in_loop(args, ctx, cfg, pictures, d_pus, outs, area):
     def step(s):
         f = s % P_
         if s == 0:
-            convert(0)
-        convert((s + 1) % P_)  # the next picture's MV derivation, overlapping this picture's MC
-        main.wait_event(ready[f])
+            for a in range(ahead):
+                convert(a)
+        convert((s + ahead) % P_)  # a later picture's MV derivation, overlapping this picture's MC
+        if args.plan_ahead:
+            ready[f].synchronize()  # the list of call s is complete when the call is issued
+        else:
+            main.wait_event(ready[f])
         ctx.predict_device(pictures[f][0], d_pus[f], *outs[f])
 
     elapsed = timed(args.steps, args.warmup, step, None)
@@ -399,8 +409,12 @@ def mvp_in_loop(args, ctx, cfg, pictures, d_pus, outs, area):
         lat[name] = {"queries": int(n), "device_ms": round(float(np.median(dev[5:])), 4),
                      "host_call_ms": round(host * 1e3, 4)}
     return {"ms_per_picture": round(ms, 4), "mpix_s": round(steps_area / elapsed / 1e6, 2),
-            "note": "conversions of picture t+1 on their own stream during picture t's prediction; "
-                    "prediction of t (planning included, plan-ahead off) waits for its conversions",
+            "plan_ahead": bool(args.plan_ahead),
+            "note": ("conversions of picture t+2 on their own stream during picture t's prediction; the host "
+                     "issues picture t's prediction (plan-ahead) once its conversions are complete"
+                     if args.plan_ahead else
+                     "conversions of picture t+1 on their own stream during picture t's prediction; "
+                     "prediction of t (planning included, plan-ahead off) waits for its conversions"),
             "batch_latency": lat}
 
 

@@ -12,7 +12,7 @@ import json
 import sys
 
 ROOT = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
-OUT = sys.argv[2] if len(sys.argv) > 2 else "profiles/r03_traffic.json"
+OUT = sys.argv[2] if len(sys.argv) > 2 else "profiles/r04_traffic.json"
 PICTURES = 4  # bench.py --pictures default, used by the pmc passes of tools/gpu_run.sh
 KERNELS = ("k_mc_dev", "k_mc_pair_dev")  # the picture path's interpolation kernel, whichever is built
 

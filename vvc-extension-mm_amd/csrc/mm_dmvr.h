@@ -112,21 +112,24 @@ MM_HD void dmvr_positions_offsets(const SeqConst& sc, const SubPuDev& u, const B
   }
 }
 
-// Thread (survivor k, sub-block e, list l) of k_dmvr_reproj_dev: the positions of its 24 non-centre
-// offsets into the survivor's items surv_base[k] + 2 * (j * n + e) + l.
-MM_HD void dmvr_reproj_thread(int k, int e, int l, const int* surv_s, const int* surv_base, const SeqConst& sc,
+// Thread t of survivor k in k_dmvr_reproj_dev (6 n threads: t = 2 (part n + e) + l): the positions of
+// sub-block e of list l at the 8 non-centre offsets 8 part .. 8 part + 7, into the survivor's items
+// surv_base[k] + 2 (j n + e) + l.
+MM_HD void dmvr_reproj_thread(int k, int t, const int* surv_s, const int* surv_base, const SeqConst& sc,
                               const SubPuDev* sp, const BlockSetup* setups, const MpaCache& cache, mm_int2* pos) {
   const int s = surv_s[k];
   const SubPuDev& u = sp[s];
-  if (e >= u.n) return;
+  const int l = t & 1, pe = t >> 1, part = pe / u.n, e = pe - part * u.n;
+  const int j0 = 8 * part;
   mm_int2* dst = pos + surv_base[k] + 2 * e + l;
   const int stride = 2 * u.n;
-  dmvr_positions_offsets(sc, u, setups, s, l, e, cache, dmvr_outer_offset, N_OFF - 1, [&](int j, int32_t fx, int32_t fy) {
-    mm_int2 q;
-    q.x = fx;
-    q.y = fy;
-    dst[(long)j * stride] = q;
-  });
+  dmvr_positions_offsets(sc, u, setups, s, l, e, cache, [&](int j) { return dmvr_outer_offset(j0 + j); }, 8,
+                         [&](int j, int32_t fx, int32_t fy) {
+                           mm_int2 q;
+                           q.x = fx;
+                           q.y = fy;
+                           dst[(long)(j0 + j) * stride] = q;
+                         });
 }
 
 // xDMVRCost's share of one 4x4 sub-block: SAD of its rows 0 and 2 (the sub-PU's even rows, RdCost

@@ -521,7 +521,8 @@ struct DmvrWork {
   int* sitems;                // position items of sub-PU s: 2 x 24 x n if it survived, else 0
   int* surv_s;                // sub-PU of survivor k
   int* surv_base;             // first position item of survivor k
-  int* surv_chunk;            // survivor holding position item 64 c (wave_find_item hints)
+  int* surv_tbase;            // first k_dmvr_reproj_dev thread of survivor k (surv_base / 8)
+  int* surv_tchunk;           // survivor holding reprojection thread 64 c (wave_find_item hints)
 };
 
 // thread per (sub-PU, offset, list) setup
@@ -536,10 +537,10 @@ __global__ void __launch_bounds__(256) k_dmvr_setup_dev(SeqConst sc, const PlanM
     dmvr_setup_thread(i, sc, sp, s_ged, out);
 }
 
-// The centre cost of every sub-PU (InterPrediction.cpp:2510-2525): one wave per sub-PU, lane
+// The centre cost of every sub-PU (InterPrediction.cpp:2510-2525): 32 lanes per sub-PU, lane
 // 2 e + l list l of luma 4x4 sub-block e -- its position at the merge MV and rows 0 and 2 of its
 // 14-bit prediction; the L0 lane takes its partner's L1 rows by shuffle for the SAD, summed over
-// the wave.  minCost = cost - cost/4 < dx*dy ends the search: the sub-PU keeps its merge MVs
+// the 32 lanes.  minCost = cost - cost/4 < dx*dy ends the search: the sub-PU keeps its merge MVs
 // (dmvr_apply with a zero delta).  Otherwise it needs 2 x 24 x n position items (sitems), which
 // k_dmvr_compact_dev turns into the survivor list.
 __global__ void __launch_bounds__(256) k_dmvr_centre_dev(SeqConst sc, Geometry geo, const PlanMeta* __restrict__ meta,
@@ -557,9 +558,8 @@ __global__ void __launch_bounds__(256) k_dmvr_centre_dev(SeqConst sc, Geometry g
   __syncthreads();
   const int n_sub = meta->n_sub;
   const RefPool pool = t.pool;
-  for (int base = blockIdx.x * 256; base < n_sub * 64; base += gridDim.x * 256) {  // uniform trip count
-    // one sub-PU per wave (its model and slots uniform: scalar loads of the record)
-    const int g = base + tid, s = __builtin_amdgcn_readfirstlane(g >> 6), e = (g >> 1) & 31, l = g & 1;
+  for (int base = blockIdx.x * 256; base < n_sub * 32; base += gridDim.x * 256) {  // uniform trip count
+    const int g = base + tid, s = g >> 5, e = (g >> 1) & 15, l = g & 1;
     int16_t p[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     SubPuDev u;
     if (s < n_sub) u = sp[s];
@@ -584,8 +584,8 @@ __global__ void __launch_bounds__(256) k_dmvr_centre_dev(SeqConst sc, Geometry g
     }
     v = l ? 0u : v;  // each pair counted once
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) v += __shfl_xor(v, d);
-    if (s < n_sub && (g & 63) == 0) {
+    for (int d = 1; d < 32; d <<= 1) v += __shfl_xor(v, d);
+    if (s < n_sub && (g & 31) == 0) {
       w.ccost[s] = v;
       const bool survives = v - (v >> 2) >= (uint32_t)(u.w * u.h);
       w.sitems[s] = survives ? 2 * (N_OFF - 1) * u.n : 0;
@@ -596,61 +596,83 @@ __global__ void __launch_bounds__(256) k_dmvr_centre_dev(SeqConst sc, Geometry g
 }
 
 // The survivor list in sub-PU order (one workgroup): an exclusive scan of sitems gives each
-// surviving sub-PU its item base and survivor index; count = (survivors << 32) | items.  (A single
-// atomic counter appended by the centre kernel serialised ~14 K device-scope atomics.)
+// surviving sub-PU its item base and survivor index; count = (survivors << 32) | items.  Rounds of
+// 1024 sub-PUs, all rounds' loads issued first, a workgroup scan per round.  (A single atomic counter
+// appended by the centre kernel serialised ~14 K device-scope atomics; one thread per run of
+// consecutive sub-PUs was a chain of dependent loads, ~100 µs.)
 constexpr int DMVR_COMPACT_WG = 1024;
+constexpr int DMVR_COMPACT_ROUNDS = 16;  // sub-PUs held in registers per thread before the scans
 __global__ void __launch_bounds__(DMVR_COMPACT_WG) k_dmvr_compact_dev(const PlanMeta* __restrict__ meta, DmvrWork w) {
   __shared__ int s_items[DMVR_COMPACT_WG / 64], s_surv[DMVR_COMPACT_WG / 64];
   const int n_sub = meta->n_sub, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int per = (n_sub + DMVR_COMPACT_WG - 1) / DMVR_COMPACT_WG;  // consecutive sub-PUs per thread
-  const int s0 = min(n_sub, tid * per), s1 = min(n_sub, s0 + per);
-  int items = 0, surv = 0;
-  for (int s = s0; s < s1; s++) {
-    const int it = w.sitems[s];
-    items += it;
-    surv += it ? 1 : 0;
-  }
-  // exclusive scan: inside the wave, then over the waves
-  int ie = items, se = surv;
+  int run_items = 0, run_surv = 0;  // totals of the rounds before (uniform)
+  for (int r0 = 0; r0 < n_sub; r0 += DMVR_COMPACT_WG * DMVR_COMPACT_ROUNDS) {
+    int it[DMVR_COMPACT_ROUNDS];
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int a = __shfl_up(ie, d), b = __shfl_up(se, d);
-    if (lane >= d) {
-      ie += a;
-      se += b;
+    for (int r = 0; r < DMVR_COMPACT_ROUNDS; r++) {
+      const int s = r0 + r * DMVR_COMPACT_WG + tid;
+      it[r] = s < n_sub ? w.sitems[s] : 0;
+    }
+#pragma unroll
+    for (int r = 0; r < DMVR_COMPACT_ROUNDS; r++) {
+      const int s = r0 + r * DMVR_COMPACT_WG + tid;
+      if (r0 + r * DMVR_COMPACT_WG >= n_sub) continue;  // uniform
+      int ie = it[r], se = it[r] ? 1 : 0;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int a = __shfl_up(ie, d), b = __shfl_up(se, d);
+        if (lane >= d) {
+          ie += a;
+          se += b;
+        }
+      }
+      if (lane == 63) {
+        s_items[wave] = ie;
+        s_surv[wave] = se;
+      }
+      __syncthreads();
+      int ib = run_items + ie - it[r], kb = run_surv + se - (it[r] ? 1 : 0);
+      int tot_items = 0, tot_surv = 0;
+#pragma unroll
+      for (int v = 0; v < DMVR_COMPACT_WG / 64; v++) {
+        const int ti = s_items[v], ts = s_surv[v];
+        if (v < wave) {
+          ib += ti;
+          kb += ts;
+        }
+        tot_items += ti;
+        tot_surv += ts;
+      }
+      __syncthreads();  // s_items / s_surv reused by the next round
+      if (it[r]) {
+        w.surv_s[kb] = s;
+        w.surv_base[kb] = ib;
+        w.surv_tbase[kb] = ib / 8;
+        write_chunks(w.surv_tchunk, kb, ib / 8, it[r] / 8);
+      }
+      run_items += tot_items;
+      run_surv += tot_surv;
     }
   }
-  if (lane == 63) {
-    s_items[wave] = ie;
-    s_surv[wave] = se;
-  }
-  __syncthreads();
-  int ib = ie - items, kb = se - surv;
-  for (int v = 0; v < wave; v++) {
-    ib += s_items[v];
-    kb += s_surv[v];
-  }
-  for (int s = s0; s < s1; s++) {
-    const int it = w.sitems[s];
-    if (!it) continue;
-    w.surv_s[kb] = s;
-    w.surv_base[kb] = ib;
-    write_chunks(w.surv_chunk, kb, ib, it);
-    ib += it;
-    kb++;
-  }
-  if (tid == DMVR_COMPACT_WG - 1) *w.count = ((unsigned long long)kb << 32) | (unsigned long long)(unsigned)ib;
+  if (tid == 0) *w.count = ((unsigned long long)run_surv << 32) | (unsigned long long)(unsigned)run_items;
 }
 
-// thread per (survivor, luma 4x4 sub-block, list), 32 per survivor (mm_dmvr.h dmvr_reproj_thread):
-// the positions of its 24 non-centre offsets -- the element's grid terms and its model's
-// MV-independent head once, the tail per offset -- 8 bytes each into the survivor's items.
+// thread per (survivor, part, luma 4x4 sub-block, list), 6 n per survivor (mm_dmvr.h
+// dmvr_reproj_thread): the positions of 8 of the 24 non-centre offsets -- the element's grid terms
+// and its model's MV-independent head once, the tail per offset -- 8 bytes each into the survivor's
+// items.
 __global__ void __launch_bounds__(256) k_dmvr_reproj_dev(SeqConst sc, const SubPuDev* __restrict__ sp,
                                                          const BlockSetup* __restrict__ setups, MpaCache cache,
                                                          DmvrWork w, mm_int2* __restrict__ pos) {
-  const int n_surv = (int)(*w.count >> 32);
-  for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < n_surv * 32; g += gridDim.x * blockDim.x)
-    dmvr_reproj_thread(g >> 5, (g >> 1) & 15, g & 1, w.surv_s, w.surv_base, sc, sp, setups, cache, pos);
+  const unsigned long long cnt = *w.count;
+  const int n_surv = (int)(cnt >> 32), n_threads = (int)(cnt & 0xffffffffull) / 8;
+  const int lane = __lane_id();
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, n_waves = (gridDim.x * blockDim.x) >> 6;
+  for (int g0 = wave * 64; g0 < n_threads; g0 += n_waves * 64) {
+    const int g = g0 + lane;
+    const int k = wave_find_item(w.surv_tbase, w.surv_tchunk, g, n_surv);
+    if (g < n_threads) dmvr_reproj_thread(k, g - w.surv_tbase[k], w.surv_s, w.surv_base, sc, sp, setups, cache, pos);
+  }
 }
 
 // The search of one surviving sub-PU per workgroup iteration (xProcessDMVRProjected,
@@ -1070,7 +1092,7 @@ struct mm_ctx {
   DevBuf<mm_int2> d_dmvr_pos;  // both lists' reprojected positions per (survivor, offset, sub-block)
   DevBuf<unsigned long long> d_dmvr_count;  // DmvrWork (k_dmvr_centre_dev's survivor list)
   DevBuf<uint32_t> d_dmvr_ccost;
-  DevBuf<int> d_dmvr_sitems, d_dmvr_surv_s, d_dmvr_surv_base, d_dmvr_surv_chunk;
+  DevBuf<int> d_dmvr_sitems, d_dmvr_surv_s, d_dmvr_surv_base, d_dmvr_surv_tbase, d_dmvr_surv_tchunk;
   // MM-MVP: the device copy of the epipole list (refreshed when its version moves, staged through a
   // pinned buffer on the context stream), the host-buffer API's query / result buffers and the
   // deferred status words (ping-pong: a call's block 0 zeroes the next call's word)
@@ -1319,7 +1341,8 @@ int mm_destroy(mm_ctx* c) {
   c->d_dmvr_sitems.release();
   c->d_dmvr_surv_s.release();
   c->d_dmvr_surv_base.release();
-  c->d_dmvr_surv_chunk.release();
+  c->d_dmvr_surv_tbase.release();
+  c->d_dmvr_surv_tchunk.release();
   c->d_mvp_q.release();
   c->d_mvp_out.release();
   c->d_mvp_status.release();
@@ -1640,7 +1663,8 @@ static int ensure_slot_buffers(mm_ctx* c, PlanSlot& S, int n, bool dmvr) {
     HIPCHK(c, c->d_dmvr_sitems.ensure(k.subs));
     HIPCHK(c, c->d_dmvr_surv_s.ensure(k.subs));
     HIPCHK(c, c->d_dmvr_surv_base.ensure(k.subs));
-    HIPCHK(c, c->d_dmvr_surv_chunk.ensure(2 * (size_t)k.dmvr_elems / 64 + 1));
+    HIPCHK(c, c->d_dmvr_surv_tbase.ensure(k.subs));
+    HIPCHK(c, c->d_dmvr_surv_tchunk.ensure(2 * (size_t)k.dmvr_elems / 8 / 64 + 1));
     S.dmvr_ensured = true;
   }
   bool fresh_jobs = false;
@@ -1707,15 +1731,16 @@ static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables
       back = false;
     }
     const int gd = (int)std::min<long>(DMVR_GRID, ((long)k.subs * N_OFF * 2 + 255) / 256 + 1);
-    const DmvrWork dw{c->d_dmvr_count.p, c->d_dmvr_ccost.p, c->d_dmvr_sitems.p, c->d_dmvr_surv_s.p,
-                      c->d_dmvr_surv_base.p, c->d_dmvr_surv_chunk.p};
+    const DmvrWork dw{c->d_dmvr_count.p,     c->d_dmvr_ccost.p,     c->d_dmvr_sitems.p,
+                      c->d_dmvr_surv_s.p,    c->d_dmvr_surv_base.p, c->d_dmvr_surv_tbase.p,
+                      c->d_dmvr_surv_tchunk.p};
     int32_t* mvd = want_mvd ? c->d_dmvr_mvd.p : nullptr;
     hipLaunchKernelGGL(k_dmvr_setup_dev, dim3(gd), dim3(256), 0, st, c->sc, S.meta.p, S.dmvr_sub.p, t, c->d_dmvr_setup.p);
-    const int gcen = (int)std::min<long>(DMVR_GRID, ((long)k.subs * 64 + 255) / 256);
+    const int gcen = (int)std::min<long>(DMVR_GRID, ((long)k.subs * 32 + 255) / 256);
     hipLaunchKernelGGL(k_dmvr_centre_dev, dim3(std::max(1, gcen)), dim3(256), 0, st, c->sc, geo, S.meta.p, S.dmvr_sub.p,
                        c->d_dmvr_setup.p, make_cache(c), t, dw, S.jobs.p, mvd);
     hipLaunchKernelGGL(k_dmvr_compact_dev, dim3(1), dim3(DMVR_COMPACT_WG), 0, st, S.meta.p, dw);
-    const int gc = (int)std::min<long>(DMVR_GRID, ((long)k.subs * 32 + 255) / 256);
+    const int gc = (int)std::min<long>(DMVR_GRID, ((long)k.dmvr_elems * 2 / 8 + 255) / 256 + 1);
     hipLaunchKernelGGL(k_dmvr_reproj_dev, dim3(gc), dim3(256), 0, st, c->sc, S.dmvr_sub.p, c->d_dmvr_setup.p,
                        make_cache(c), dw, c->d_dmvr_pos.p);
     hipLaunchKernelGGL(k_dmvr_search_dev, dim3(std::max(1, std::min(DMVR_SEARCH_GRID, k.subs))), dim3(DMVR_SEARCH_WG),
