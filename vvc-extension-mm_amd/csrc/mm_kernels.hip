@@ -516,22 +516,22 @@ constexpr int DMVR_GRID = 2048;  // workgroups of 256 of the grid-stride setup k
 
 // The picture's DMVR survivors (sub-PUs whose centre cost does not end the search) and their items
 struct DmvrWork {
-  unsigned long long* count;  // (survivors << 32) | position items (k_dmvr_compact_dev)
+  unsigned long long* count;  // (survivors << 32) | position items (k_dmvr_centre_dev)
   uint32_t* ccost;            // centre cost (xDMVRCost at the merge MVs) per sub-PU
-  int* sitems;                // position items of sub-PU s: 2 x 24 x n if it survived, else 0
   int* surv_s;                // sub-PU of survivor k
   int* surv_base;             // first position item of survivor k
   int* surv_tbase;            // first k_dmvr_reproj_dev thread of survivor k (surv_base / 8)
   int* surv_tchunk;           // survivor holding reprojection thread 64 c (wave_find_item hints)
 };
 
-// thread per (sub-PU, offset, list) setup
+// thread per (sub-PU, offset, list) setup; also clears the survivor count for k_dmvr_centre_dev
 __global__ void __launch_bounds__(256) k_dmvr_setup_dev(SeqConst sc, const PlanMeta* __restrict__ meta,
                                                         const SubPuDev* __restrict__ sp, const PicTables t,
-                                                        BlockSetup* __restrict__ out) {
+                                                        BlockSetup* __restrict__ out, unsigned long long* __restrict__ count) {
   __shared__ M3 s_ged[3 + MAX_SLOTS];  // indexed per lane: staged with scalar loads (stage_arg_words)
   stage_arg_words<sizeof(s_ged) / 4>(reinterpret_cast<const uint32_t*>(t.ged), reinterpret_cast<uint32_t*>(s_ged));
   __syncthreads();
+  if (blockIdx.x == 0 && threadIdx.x == 0) *count = 0ull;
   const int n_jobs = meta->n_sub * N_OFF * 2;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n_jobs; i += gridDim.x * blockDim.x)
     dmvr_setup_thread(i, sc, sp, s_ged, out);
@@ -541,8 +541,10 @@ __global__ void __launch_bounds__(256) k_dmvr_setup_dev(SeqConst sc, const PlanM
 // 2 e + l list l of luma 4x4 sub-block e -- its position at the merge MV and rows 0 and 2 of its
 // 14-bit prediction; the L0 lane takes its partner's L1 rows by shuffle for the SAD, summed over
 // the 32 lanes.  minCost = cost - cost/4 < dx*dy ends the search: the sub-PU keeps its merge MVs
-// (dmvr_apply with a zero delta).  Otherwise it needs 2 x 24 x n position items (sitems), which
-// k_dmvr_compact_dev turns into the survivor list.
+// (dmvr_apply with a zero delta).  Otherwise it joins the survivor list with 2 x 24 x n position
+// items, allocated for the workgroup's survivors together by one atomic (a counter bumped per
+// sub-PU serialised ~14 K device-scope atomics, ~100 µs; a separate one-workgroup scan kernel took
+// 25 µs).  The list order varies from run to run; each survivor decides alone, so results do not.
 __global__ void __launch_bounds__(256) k_dmvr_centre_dev(SeqConst sc, Geometry geo, const PlanMeta* __restrict__ meta,
                                                          const SubPuDev* __restrict__ sp,
                                                          const BlockSetup* __restrict__ setups, MpaCache cache,
@@ -551,10 +553,12 @@ __global__ void __launch_bounds__(256) k_dmvr_centre_dev(SeqConst sc, Geometry g
 #if defined(__HIP_DEVICE_COMPILE__)  // device-only filter paths (mm_filter.h predict_rows02, PtrRows)
   __shared__ PackedTaps s_taps;
   __shared__ RefDev s_ref[MAX_SLOTS];  // indexed per lane: rebuilt from scalar loads (stage_ref_table)
+  __shared__ int s_items[8], s_pre[8], s_base[2];
   const int tid = threadIdx.x;
   if (tid < sizeof(PackedTaps) / 16)
     reinterpret_cast<uint4*>(&s_taps)[tid] = reinterpret_cast<const uint4*>(&c_packed_taps)[tid];
   stage_ref_table<MAX_SLOTS>(t.pool_slot4, t.pool, s_ref);
+  if (tid < 8) s_items[tid] = 0;
   __syncthreads();
   const int n_sub = meta->n_sub;
   const RefPool pool = t.pool;
@@ -585,76 +589,43 @@ __global__ void __launch_bounds__(256) k_dmvr_centre_dev(SeqConst sc, Geometry g
     v = l ? 0u : v;  // each pair counted once
 #pragma unroll
     for (int d = 1; d < 32; d <<= 1) v += __shfl_xor(v, d);
+    // survivors of this workgroup's 8 sub-PUs: one 64-bit atomic per workgroup allocates their
+    // survivor indices and position items together (so item bases grow with the index)
+    const int slot = tid >> 5;
+    int items = 0;
     if (s < n_sub && (g & 31) == 0) {
       w.ccost[s] = v;
       const bool survives = v - (v >> 2) >= (uint32_t)(u.w * u.h);
-      w.sitems[s] = survives ? 2 * (N_OFF - 1) * u.n : 0;
+      items = survives ? 2 * (N_OFF - 1) * u.n : 0;
       if (!survives) dmvr_apply(s, u, 0, 0, jobs, mvd);  // notZeroCost = false: no refinement (:2520-2525)
+      s_items[slot] = items;
     }
+    __syncthreads();
+    if (tid == 0) {
+      int ni = 0, ns = 0;
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int it = (base + 32 * k < n_sub * 32) ? s_items[k] : 0;
+        s_pre[k] = (ns << 20) | ni;  // survivors before, items before (< 2^20 per workgroup)
+        ni += it;
+        ns += it ? 1 : 0;
+      }
+      unsigned long long old = 0;
+      if (ns) old = atomicAdd(w.count, ((unsigned long long)ns << 32) | (unsigned long long)ni);
+      s_base[0] = (int)(old >> 32);
+      s_base[1] = (int)(old & 0xffffffffull);
+    }
+    __syncthreads();
+    if (items) {
+      const int k = s_base[0] + (s_pre[slot] >> 20), ib = s_base[1] + (s_pre[slot] & 0xfffff);
+      w.surv_s[k] = s;
+      w.surv_base[k] = ib;
+      w.surv_tbase[k] = ib / 8;
+      write_chunks(w.surv_tchunk, k, ib / 8, items / 8);
+    }
+    __syncthreads();  // s_items / s_pre / s_base reused by the next iteration
   }
 #endif
-}
-
-// The survivor list in sub-PU order (one workgroup): an exclusive scan of sitems gives each
-// surviving sub-PU its item base and survivor index; count = (survivors << 32) | items.  Rounds of
-// 1024 sub-PUs, all rounds' loads issued first, a workgroup scan per round.  (A single atomic counter
-// appended by the centre kernel serialised ~14 K device-scope atomics; one thread per run of
-// consecutive sub-PUs was a chain of dependent loads, ~100 µs.)
-constexpr int DMVR_COMPACT_WG = 1024;
-constexpr int DMVR_COMPACT_ROUNDS = 16;  // sub-PUs held in registers per thread before the scans
-__global__ void __launch_bounds__(DMVR_COMPACT_WG) k_dmvr_compact_dev(const PlanMeta* __restrict__ meta, DmvrWork w) {
-  __shared__ int s_items[DMVR_COMPACT_WG / 64], s_surv[DMVR_COMPACT_WG / 64];
-  const int n_sub = meta->n_sub, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  int run_items = 0, run_surv = 0;  // totals of the rounds before (uniform)
-  for (int r0 = 0; r0 < n_sub; r0 += DMVR_COMPACT_WG * DMVR_COMPACT_ROUNDS) {
-    int it[DMVR_COMPACT_ROUNDS];
-#pragma unroll
-    for (int r = 0; r < DMVR_COMPACT_ROUNDS; r++) {
-      const int s = r0 + r * DMVR_COMPACT_WG + tid;
-      it[r] = s < n_sub ? w.sitems[s] : 0;
-    }
-#pragma unroll
-    for (int r = 0; r < DMVR_COMPACT_ROUNDS; r++) {
-      const int s = r0 + r * DMVR_COMPACT_WG + tid;
-      if (r0 + r * DMVR_COMPACT_WG >= n_sub) continue;  // uniform
-      int ie = it[r], se = it[r] ? 1 : 0;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const int a = __shfl_up(ie, d), b = __shfl_up(se, d);
-        if (lane >= d) {
-          ie += a;
-          se += b;
-        }
-      }
-      if (lane == 63) {
-        s_items[wave] = ie;
-        s_surv[wave] = se;
-      }
-      __syncthreads();
-      int ib = run_items + ie - it[r], kb = run_surv + se - (it[r] ? 1 : 0);
-      int tot_items = 0, tot_surv = 0;
-#pragma unroll
-      for (int v = 0; v < DMVR_COMPACT_WG / 64; v++) {
-        const int ti = s_items[v], ts = s_surv[v];
-        if (v < wave) {
-          ib += ti;
-          kb += ts;
-        }
-        tot_items += ti;
-        tot_surv += ts;
-      }
-      __syncthreads();  // s_items / s_surv reused by the next round
-      if (it[r]) {
-        w.surv_s[kb] = s;
-        w.surv_base[kb] = ib;
-        w.surv_tbase[kb] = ib / 8;
-        write_chunks(w.surv_tchunk, kb, ib / 8, it[r] / 8);
-      }
-      run_items += tot_items;
-      run_surv += tot_surv;
-    }
-  }
-  if (tid == 0) *w.count = ((unsigned long long)run_surv << 32) | (unsigned long long)(unsigned)run_items;
 }
 
 // thread per (survivor, part, luma 4x4 sub-block, list), 6 n per survivor (mm_dmvr.h
@@ -1092,7 +1063,7 @@ struct mm_ctx {
   DevBuf<mm_int2> d_dmvr_pos;  // both lists' reprojected positions per (survivor, offset, sub-block)
   DevBuf<unsigned long long> d_dmvr_count;  // DmvrWork (k_dmvr_centre_dev's survivor list)
   DevBuf<uint32_t> d_dmvr_ccost;
-  DevBuf<int> d_dmvr_sitems, d_dmvr_surv_s, d_dmvr_surv_base, d_dmvr_surv_tbase, d_dmvr_surv_tchunk;
+  DevBuf<int> d_dmvr_surv_s, d_dmvr_surv_base, d_dmvr_surv_tbase, d_dmvr_surv_tchunk;
   // MM-MVP: the device copy of the epipole list (refreshed when its version moves, staged through a
   // pinned buffer on the context stream), the host-buffer API's query / result buffers and the
   // deferred status words (ping-pong: a call's block 0 zeroes the next call's word)
@@ -1338,7 +1309,6 @@ int mm_destroy(mm_ctx* c) {
   c->d_dmvr_pos.release();
   c->d_dmvr_count.release();
   c->d_dmvr_ccost.release();
-  c->d_dmvr_sitems.release();
   c->d_dmvr_surv_s.release();
   c->d_dmvr_surv_base.release();
   c->d_dmvr_surv_tbase.release();
@@ -1660,7 +1630,6 @@ static int ensure_slot_buffers(mm_ctx* c, PlanSlot& S, int n, bool dmvr) {
     HIPCHK(c, c->d_dmvr_pos.ensure(2 * (size_t)k.dmvr_elems));
     HIPCHK(c, c->d_dmvr_count.ensure(1));
     HIPCHK(c, c->d_dmvr_ccost.ensure(k.subs));
-    HIPCHK(c, c->d_dmvr_sitems.ensure(k.subs));
     HIPCHK(c, c->d_dmvr_surv_s.ensure(k.subs));
     HIPCHK(c, c->d_dmvr_surv_base.ensure(k.subs));
     HIPCHK(c, c->d_dmvr_surv_tbase.ensure(k.subs));
@@ -1731,15 +1700,14 @@ static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables
       back = false;
     }
     const int gd = (int)std::min<long>(DMVR_GRID, ((long)k.subs * N_OFF * 2 + 255) / 256 + 1);
-    const DmvrWork dw{c->d_dmvr_count.p,     c->d_dmvr_ccost.p,     c->d_dmvr_sitems.p,
-                      c->d_dmvr_surv_s.p,    c->d_dmvr_surv_base.p, c->d_dmvr_surv_tbase.p,
-                      c->d_dmvr_surv_tchunk.p};
+    const DmvrWork dw{c->d_dmvr_count.p, c->d_dmvr_ccost.p, c->d_dmvr_surv_s.p, c->d_dmvr_surv_base.p,
+                      c->d_dmvr_surv_tbase.p, c->d_dmvr_surv_tchunk.p};
     int32_t* mvd = want_mvd ? c->d_dmvr_mvd.p : nullptr;
-    hipLaunchKernelGGL(k_dmvr_setup_dev, dim3(gd), dim3(256), 0, st, c->sc, S.meta.p, S.dmvr_sub.p, t, c->d_dmvr_setup.p);
+    hipLaunchKernelGGL(k_dmvr_setup_dev, dim3(gd), dim3(256), 0, st, c->sc, S.meta.p, S.dmvr_sub.p, t, c->d_dmvr_setup.p,
+                       dw.count);
     const int gcen = (int)std::min<long>(DMVR_GRID, ((long)k.subs * 32 + 255) / 256);
     hipLaunchKernelGGL(k_dmvr_centre_dev, dim3(std::max(1, gcen)), dim3(256), 0, st, c->sc, geo, S.meta.p, S.dmvr_sub.p,
                        c->d_dmvr_setup.p, make_cache(c), t, dw, S.jobs.p, mvd);
-    hipLaunchKernelGGL(k_dmvr_compact_dev, dim3(1), dim3(DMVR_COMPACT_WG), 0, st, S.meta.p, dw);
     const int gc = (int)std::min<long>(DMVR_GRID, ((long)k.dmvr_elems * 2 / 8 + 255) / 256 + 1);
     hipLaunchKernelGGL(k_dmvr_reproj_dev, dim3(gc), dim3(256), 0, st, c->sc, S.dmvr_sub.p, c->d_dmvr_setup.p,
                        make_cache(c), dw, c->d_dmvr_pos.p);
