@@ -386,7 +386,9 @@ __global__ void __launch_bounds__(256) k_reproj_dev(SeqConst sc, const PlanMeta*
 // The tap-pair tables (4 KB) are copied into LDS once per workgroup: every lane indexes them by
 // its own phase, and from __constant__ memory those lookups are ~16 vector loads per wave that
 // compete with the reference-window loads for the texture-address path.
-// amdgpu_waves_per_eu(4): 126 VGPRs without spills, 4 waves per SIMD (130 VGPRs -> 3 otherwise)
+// amdgpu_waves_per_eu(3): 151 VGPRs, 3 waves per SIMD.  At 4 waves (128 VGPRs) the round-4 body spills
+// 7 VGPRs to scratch; 3 spill-free waves are faster (C3 0.1735-0.1743 vs 0.1764-0.1792 ms per picture,
+// k_mc 94-96 vs 97-99 us, profiles/r04_ab_occupancy.txt)
 //
 // Band-per-XCD mapping: the sub-blocks are enumerated bin by bin in picture order and cut into
 // N_BANDS = 8 bands of about equal size (mm_devplan.h band_cut).  Workgroup b predicts band b % 8 --
@@ -398,7 +400,7 @@ __global__ void __launch_bounds__(256) k_reproj_dev(SeqConst sc, const PlanMeta*
 // table in LDS once for all its blocks.
 static_assert(N_BANDS == 8, "one band per XCD");
 template <bool UNI_HP>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_mc_dev(Geometry geo, const PlanMeta* __restrict__ meta, McRec mc,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k_mc_dev(Geometry geo, const PlanMeta* __restrict__ meta, McRec mc,
                                                 const PicTables t, int16_t* __restrict__ dst_y, int dsy,
                                                 int16_t* __restrict__ dst_cb, int16_t* __restrict__ dst_cr, int dsc) {
   const int band = blockIdx.x & 7, stride = (int)(gridDim.x >> 3) * 256;
@@ -666,7 +668,8 @@ constexpr int DMVR_WIN_W = 64;                   // staged union window per list
 [[maybe_unused]] constexpr int DMVR_WIN_H = 48;
 [[maybe_unused]] constexpr int DMVR_WIN_STRIDE = DMVR_WIN_W / 2 + 1;  // dwords per LDS row: odd, so rows start on different banks
 
-__global__ void __launch_bounds__(DMVR_SEARCH_WG) k_dmvr_search_dev(Geometry geo, const SubPuDev* __restrict__ sp,
+// amdgpu_waves_per_eu(5): 96 instead of 101 VGPRs, 5 waves per SIMD: 195 vs 202 us (profiles/r04_ab_occupancy.txt)
+__global__ void __launch_bounds__(DMVR_SEARCH_WG) __attribute__((amdgpu_waves_per_eu(5))) k_dmvr_search_dev(Geometry geo, const SubPuDev* __restrict__ sp,
                                                                    const mm_int2* __restrict__ pos, const PicTables t,
                                                                    DmvrWork w, JobDev* __restrict__ jobs,
                                                                    int32_t* __restrict__ mvd) {
