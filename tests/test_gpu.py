@@ -749,11 +749,14 @@ def test_pred_dmvr_every_branch_vs_oracle():
         assert tot[k] > 0, (k, tot)
 
 
-def test_mvp_convert_vs_oracle():
-    """Batched MM-MVP on the GPU == the oracle for every model pair (incl. CLASSIC), both epipoles."""
+@pytest.mark.parametrize("n", [20000, 40000])
+def test_mvp_convert_vs_oracle(n):
+    """Batched MM-MVP on the GPU == the oracle for every model pair (incl. CLASSIC), both epipoles;
+    40 K queries take the model-sorted path (MVP_SORT_MIN = 32768), where the status of bad
+    queries must still name the lowest failing input index."""
     from test_mvp import ALL as MVP_ALL, EPI2
     params = mm360.seq_params(2048, 1024, MVP_ALL)
-    q = W.mvp_queries(2048, 1024, MVP_ALL, 20000, seed=21)
+    q = W.mvp_queries(2048, 1024, MVP_ALL, n, seed=21)
     want = Oracle(params, EPI2).mvp(q)
     with _ctx(params, EPI2) as ctx:
         got = ctx.mvp_convert(q)
@@ -765,6 +768,19 @@ def test_mvp_convert_vs_oracle():
         got_dev = d_out.cpu().numpy()
     assert np.array_equal(got, want), np.argwhere((got != want).any(axis=1))[:5]
     assert np.array_equal(got_dev, want), np.argwhere((got_dev != want).any(axis=1))[:5]
+    if n >= 32768:
+        bad = q.copy()
+        bad["model_desired"][n - 5] = 99  # sorted into key 0, ahead of most queries
+        bad["shift_hor"][n - 900] = 9
+        with _ctx(params, EPI2) as ctx:
+            d_out = torch.zeros((n, 2), dtype=torch.int32, device="cuda")
+            ctx.mvp_convert_device(mm360.queries_to_device(bad), d_out)
+            with pytest.raises(mm360.MMError) as e:
+                ctx.mvp_status()
+            assert e.value.code == mm360.MM_ERR_ARG and f"MVP query {n - 900}:" in str(e.value), str(e.value)
+            ok = np.ones(n, bool)
+            ok[[n - 5, n - 900]] = False
+            assert np.array_equal(d_out.cpu().numpy()[ok], want[ok])
 
 
 def test_mvp_device_errors_and_epipole_refresh():

@@ -824,14 +824,64 @@ __device__ __forceinline__ void mvp_regroup(int key, int* s_cnt, int* s_perm, in
   *n_work = s_cnt[MVP_KEYS];
 }
 
+// Queries sorted by (candidate model, desired model) before k_mvp_dev: a launch over the bench's
+// query mix took 74 us, the same queries in model order 41 us -- workgroups that run one model
+// pair keep its code in the instruction cache (tools/mvp_probe.py).  A counting sort in two small
+// kernels: k_mvp_bucket counts the keys of its 256 queries in LDS and takes each key's range with
+// one atomic per key and workgroup (the order inside a key varies from run to run; each query
+// converts alone, so results do not); k_mvp_place adds the keys' starts.  The counters alternate
+// between calls: a call's k_mvp_bucket clears the next call's set.
+constexpr int MVP_BINS = NUM_MODELS * NUM_MODELS;
+constexpr int MVP_SORT_MIN = 32768;  // batches at least this large are sorted (mm_mvp_convert_device)
+__device__ __forceinline__ int mvp_key(const mm_mvp_query& x) {
+  const bool ok = x.model_orig >= 0 && x.model_orig < NUM_MODELS && x.model_desired >= 0 && x.model_desired < NUM_MODELS;
+  return ok ? x.model_orig * NUM_MODELS + x.model_desired : 0;
+}
+__global__ void __launch_bounds__(MVP_BLOCK) k_mvp_bucket(const mm_mvp_query* __restrict__ q, int n,
+                                                          unsigned* __restrict__ bins, unsigned* __restrict__ next_bins,
+                                                          int* __restrict__ local) {
+  __shared__ unsigned s_h[MVP_BINS], s_base[MVP_BINS];
+  const int tid = threadIdx.x, i = blockIdx.x * MVP_BLOCK + tid;
+  for (int b = tid; b < MVP_BINS; b += MVP_BLOCK) s_h[b] = 0u;
+  if (blockIdx.x == 0)
+    for (int b = tid; b < MVP_BINS; b += MVP_BLOCK) next_bins[b] = 0u;
+  __syncthreads();
+  int key = 0;
+  unsigned rank = 0;
+  if (i < n) {
+    key = mvp_key(q[i]);
+    rank = atomicAdd(&s_h[key], 1u);
+  }
+  __syncthreads();
+  for (int b = tid; b < MVP_BINS; b += MVP_BLOCK)
+    if (s_h[b]) s_base[b] = atomicAdd(&bins[b], s_h[b]);
+  __syncthreads();
+  if (i < n) local[i] = (int)(s_base[key] + rank);
+}
+__global__ void __launch_bounds__(MVP_BLOCK) k_mvp_place(const mm_mvp_query* __restrict__ q, int n,
+                                                         const unsigned* __restrict__ bins,
+                                                         const int* __restrict__ local, int* __restrict__ perm) {
+  __shared__ unsigned s_start[MVP_BINS];
+  const int tid = threadIdx.x, i = blockIdx.x * MVP_BLOCK + tid;
+  if (tid == 0) {
+    unsigned acc = 0;
+    for (int b = 0; b < MVP_BINS; b++) {
+      s_start[b] = acc;
+      acc += bins[b];
+    }
+  }
+  __syncthreads();
+  if (i < n) perm[s_start[mvp_key(q[i])] + local[i]] = i;
+}
+
 __global__ void __launch_bounds__(MVP_BLOCK) k_mvp_dev(SeqConst sc, const mm_mvp_query* __restrict__ q, int n,
-                                                       uint32_t active, mmmvp::EpiTable et, int32_t* __restrict__ out,
-                                                       unsigned long long* __restrict__ status,
+                                                       const int* __restrict__ order, uint32_t active, mmmvp::EpiTable et,
+                                                       int32_t* __restrict__ out, unsigned long long* __restrict__ status,
                                                        unsigned long long* __restrict__ next_status) {
   using namespace mmmvp;
   __shared__ mm_mvp_query s_q[MVP_BLOCK];
   __shared__ float s_sx[MVP_BLOCK], s_sy[MVP_BLOCK];
-  __shared__ int s_perm[MVP_BLOCK], s_cnt[MVP_KEYS + 1], s_ok[MVP_BLOCK];
+  __shared__ int s_perm[MVP_BLOCK], s_cnt[MVP_KEYS + 1], s_ok[MVP_BLOCK], s_qi[MVP_BLOCK];
   __shared__ unsigned long long s_status;
   const int tid = threadIdx.x, i0 = blockIdx.x * MVP_BLOCK, i = i0 + tid;
   if (tid == 0) s_status = 0;
@@ -839,16 +889,18 @@ __global__ void __launch_bounds__(MVP_BLOCK) k_mvp_dev(SeqConst sc, const mm_mvp
   __syncthreads();  // s_status is zeroed before any wave's atomicMax (waves 1-3 may run ahead of wave 0)
   int key = -1;
   if (i < n) {
-    const mm_mvp_query x = q[i];
+    const int qi = order ? order[i] : i;  // the query this thread converts (model order)
+    s_qi[tid] = qi;
+    const mm_mvp_query x = q[qi];
     s_q[tid] = x;
     int32_t o[2] = {0, 0};
     int code = mvp_validate(x, active);
     if (code == MM_OK && !mvp_early(x, et, o, &code)) key = x.model_orig;
     if (key < 0) {
-      out[2 * i] = o[0];
-      out[2 * i + 1] = o[1];
+      out[2 * qi] = o[0];
+      out[2 * qi + 1] = o[1];
     }
-    if (code) atomicMax(&s_status, status_word(i, code));
+    if (code) atomicMax(&s_status, status_word(qi, code));
   }
   int nw;
   mvp_regroup(key, s_cnt, s_perm, &nw);
@@ -858,8 +910,9 @@ __global__ void __launch_bounds__(MVP_BLOCK) k_mvp_dev(SeqConst sc, const mm_mvp
     float sx = 0.0f, sy = 0.0f;
     const bool ok = mvp_candidate_motion(sc, s_q[k], et, &sx, &sy);
     if (!ok) {
-      atomicMax(&s_status, status_word(i0 + k, MM_ERR_NOEPIPOLE));
-      out[2 * (i0 + k)] = out[2 * (i0 + k) + 1] = 0;
+      const int qk = s_qi[k];
+      atomicMax(&s_status, status_word(qk, MM_ERR_NOEPIPOLE));
+      out[2 * qk] = out[2 * qk + 1] = 0;
     }
     s_sx[k] = sx;
     s_sy[k] = sy;
@@ -872,9 +925,10 @@ __global__ void __launch_bounds__(MVP_BLOCK) k_mvp_dev(SeqConst sc, const mm_mvp
   if (tid < nw) {
     const int k = s_perm[tid];
     int32_t o[2] = {0, 0};
-    if (!mvp_desired_mv(sc, s_q[k], et, s_sx[k], s_sy[k], o)) atomicMax(&s_status, status_word(i0 + k, MM_ERR_NOEPIPOLE));
-    out[2 * (i0 + k)] = o[0];
-    out[2 * (i0 + k) + 1] = o[1];
+    const int qk = s_qi[k];
+    if (!mvp_desired_mv(sc, s_q[k], et, s_sx[k], s_sy[k], o)) atomicMax(&s_status, status_word(qk, MM_ERR_NOEPIPOLE));
+    out[2 * qk] = o[0];
+    out[2 * qk + 1] = o[1];
   }
   __syncthreads();
   if (tid == 0 && s_status) atomicMax(status, s_status);
@@ -1082,6 +1136,9 @@ struct mm_ctx {
   DevBuf<mm_mvp_query> d_mvp_q;
   DevBuf<int32_t> d_mvp_out;
   DevBuf<unsigned long long> d_mvp_status;
+  DevBuf<unsigned> d_mvp_bins;  // 2 x MVP_BINS key counters (alternating sorted calls)
+  int mvp_sort_par = 0;
+  DevBuf<int> d_mvp_local, d_mvp_perm;
   int mvp_par = 0;
   bool mvp_pending = false;
   DevBuf<int> d_me_off, d_me_chunk;
@@ -1276,6 +1333,8 @@ int mm_create(const mm_seq_params* p, int device, mm_ctx** out_ctx) {
   if (c->d_status.ensure(2) != hipSuccess || hipMemsetAsync(c->d_status.p, 0, 2 * sizeof(unsigned long long), c->stream) != hipSuccess ||
       c->d_mvp_status.ensure(2) != hipSuccess ||
       hipMemsetAsync(c->d_mvp_status.p, 0, 2 * sizeof(unsigned long long), c->stream) != hipSuccess ||
+      c->d_mvp_bins.ensure(2 * MVP_BINS) != hipSuccess ||
+      hipMemsetAsync(c->d_mvp_bins.p, 0, 2 * MVP_BINS * sizeof(unsigned), c->stream) != hipSuccess ||
       hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) {
     mm_destroy(c);
     return MM_ERR_HIP;
@@ -1319,6 +1378,9 @@ int mm_destroy(mm_ctx* c) {
   c->d_mvp_q.release();
   c->d_mvp_out.release();
   c->d_mvp_status.release();
+  c->d_mvp_bins.release();
+  c->d_mvp_local.release();
+  c->d_mvp_perm.release();
   c->d_epi.release();
   if (c->h_epi) (void)hipHostFree(c->h_epi);
   if (c->ev_epi) (void)hipEventDestroy(c->ev_epi);
@@ -2101,8 +2163,27 @@ int mm_mvp_convert_device(mm_ctx* c, const mm_mvp_query* d_q, int n, int32_t* d_
   if (c->mvp_on_own && c->epi_fresh) HIPCHK(c, hipStreamWaitEvent(ms, c->ev_epi, 0));  // the table copy
   c->epi_fresh = false;
   c->timed = c->call_timing || !c->mvp_on_own;
+  const int nb = (n + MVP_BLOCK - 1) / MVP_BLOCK;
+  // Picture-sized batches are sorted by model pair first (k_mvp_bucket / k_mvp_place: C3's 156 K
+  // queries 74 -> 68 us, MVP in the loop 0.2135 -> 0.208 ms per picture); below MVP_SORT_MIN the two
+  // extra launches cost more than the coherence gains (a CTU's 136 queries: +8 us), and the
+  // queries are converted in input order.
+  const bool sort = n >= MVP_SORT_MIN;
+  if (sort) {
+    // the sort buffers are shared by the calls of the context: growing them drains the device
+    // (DevBuf::ensure), so a conversion still running on the MVP stream keeps its buffers
+    HIPCHK(c, c->d_mvp_local.ensure(n));
+    HIPCHK(c, c->d_mvp_perm.ensure(n));
+  }
   if (c->timed) HIPCHK(c, hipEventRecord(c->ev0, ms));
-  hipLaunchKernelGGL(k_mvp_dev, dim3((n + MVP_BLOCK - 1) / MVP_BLOCK), dim3(MVP_BLOCK), 0, ms, c->sc, d_q, n,
+  if (sort) {
+    unsigned* bins = c->d_mvp_bins.p + MVP_BINS * c->mvp_sort_par;
+    hipLaunchKernelGGL(k_mvp_bucket, dim3(nb), dim3(MVP_BLOCK), 0, ms, d_q, n, bins,
+                       c->d_mvp_bins.p + MVP_BINS * (c->mvp_sort_par ^ 1), c->d_mvp_local.p);
+    hipLaunchKernelGGL(k_mvp_place, dim3(nb), dim3(MVP_BLOCK), 0, ms, d_q, n, bins, c->d_mvp_local.p, c->d_mvp_perm.p);
+    c->mvp_sort_par ^= 1;
+  }
+  hipLaunchKernelGGL(k_mvp_dev, dim3(nb), dim3(MVP_BLOCK), 0, ms, c->sc, d_q, n, sort ? c->d_mvp_perm.p : nullptr,
                      c->prm.active_models, et, d_mv_out, st, c->d_mvp_status.p + (c->mvp_par ^ 1));
   HIPCHK(c, hipGetLastError());
   if (c->timed) HIPCHK(c, hipEventRecord(c->ev1, ms));
