@@ -829,9 +829,14 @@ __device__ __forceinline__ void mvp_regroup(int key, int* s_cnt, int* s_perm, in
 // pair keep its code in the instruction cache (tools/mvp_probe.py).  A counting sort in two small
 // kernels: k_mvp_bucket counts the keys of its 256 queries in LDS and takes each key's range with
 // one atomic per key and workgroup (the order inside a key varies from run to run; each query
-// converts alone, so results do not); k_mvp_place adds the keys' starts.  The counters alternate
-// between calls: a call's k_mvp_bucket clears the next call's set.
+// converts alone, so results do not); k_mvp_place adds the keys' starts.  Each key has MVP_SUBS
+// counters, workgroup b adding to counter b % MVP_SUBS: one counter per key took all ~600
+// workgroups' atomics on 49 addresses (k_mvp_bucket 17 us on the bench mix, profiles/
+// r04_mvp_sort.txt).  The counters alternate between calls: a call's k_mvp_bucket clears the next
+// call's set.
 constexpr int MVP_BINS = NUM_MODELS * NUM_MODELS;
+constexpr int MVP_SUBS = 8;
+constexpr int MVP_COUNTERS = MVP_BINS * MVP_SUBS;  // [key][sub]
 constexpr int MVP_SORT_MIN = 32768;  // batches at least this large are sorted (mm_mvp_convert_device)
 __device__ __forceinline__ int mvp_key(const mm_mvp_query& x) {
   const bool ok = x.model_orig >= 0 && x.model_orig < NUM_MODELS && x.model_desired >= 0 && x.model_desired < NUM_MODELS;
@@ -841,10 +846,10 @@ __global__ void __launch_bounds__(MVP_BLOCK) k_mvp_bucket(const mm_mvp_query* __
                                                           unsigned* __restrict__ bins, unsigned* __restrict__ next_bins,
                                                           int* __restrict__ local) {
   __shared__ unsigned s_h[MVP_BINS], s_base[MVP_BINS];
-  const int tid = threadIdx.x, i = blockIdx.x * MVP_BLOCK + tid;
+  const int tid = threadIdx.x, i = blockIdx.x * MVP_BLOCK + tid, sub = blockIdx.x % MVP_SUBS;
   for (int b = tid; b < MVP_BINS; b += MVP_BLOCK) s_h[b] = 0u;
   if (blockIdx.x == 0)
-    for (int b = tid; b < MVP_BINS; b += MVP_BLOCK) next_bins[b] = 0u;
+    for (int b = tid; b < MVP_COUNTERS; b += MVP_BLOCK) next_bins[b] = 0u;
   __syncthreads();
   int key = 0;
   unsigned rank = 0;
@@ -854,24 +859,42 @@ __global__ void __launch_bounds__(MVP_BLOCK) k_mvp_bucket(const mm_mvp_query* __
   }
   __syncthreads();
   for (int b = tid; b < MVP_BINS; b += MVP_BLOCK)
-    if (s_h[b]) s_base[b] = atomicAdd(&bins[b], s_h[b]);
+    if (s_h[b]) s_base[b] = atomicAdd(&bins[b * MVP_SUBS + sub], s_h[b]);
   __syncthreads();
   if (i < n) local[i] = (int)(s_base[key] + rank);
 }
 __global__ void __launch_bounds__(MVP_BLOCK) k_mvp_place(const mm_mvp_query* __restrict__ q, int n,
                                                          const unsigned* __restrict__ bins,
                                                          const int* __restrict__ local, int* __restrict__ perm) {
-  __shared__ unsigned s_start[MVP_BINS];
-  const int tid = threadIdx.x, i = blockIdx.x * MVP_BLOCK + tid;
+  __shared__ unsigned s_cnt[MVP_COUNTERS], s_key[MVP_BINS];
+  const int tid = threadIdx.x, i = blockIdx.x * MVP_BLOCK + tid, sub = blockIdx.x % MVP_SUBS;
+  for (int k = tid; k < MVP_COUNTERS; k += MVP_BLOCK) s_cnt[k] = bins[k];
+  __syncthreads();
+  // this workgroup's counter of key b starts after the key's earlier counters (thread b) ...
+  if (tid < MVP_BINS) {
+    unsigned acc = 0;
+    for (int j = 0; j < MVP_SUBS; j++) {
+      const unsigned c = s_cnt[tid * MVP_SUBS + j];
+      if (j == sub) s_cnt[tid * MVP_SUBS] = acc;  // (slot j = 0 is read before it is overwritten)
+      acc += c;
+    }
+    s_key[tid] = acc;
+  }
+  __syncthreads();
+  // ... and after all earlier keys (one thread scans the 49 key totals)
   if (tid == 0) {
     unsigned acc = 0;
     for (int b = 0; b < MVP_BINS; b++) {
-      s_start[b] = acc;
-      acc += bins[b];
+      const unsigned t = s_key[b];
+      s_key[b] = acc;
+      acc += t;
     }
   }
   __syncthreads();
-  if (i < n) perm[s_start[mvp_key(q[i])] + local[i]] = i;
+  if (i < n) {
+    const int key = mvp_key(q[i]);
+    perm[s_key[key] + s_cnt[key * MVP_SUBS] + local[i]] = i;
+  }
 }
 
 __global__ void __launch_bounds__(MVP_BLOCK) k_mvp_dev(SeqConst sc, const mm_mvp_query* __restrict__ q, int n,
@@ -1136,7 +1159,7 @@ struct mm_ctx {
   DevBuf<mm_mvp_query> d_mvp_q;
   DevBuf<int32_t> d_mvp_out;
   DevBuf<unsigned long long> d_mvp_status;
-  DevBuf<unsigned> d_mvp_bins;  // 2 x MVP_BINS key counters (alternating sorted calls)
+  DevBuf<unsigned> d_mvp_bins;  // 2 x MVP_COUNTERS key counters (alternating sorted calls)
   int mvp_sort_par = 0;
   DevBuf<int> d_mvp_local, d_mvp_perm;
   int mvp_par = 0;
@@ -1333,8 +1356,8 @@ int mm_create(const mm_seq_params* p, int device, mm_ctx** out_ctx) {
   if (c->d_status.ensure(2) != hipSuccess || hipMemsetAsync(c->d_status.p, 0, 2 * sizeof(unsigned long long), c->stream) != hipSuccess ||
       c->d_mvp_status.ensure(2) != hipSuccess ||
       hipMemsetAsync(c->d_mvp_status.p, 0, 2 * sizeof(unsigned long long), c->stream) != hipSuccess ||
-      c->d_mvp_bins.ensure(2 * MVP_BINS) != hipSuccess ||
-      hipMemsetAsync(c->d_mvp_bins.p, 0, 2 * MVP_BINS * sizeof(unsigned), c->stream) != hipSuccess ||
+      c->d_mvp_bins.ensure(2 * MVP_COUNTERS) != hipSuccess ||
+      hipMemsetAsync(c->d_mvp_bins.p, 0, 2 * MVP_COUNTERS * sizeof(unsigned), c->stream) != hipSuccess ||
       hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) {
     mm_destroy(c);
     return MM_ERR_HIP;
@@ -2177,9 +2200,9 @@ int mm_mvp_convert_device(mm_ctx* c, const mm_mvp_query* d_q, int n, int32_t* d_
   }
   if (c->timed) HIPCHK(c, hipEventRecord(c->ev0, ms));
   if (sort) {
-    unsigned* bins = c->d_mvp_bins.p + MVP_BINS * c->mvp_sort_par;
+    unsigned* bins = c->d_mvp_bins.p + MVP_COUNTERS * c->mvp_sort_par;
     hipLaunchKernelGGL(k_mvp_bucket, dim3(nb), dim3(MVP_BLOCK), 0, ms, d_q, n, bins,
-                       c->d_mvp_bins.p + MVP_BINS * (c->mvp_sort_par ^ 1), c->d_mvp_local.p);
+                       c->d_mvp_bins.p + MVP_COUNTERS * (c->mvp_sort_par ^ 1), c->d_mvp_local.p);
     hipLaunchKernelGGL(k_mvp_place, dim3(nb), dim3(MVP_BLOCK), 0, ms, d_q, n, bins, c->d_mvp_local.p, c->d_mvp_perm.p);
     c->mvp_sort_par ^= 1;
   }
