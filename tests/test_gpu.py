@@ -357,6 +357,38 @@ def test_pred_stripes_do_not_change_results():
             ctx.set_stripes(0)
 
 
+def test_pred_contexts_in_flight_together():
+    """Independent pictures predicted by two contexts at once (INTEGRATION.md 'in flight together'):
+    each context on its own stream with plan-ahead off, calls interleaved without synchronisation,
+    every output == the oracle (the contexts share no mutable device state)."""
+    cfg = W.CONFIGS["C2"]
+    params = mm360.seq_params(cfg.width, cfg.height, cfg.models)
+    lists = [W.pu_list(cfg, frame=f) for f in (7, 8)]
+    refs = {poc: W.ref_planes(cfg.width, cfg.height, poc) for poc in W.REF_POCS}
+    want = [Oracle(params, EPI).predict(W.CUR_POC, p, refs, cfg.width, cfg.height) for p in lists]
+    streams = [torch.cuda.Stream() for _ in lists]
+    with _ctx(params) as c0, _ctx(params) as c1:
+        ctxs = [c0, c1]
+        for ctx, s in zip(ctxs, streams):
+            ctx.set_stream(s.cuda_stream)
+            ctx.set_plan_ahead(False)
+            for poc, (y, cb, cr) in refs.items():
+                ctx.upload_ref(poc, torch.from_numpy(y).cuda(), torch.from_numpy(cb).cuda(), torch.from_numpy(cr).cuda())
+        d_lists = [mm360.pus_to_device(p) for p in lists]
+        torch.cuda.synchronize()
+        outs = [[_planes(cfg, -5) for _ in range(3)] for _ in lists]
+        for r in range(3):
+            for k, ctx in enumerate(ctxs):
+                ctx.predict_device(W.CUR_POC, d_lists[k], *outs[k][r])
+        torch.cuda.synchronize()
+        for k, ctx in enumerate(ctxs):
+            assert ctx.status() == (mm360.MM_OK, -1)
+            for r in range(3):
+                for x, t, name in zip(want[k], outs[k][r], ("y", "cb", "cr")):
+                    got = t.cpu().numpy()
+                    assert np.array_equal(got, x), (k, r, plane_mismatch(name, got, x))
+
+
 def test_pred_plan_ahead_rotating_pictures():
     """mm_set_plan_ahead: three different PU lists predicted back to back (twice round, so each
     plan slot is reused while the other picture's kernels may still run; a smaller list first, so
