@@ -831,13 +831,14 @@ __device__ __forceinline__ void mvp_regroup(int key, int* s_cnt, int* s_perm, in
 // one atomic per key and workgroup (the order inside a key varies from run to run; each query
 // converts alone, so results do not); k_mvp_place adds the keys' starts.  Each key has MVP_SUBS
 // counters, workgroup b adding to counter b % MVP_SUBS: one counter per key took all ~600
-// workgroups' atomics on 49 addresses (k_mvp_bucket 17 us on the bench mix, profiles/
+// workgroups' atomics on the keys' 121 addresses (k_mvp_bucket 17 us on the bench mix, profiles/
 // r04_mvp_sort.txt).  The counters alternate between calls: a call's k_mvp_bucket clears the next
 // call's set.
 constexpr int MVP_BINS = NUM_MODELS * NUM_MODELS;
 constexpr int MVP_SUBS = 8;
 constexpr int MVP_COUNTERS = MVP_BINS * MVP_SUBS;  // [key][sub]
 constexpr int MVP_SORT_MIN = 32768;  // batches at least this large are sorted (mm_mvp_convert_device)
+static_assert(MVP_BINS <= MVP_BLOCK, "k_mvp_place gives every key one thread");
 __device__ __forceinline__ int mvp_key(const mm_mvp_query& x) {
   const bool ok = x.model_orig >= 0 && x.model_orig < NUM_MODELS && x.model_desired >= 0 && x.model_desired < NUM_MODELS;
   return ok ? x.model_orig * NUM_MODELS + x.model_desired : 0;
