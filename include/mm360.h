@@ -23,6 +23,8 @@
  *   mm_filter        <- InterpolationFilter::filterHor/filterVer  SRC/InterpolationFilter.h:123-128
  *   mm_pred_dmvr     <- InterPrediction::xProcessDMVRProjected  SRC/InterPrediction.cpp:2442-2634
  *   mm_mvp_convert   <- MVReprojection::motionVectorInDesiredMotionModel  SRC/MVReprojection.cpp:168-217
+ *   mm_mvp_convert_host <- the same, per query on the host, at the spatial merge / AMVP call sites
+ *                       (UnitTools.cpp:2930-2992, 3134-3167); device batches serve TMVP (:2267-2304)
  *   mm_sad_window    <- InterSearch::xMVReprojectionInterpolation + RdCost::xGetSAD per candidate
  *                       (EncoderLib/InterSearch.cpp:6277-6385, 363-443; SRC/RdCost.cpp:482-517)
  *   mm_upload_org    <- the original picture (pcPatternKey) the encoder SAD compares against
@@ -290,18 +292,35 @@ int mm_mvp_convert(mm_ctx* ctx, const mm_mvp_query* queries, int n, int32_t* mv_
 /* The same with queries and results in device memory: validation, GEODESIC_CAMPOSE epipole lookup
  * (a device copy of the context's EpipoleList, refreshed when the list changed) and both model
  * evaluations run on the device, stream-ordered on the context stream with no host
- * synchronisation.  The lowest failing query's code is reported by the next mm_mvp_status /
- * mm_synchronize (its result words are 0). */
+ * synchronisation.  Failures accumulate in one status word until the next mm_mvp_status /
+ * mm_synchronize reads (and clears) it: that call reports a failing query of the conversions issued
+ * since the previous read -- the lowest failing index among them -- so conversions issued
+ * back to back lose no failure (the failing queries' result words are 0). */
 int mm_mvp_convert_device(mm_ctx* ctx, const mm_mvp_query* d_queries, int n, int32_t* d_mv_out);
 int mm_mvp_status(mm_ctx* ctx, int* first_bad_query);
 /* The stream MM-MVP conversions run on (hipStream_t; NULL = the context stream, the default).  A
  * decoder that derives picture t+1's MVs while picture t is motion-compensated converts on its
  * own stream, so the conversions overlap the picture kernels; it orders the prediction of t+1
  * after them itself (an event on this stream).  Epipole-table refreshes (made on the context
- * stream) are ordered before the conversions that follow them.  mm_mvp_status / mm_mvp_convert
+ * stream) are ordered before the conversions that follow them, and after the conversions still
+ * reading the table they replace (two tables alternate per EpipoleList version).  mm_mvp_status / mm_mvp_convert
  * wait for this stream; the call's device time (mm_last_timing) is recorded only while call
  * timing is on. */
 int mm_set_mvp_stream(mm_ctx* ctx, void* hip_stream);
+
+/* MM-MVP one query at a time on the calling host thread, for the candidates VTM converts in
+ * decoding order: spatial merge and AMVP candidates take the neighbour's FINAL MV
+ * (UnitTools.cpp:2930-2992 merge, 3134-3167 addMVPCandUnscaled), which the PUs decoded just before
+ * produced, so they cannot wait for a device batch.  Replaces motionVectorInDesiredMotionModel
+ * (MVReprojection.cpp:168-217) at those call sites with the same bodies as the device conversion
+ * (csrc/mm_mvp.h) compiled for the host: results are identical to mm_mvp_convert_device's.  No
+ * device work and no context: `params` are the sequence's (mm_create's), `epipoles` the
+ * EpipoleList GEODESIC_CAMPOSE reads (a context's own list via mm_get_epipole_list, or NULL when
+ * no query needs one).  Returns MM_OK or the lowest failing query's code (its result words 0);
+ * first_bad (optional) = that query's index.  Re-entrant for distinct epipole lists; one thread
+ * per list. */
+int mm_mvp_convert_host(const mm_seq_params* params, mm_epipole_list* epipoles, const mm_mvp_query* queries, int n,
+                        int32_t* mv_out, int* first_bad);
 
 /* Single-block interpolation (InterpolationFilter::filterHor/filterVer on the device), for
  * parity tests of the integer pel pipeline.  comp 0 = luma 8-tap (16 phases), else chroma 4-tap

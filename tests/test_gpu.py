@@ -360,13 +360,19 @@ def test_pred_stripes_do_not_change_results():
 def test_pred_contexts_in_flight_together():
     """Independent pictures predicted by two contexts at once (INTEGRATION.md 'in flight together'):
     each context on its own stream with plan-ahead off, calls interleaved without synchronisation,
-    every output == the oracle (the contexts share no mutable device state)."""
+    every output == the oracle (the contexts share no mutable device state).  Context 0 starts with
+    a third of its list, so its buffers grow mid-sequence while context 1's pictures are in flight:
+    growth retires the old buffers behind events on the growing context's own streams (no device-wide
+    synchronisation, DevBuf::ensure)."""
     cfg = W.CONFIGS["C2"]
     params = mm360.seq_params(cfg.width, cfg.height, cfg.models)
-    lists = [W.pu_list(cfg, frame=f) for f in (7, 8)]
+    full = [W.pu_list(cfg, frame=f) for f in (7, 8)]
+    short = full[0][: len(full[0]) // 3]
+    lists = [[short, full[0], full[0]], [full[1]] * 3]  # [context][round]
     refs = {poc: W.ref_planes(cfg.width, cfg.height, poc) for poc in W.REF_POCS}
-    want = [Oracle(params, EPI).predict(W.CUR_POC, p, refs, cfg.width, cfg.height) for p in lists]
-    streams = [torch.cuda.Stream() for _ in lists]
+    orc = Oracle(params, EPI)
+    want = {id(p): orc.predict(W.CUR_POC, p, refs, cfg.width, cfg.height) for p in (short, full[0], full[1])}
+    streams = [torch.cuda.Stream() for _ in range(2)]
     with _ctx(params) as c0, _ctx(params) as c1:
         ctxs = [c0, c1]
         for ctx, s in zip(ctxs, streams):
@@ -374,17 +380,17 @@ def test_pred_contexts_in_flight_together():
             ctx.set_plan_ahead(False)
             for poc, (y, cb, cr) in refs.items():
                 ctx.upload_ref(poc, torch.from_numpy(y).cuda(), torch.from_numpy(cb).cuda(), torch.from_numpy(cr).cuda())
-        d_lists = [mm360.pus_to_device(p) for p in lists]
+        d_lists = {id(p): mm360.pus_to_device(p) for p in (short, full[0], full[1])}
         torch.cuda.synchronize()
-        outs = [[_planes(cfg, -5) for _ in range(3)] for _ in lists]
+        outs = [[_planes(cfg, 0) for _ in range(3)] for _ in range(2)]  # the short list leaves zeros, as the oracle
         for r in range(3):
             for k, ctx in enumerate(ctxs):
-                ctx.predict_device(W.CUR_POC, d_lists[k], *outs[k][r])
+                ctx.predict_device(W.CUR_POC, d_lists[id(lists[k][r])], *outs[k][r])
         torch.cuda.synchronize()
         for k, ctx in enumerate(ctxs):
             assert ctx.status() == (mm360.MM_OK, -1)
             for r in range(3):
-                for x, t, name in zip(want[k], outs[k][r], ("y", "cb", "cr")):
+                for x, t, name in zip(want[id(lists[k][r])], outs[k][r], ("y", "cb", "cr")):
                     got = t.cpu().numpy()
                     assert np.array_equal(got, x), (k, r, plane_mismatch(name, got, x))
 
@@ -874,6 +880,80 @@ def test_mvp_device_error_in_later_waves_is_reported():
         ok[[256 * b + int(l) for b, l in enumerate(lanes)]] = False
         want = Oracle(params, EPI2).mvp(q[ok])
         assert np.array_equal(d_out.cpu().numpy()[ok], want)
+
+
+def test_mvp_c3_size_vs_oracle():
+    """MM-MVP at the C3 size (6144x3072, all models of the C3 config, the bench's 2 queries per PU
+    of a C3 picture: the model-sorted device path) == the oracle, and the host per-query form
+    (mm_mvp_convert_host, used at the spatial candidates) gives the same MVs."""
+    from test_mvp import EPI2
+    cfg = W.CONFIGS["C3"]
+    models = tuple(cfg.models) + (mm360.GEODESIC_CAMPOSE,)
+    params = mm360.seq_params(cfg.width, cfg.height, models)
+    q = W.mvp_queries(cfg.width, cfg.height, models, 2 * 77947, seed=5)
+    want = Oracle(params, EPI2).mvp(q)
+    with _ctx(params, EPI2) as ctx:
+        d_out = torch.full((len(q), 2), -7, dtype=torch.int32, device="cuda")
+        ctx.mvp_convert_device(mm360.queries_to_device(q), d_out)
+        ctx.mvp_status()
+        got = d_out.cpu().numpy()
+        host = mm360.mvp_convert_host(params, q[:20000], ctx.epipole_list())
+    assert np.array_equal(got, want), np.argwhere((got != want).any(axis=1))[:5]
+    assert np.array_equal(host, want[:20000])
+
+
+def test_mvp_epipole_refresh_behind_side_stream_conversions():
+    """Conversions on their own MVP stream, then EpipoleList changes that sort new entries BEFORE the
+    existing ones (an earlier POC, random-access order) with no synchronisation in between: every
+    batch converts against the list as it was when the batch was issued.  Three versions, so the
+    first table is reused by the third refresh (which must wait for the first batch)."""
+    from test_mvp import ALL as MVP_ALL
+    params = mm360.seq_params(2048, 1024, MVP_ALL)
+    q = W.mvp_queries(2048, 1024, MVP_ALL, 120000, seed=8)
+    cam = (q["model_orig"] == mm360.GEODESIC_CAMPOSE) | (q["model_desired"] == mm360.GEODESIC_CAMPOSE)
+    q["cur_poc_orig"][cam] = W.CUR_POC
+    q["cur_poc_desired"][cam] = W.CUR_POC
+    versions = [[(W.CUR_POC, -1, (0, 11863283, 11863283))],
+                [(W.CUR_POC, -1, (0, 11863283, 11863283)), (2, 0, (1 << 24, 0, 0))],
+                [(W.CUR_POC, -1, (0, 11863283, 11863283)), (2, 0, (1 << 24, 0, 0)), (W.CUR_POC, 0, (0, 1 << 24, 0))]]
+    wants = [Oracle(params, v).mvp(q) for v in versions]
+    side = torch.cuda.Stream()
+    with _ctx(params, versions[0]) as ctx:
+        ctx.set_mvp_stream(side.cuda_stream)
+        d_q = mm360.queries_to_device(q)
+        torch.cuda.synchronize()
+        outs = [torch.zeros((len(q), 2), dtype=torch.int32, device="cuda") for _ in versions]
+        for k, v in enumerate(versions):
+            if k:
+                cur, ref, qq = v[-1]
+                ctx.set_epipole(cur, ref, qq)  # sorts before (W.CUR_POC, -1)
+            ctx.mvp_convert_device(d_q, outs[k])
+        ctx.mvp_status()
+        for k in range(len(versions)):
+            got = outs[k].cpu().numpy()
+            assert np.array_equal(got, wants[k]), (k, np.argwhere((got != wants[k]).any(axis=1))[:5])
+    assert not np.array_equal(wants[0], wants[2])  # the versions convert differently
+
+
+def test_mvp_status_sticky_over_calls():
+    """A failing conversion followed by a clean one, with no status read in between: the next
+    mm_mvp_status still reports the failure (the status word accumulates until it is read)."""
+    from test_mvp import ALL as MVP_ALL, EPI2
+    params = mm360.seq_params(256, 128, MVP_ALL)
+    q = W.mvp_queries(256, 128, MVP_ALL, 3000, seed=12)
+    bad = q.copy()
+    bad["shift_ver"][1234] = 9
+    with _ctx(params, EPI2) as ctx:
+        d_out = torch.zeros((len(q), 2), dtype=torch.int32, device="cuda")
+        ctx.mvp_convert_device(mm360.queries_to_device(bad), d_out)
+        ctx.mvp_convert_device(mm360.queries_to_device(q), d_out)
+        ctx.mvp_convert_device(mm360.queries_to_device(q), d_out)
+        with pytest.raises(mm360.MMError) as e:
+            ctx.mvp_status()
+        assert e.value.code == mm360.MM_ERR_ARG and "MVP query 1234" in str(e.value), str(e.value)
+        ctx.mvp_convert_device(mm360.queries_to_device(q), d_out)
+        ctx.mvp_status()  # read and cleared: clean again
+        assert np.array_equal(d_out.cpu().numpy(), Oracle(params, EPI2).mvp(q))
 
 
 @pytest.mark.parametrize("plan_ahead", [False, True])

@@ -49,3 +49,41 @@ def test_mvp_early_returns_and_errors():
     params2 = mm360.seq_params(256, 128, W.MPA3)
     with pytest.raises(RuntimeError, match="5"):  # model not active
         twin.mvp(params2, q, EPI2)
+
+
+@pytest.mark.parametrize("w,h,flavor", [(256, 128, 1), (2048, 1024, 1), (6144, 3072, 1), (2048, 1024, 0)])
+def test_host_mvp_matches_oracle(w, h, flavor):
+    """mm_mvp_convert_host (the product library's host form, for the spatial candidates VTM converts
+    in decoding order) equals the oracle query by query, without a GPU."""
+    params = mm360.seq_params(w, h, ALL, ged_flavor=flavor)
+    q = W.mvp_queries(w, h, ALL, 3000, seed=7 * w + flavor)
+    want = Oracle(params, EPI2).mvp(q)
+    epi = mm360.EpipoleList()
+    for cur, ref, q24 in EPI2:
+        epi.add(cur, ref, q24, make_available=True)
+    got = mm360.mvp_convert_host(params, q, epi)
+    bad = np.argwhere((got != want).any(axis=1))[:, 0]
+    assert len(bad) == 0, [(int(i), q[i], got[i], want[i]) for i in bad[:3]]
+    # one query per call (the decoder's per-candidate use) gives the same MVs
+    one = np.concatenate([mm360.mvp_convert_host(params, q[i:i + 1], epi) for i in range(0, 200)])
+    assert (one == want[:200]).all()
+
+
+def test_host_mvp_errors_and_epipole_refresh():
+    params = mm360.seq_params(256, 128, ALL)
+    q = W.mvp_queries(256, 128, ALL, 64, seed=3)
+    q["model_orig"][10] = mm360.GEODESIC_CAMPOSE
+    q["model_desired"][10] = mm360.ROTATIONAL
+    q["mv_hor"][10] = 37
+    epi = mm360.EpipoleList()
+    with pytest.raises(mm360.MMError) as e:  # no epipoles at all
+        mm360.mvp_convert_host(params, q, epi)
+    assert e.value.code == mm360.MM_ERR_NOEPIPOLE
+    # adding the epipoles afterwards refreshes the host table (list version)
+    for cur, ref, q24 in EPI2:
+        epi.add(cur, ref, q24, make_available=True)
+    want = Oracle(params, EPI2).mvp(q)
+    assert (mm360.mvp_convert_host(params, q, epi) == want).all()
+    with pytest.raises(mm360.MMError) as e:  # model not active
+        mm360.mvp_convert_host(mm360.seq_params(256, 128, W.MPA3), q, epi)
+    assert e.value.code == mm360.MM_ERR_MODEL

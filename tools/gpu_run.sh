@@ -18,6 +18,10 @@ run() {  # name limit cmd...
 for step in "$@"; do
   case $step in
     tests) run gpu_tests 900 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread ;;
+    race_probe) run race_probe 900 env MM360_LIB=tmp_variants/probe/libmm360.so python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread ;;
+    abb=*)  # abb=<rounds>=<v1,v2,...>: alternating headline runs of library variants (default = in-tree)
+      rounds=$(echo "$step" | cut -d= -f2); vs=$(echo "$step" | cut -d= -f3 | tr ',' ' ')
+      run "abb_$(echo "$vs" | tr ' ' '_')" 900 bash tools/ab_bench.sh "$rounds" $vs ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     bench_c4) run bench_c4 600 python bench.py --config C4 ;;

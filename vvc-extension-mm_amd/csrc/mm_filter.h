@@ -264,6 +264,10 @@ struct PtrRows {
     typedef uint32_t u2 __attribute__((ext_vector_type(2), aligned(4)));
     typedef uint32_t u3 __attribute__((ext_vector_type(3), aligned(4)));
     const char* p = base + (long)r * row_bytes;
+#if defined(MM_PROBE_NOLOAD)  // timing probe (wrong results): the window's words without the load
+    for (int k = 0; k < ND; k++) d[k] = (uint32_t)(size_t)p + 0x10001u * k;
+    return;
+#endif
     if constexpr (ND == 6) {
       const u4 a = *reinterpret_cast<const u4*>(p);
       const u2 b = *reinterpret_cast<const u2*>(p + 16);
@@ -301,6 +305,21 @@ __device__ __forceinline__ void predict_rows(const Rows& rows, const uint32_t* _
   }
 #pragma unroll
   for (int k = 0; k < NP; k++) ve[k] = vt[k];
+#if defined(MM_PROBE_NOFILTER)  // timing probe (wrong results): the window loads without the filter
+  {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      uint32_t d[ND];
+      rows.template load<ND>(r, d);
+#pragma unroll
+      for (int k = 0; k < ND; k++) acc ^= d[k];
+    }
+#pragma unroll
+    for (int i = 0; i < SBW * SBH; i++) out[i] = (int16_t)(acc >> (i & 15));
+    return;
+  }
+#endif
   uint32_t tmp[R + 1][SBW];  // H outputs; only the low 16 bits are used
 #pragma unroll
   for (int c = 0; c < SBW; c++) tmp[R][c] = 0u;

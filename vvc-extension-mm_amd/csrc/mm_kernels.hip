@@ -130,8 +130,8 @@ __global__ void __launch_bounds__(PLAN_BLOCK) k_plan_count(const mm_pu_desc* __r
                                                     unsigned long long* __restrict__ blkq, int n_quarters) {
   __shared__ unsigned long long s_cnt[PLAN_Q][N_KEYS], s_status;
   const int tid = threadIdx.x, q = tid / PLACE_BLOCK;
-  for (int k = tid; k < PLAN_Q * N_KEYS; k += PLAN_BLOCK) (&s_cnt[0][0])[k] = 0;
-  if (tid == 0) s_status = 0;
+  for (int k = tid; k < PLAN_Q * N_KEYS; k += PLAN_BLOCK) lds_put((&s_cnt[0][0])[k], 0ull, 0ull);
+  if (tid == 0) lds_put(s_status, 0ull, 0ull);
   __syncthreads();
   const int i = blockIdx.x * blockDim.x + tid;
   if (i < n) {
@@ -178,7 +178,7 @@ __global__ void __launch_bounds__(PLACE_BLOCK) k_plan_place(const mm_pu_desc* __
   __shared__ int s_ok;
   const int tid = threadIdx.x;
   if (blockIdx.x == 0 && tid == 0 && next_status) *next_status = 0ull;
-  if (tid < N_JOB_KEYS) s_job[tid] = 0;
+  if (tid < N_JOB_KEYS) lds_put(s_job[tid], 0ull, 0ull);
   // bucket totals and this quarter's offsets inside the buckets: the column sums of blk, split
   // over the block's 4 waves (wave w takes count rows w, w + 4, ...), plus the quarters before this
   // one in its count block (blkq), combined through LDS
@@ -198,8 +198,8 @@ __global__ void __launch_bounds__(PLACE_BLOCK) k_plan_place(const mm_pu_desc* __
           if (b < b0) pp += v;
         }
         if (q0 + w < (int)blockIdx.x) pp += blkq[(long)(q0 + w) * N_KEYS + key];  // PLAN_Q == NWAVE
-        s_ptot[w][key] = tp;
-        s_ppre[w][key] = pp;
+        lds_put(s_ptot[w][key], tp, 0ull);
+        lds_put(s_ppre[w][key], pp, 0ull);
       }
     }
   }
@@ -213,17 +213,17 @@ __global__ void __launch_bounds__(PLACE_BLOCK) k_plan_place(const mm_pu_desc* __
       pre += s_ppre[w][tid];
     }
     if (tid < N_PU_KEYS)
-      g_pu[tid] = pre;
+      lds_put(g_pu[tid], pre, 0ull);
     else if (tid < DMVR_KEY)
-      g_job[tid - N_PU_KEYS] = pre;
+      lds_put(g_job[tid - N_PU_KEYS], pre, 0ull);
     else
-      g_dm = pre;
+      lds_put(g_dm, pre, 0ull);
   }
   // PlanMeta = exclusive prefix of the bucket totals: the job buckets are one wave (lanes 6..69
   // are threads N_PU_KEYS..N_KEYS-1, scanned in two waves' halves through LDS), the PU buckets
   // are few
   __shared__ unsigned long long s_tot[N_KEYS];
-  if (tid < N_KEYS) s_tot[tid] = tot;
+  if (tid < N_KEYS) lds_put(s_tot[tid], tot, 0ull);
   __syncthreads();
   static_assert(N_JOB_KEYS == 64, "one lane per job bucket");
   if (tid < 64) {
@@ -238,35 +238,43 @@ __global__ void __launch_bounds__(PLACE_BLOCK) k_plan_place(const mm_pu_desc* __
         se += ue;
       }
     }
-    s_meta.job_base[tid] = si - items;
-    s_meta.elem_base[tid] = se - elems;
+    lds_put(s_meta.job_base[tid], si - items, 0);
+    lds_put(s_meta.elem_base[tid], se - elems, 0);
     if (tid == 63) {
-      s_meta.n_jobs = si;
-      s_meta.n_elems = se;
+      lds_put(s_meta.n_jobs, si, 0);
+      lds_put(s_meta.n_elems, se, 0);
     }
     if (tid == 0) {
-      int acc = 0, sacc = 0;
+      int acc = 0, sacc = 0, pb[N_PU_KEYS], sbb[N_PU_KEYS], band[N_BANDS + 1];
 #pragma unroll
       for (int k = 0; k < N_PU_KEYS; k++) {
-        s_meta.pu_base[k] = acc;
-        s_meta.sb_base[k] = sacc;
+        pb[k] = acc;
+        sbb[k] = sacc;
         acc += packed_items(s_tot[k]);
         sacc += packed_elems(s_tot[k]);
       }
-      s_meta.n_pus = acc;
-      s_meta.n_sb = sacc;
-      band_cut(s_meta.sb_base, sacc, s_meta.band);
-      s_meta.n_sub = packed_items(s_tot[DMVR_KEY]);
-      s_meta.n_dmvr_elems = packed_elems(s_tot[DMVR_KEY]);
+      band_cut(sbb, sacc, band);
+#pragma unroll
+      for (int k = 0; k < N_PU_KEYS; k++) {
+        lds_put(s_meta.pu_base[k], pb[k], 0);
+        lds_put(s_meta.sb_base[k], sbb[k], 0);
+      }
+#pragma unroll
+      for (int r = 0; r <= N_BANDS; r++) lds_put(s_meta.band[r], band[r], 0);
+      lds_put(s_meta.n_pus, acc, 0);
+      lds_put(s_meta.n_sb, sacc, 0);
+      lds_put(s_meta.n_sub, packed_items(s_tot[DMVR_KEY]), 0);
+      lds_put(s_meta.n_dmvr_elems, packed_elems(s_tot[DMVR_KEY]), 0);
     }
   }
   __syncthreads();
   if (tid == 0) {
-    s_ok = s_meta.n_pus <= caps.pus && s_meta.n_sb <= caps.sb && s_meta.n_jobs <= caps.jobs &&
+    const int ok = s_meta.n_pus <= caps.pus && s_meta.n_sb <= caps.sb && s_meta.n_jobs <= caps.jobs &&
            s_meta.n_elems <= caps.elems && s_meta.n_sub <= caps.subs && s_meta.n_dmvr_elems <= caps.dmvr_elems;
+    lds_put(s_ok, ok, 0);
     if (blockIdx.x == 0) {
       PlanMeta m = s_meta;
-      if (!s_ok) {  // over capacity (overlapping PUs): nothing is predicted, the call fails
+      if (!ok) {  // over capacity (overlapping PUs): nothing is predicted, the call fails
         m.n_pus = m.n_sb = m.n_jobs = m.n_elems = m.n_sub = m.n_dmvr_elems = 0;
         for (int r = 0; r <= N_BANDS; r++) m.band[r] = 0;
         atomicMax(status, status_word(0, MM_ERR_ARG));
@@ -310,7 +318,7 @@ __global__ void __launch_bounds__(PLACE_BLOCK) k_plan_place(const mm_pu_desc* __
         const unsigned long long a = __shfl_up(inc, d);
         if (lane >= d) inc += a;
       }
-      if (lane == 63) s_wsum[k][w] = inc;
+      if (lane == 63) lds_put(s_wsum[k][w], inc, 0ull);
       if (ok && p.key == k) mine = inc - vk;
     }
 #pragma unroll
@@ -318,7 +326,7 @@ __global__ void __launch_bounds__(PLACE_BLOCK) k_plan_place(const mm_pu_desc* __
       const unsigned long long b = __shfl_up(incd, d);
       if (lane >= d) incd += b;
     }
-    if (lane == 63) s_wsum[N_PU_KEYS][w] = incd;
+    if (lane == 63) lds_put(s_wsum[N_PU_KEYS][w], incd, 0ull);
     __syncthreads();
     unsigned long long before = 0, befd = 0;
     for (int k = 0; k < w; k++) {
@@ -355,14 +363,18 @@ __global__ void __launch_bounds__(256) k_setup_dev(SeqConst sc, const PlanMeta* 
                                                    BlockSetup* __restrict__ out) {
   static_assert(sizeof(BlockSetup) % 8 == 0, "BlockSetup image is copied in 8-byte words");
   __shared__ alignas(16) BlockSetup s_set[256];
-  __shared__ M3 s_ged[3 + MAX_SLOTS];  // indexed per lane: staged with scalar loads (stage_arg_words)
+  __shared__ M3 s_ged[3 + MAX_SLOTS];  // indexed per lane: staged by stage_arg_words
   const int n_jobs = meta->n_jobs;
   const int base = blockIdx.x * 256;
   if (base >= n_jobs) return;
   stage_arg_words<sizeof(s_ged) / 4>(reinterpret_cast<const uint32_t*>(t.ged), reinterpret_cast<uint32_t*>(s_ged));
   __syncthreads();
   const int i = base + threadIdx.x;
-  if (i < n_jobs) setup_job(jobs[i], sc, s_ged, &s_set[threadIdx.x]);
+  if (i < n_jobs) {
+    BlockSetup b;
+    setup_job(jobs[i], sc, s_ged, &b);
+    lds_put(s_set[threadIdx.x], b, BlockSetup{});
+  }
   __syncthreads();
   const int cnt = min(256, n_jobs - base);
   const int words = cnt * (int)(sizeof(BlockSetup) / 8);
@@ -412,7 +424,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k
   const int first = b0 + (int)(blockIdx.x >> 3) * 256;
   if (first >= b1) return;  // whole workgroup past the band's end
   if (threadIdx.x < sizeof(PackedTaps) / 16)
-    reinterpret_cast<uint4*>(&s_taps)[threadIdx.x] = reinterpret_cast<const uint4*>(&c_packed_taps)[threadIdx.x];
+    lds_put(reinterpret_cast<uint4*>(&s_taps)[threadIdx.x], reinterpret_cast<const uint4*>(&c_packed_taps)[threadIdx.x], make_uint4(~0u, ~0u, ~0u, ~0u));
   stage_ref_table<MAX_SLOTS>(t.pool_slot4, t.pool, s_ref);
   __syncthreads();
   const Taps taps{c_luma_taps, c_chroma_taps, &s_taps, t.pool};
@@ -449,7 +461,7 @@ using namespace mmme;
 
 __global__ void __launch_bounds__(256) k_me_setup(SeqConst sc, MeWindow w, const MeBlockDev* __restrict__ blocks,
                                                   int n_jobs, const PicTables t, BlockSetup* __restrict__ out) {
-  __shared__ M3 s_ged[3 + MAX_SLOTS];  // indexed per lane: staged with scalar loads (stage_arg_words)
+  __shared__ M3 s_ged[3 + MAX_SLOTS];  // indexed per lane: staged by stage_arg_words
   stage_arg_words<sizeof(s_ged) / 4>(reinterpret_cast<const uint32_t*>(t.ged), reinterpret_cast<uint32_t*>(s_ged));
   __syncthreads();
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -483,7 +495,7 @@ __global__ void __launch_bounds__(256) k_me_sad(SeqConst sc, Geometry geo, MeWin
                                                 int n_elems, const BlockSetup* __restrict__ setups, MpaCache cache,
                                                 const PicTables t, const int16_t* __restrict__ org, int org_stride,
                                                 uint32_t* __restrict__ sads) {
-  __shared__ RefDev s_ref[MAX_SLOTS];  // indexed per lane: rebuilt from scalar loads (stage_ref_table)
+  __shared__ RefDev s_ref[MAX_SLOTS];  // indexed per lane: staged by stage_ref_table
   stage_ref_table<MAX_SLOTS>(t.pool_slot4, t.pool, s_ref);
   __syncthreads();
   const int g = xcd_block() * blockDim.x + threadIdx.x;
@@ -530,7 +542,7 @@ struct DmvrWork {
 __global__ void __launch_bounds__(256) k_dmvr_setup_dev(SeqConst sc, const PlanMeta* __restrict__ meta,
                                                         const SubPuDev* __restrict__ sp, const PicTables t,
                                                         BlockSetup* __restrict__ out, unsigned long long* __restrict__ count) {
-  __shared__ M3 s_ged[3 + MAX_SLOTS];  // indexed per lane: staged with scalar loads (stage_arg_words)
+  __shared__ M3 s_ged[3 + MAX_SLOTS];  // indexed per lane: staged by stage_arg_words
   stage_arg_words<sizeof(s_ged) / 4>(reinterpret_cast<const uint32_t*>(t.ged), reinterpret_cast<uint32_t*>(s_ged));
   __syncthreads();
   if (blockIdx.x == 0 && threadIdx.x == 0) *count = 0ull;
@@ -554,13 +566,13 @@ __global__ void __launch_bounds__(256) k_dmvr_centre_dev(SeqConst sc, Geometry g
                                                          int32_t* __restrict__ mvd) {
 #if defined(__HIP_DEVICE_COMPILE__)  // device-only filter paths (mm_filter.h predict_rows02, PtrRows)
   __shared__ PackedTaps s_taps;
-  __shared__ RefDev s_ref[MAX_SLOTS];  // indexed per lane: rebuilt from scalar loads (stage_ref_table)
+  __shared__ RefDev s_ref[MAX_SLOTS];  // indexed per lane: staged by stage_ref_table
   __shared__ int s_items[8], s_pre[8], s_base[2];
   const int tid = threadIdx.x;
   if (tid < sizeof(PackedTaps) / 16)
-    reinterpret_cast<uint4*>(&s_taps)[tid] = reinterpret_cast<const uint4*>(&c_packed_taps)[tid];
+    lds_put(reinterpret_cast<uint4*>(&s_taps)[tid], reinterpret_cast<const uint4*>(&c_packed_taps)[tid], make_uint4(~0u, ~0u, ~0u, ~0u));
   stage_ref_table<MAX_SLOTS>(t.pool_slot4, t.pool, s_ref);
-  if (tid < 8) s_items[tid] = 0;
+  if (tid < 8) lds_put(s_items[tid], 0, 0);
   __syncthreads();
   const int n_sub = meta->n_sub;
   const RefPool pool = t.pool;
@@ -600,7 +612,7 @@ __global__ void __launch_bounds__(256) k_dmvr_centre_dev(SeqConst sc, Geometry g
       const bool survives = v - (v >> 2) >= (uint32_t)(u.w * u.h);
       items = survives ? 2 * (N_OFF - 1) * u.n : 0;
       if (!survives) dmvr_apply(s, u, 0, 0, jobs, mvd);  // notZeroCost = false: no refinement (:2520-2525)
-      s_items[slot] = items;
+      lds_put(s_items[slot], items, 0);
     }
     __syncthreads();
     if (tid == 0) {
@@ -608,14 +620,14 @@ __global__ void __launch_bounds__(256) k_dmvr_centre_dev(SeqConst sc, Geometry g
 #pragma unroll
       for (int k = 0; k < 8; k++) {
         const int it = (base + 32 * k < n_sub * 32) ? s_items[k] : 0;
-        s_pre[k] = (ns << 20) | ni;  // survivors before, items before (< 2^20 per workgroup)
+        lds_put(s_pre[k], (ns << 20) | ni, 0);  // survivors before, items before (< 2^20 per workgroup)
         ni += it;
         ns += it ? 1 : 0;
       }
       unsigned long long old = 0;
       if (ns) old = atomicAdd(w.count, ((unsigned long long)ns << 32) | (unsigned long long)ni);
-      s_base[0] = (int)(old >> 32);
-      s_base[1] = (int)(old & 0xffffffffull);
+      lds_put(s_base[0], (int)(old >> 32), 0);
+      lds_put(s_base[1], (int)(old & 0xffffffffull), 0);
     }
     __syncthreads();
     if (items) {
@@ -682,7 +694,7 @@ __global__ void __launch_bounds__(DMVR_SEARCH_WG) __attribute__((amdgpu_waves_pe
   const int tid = threadIdx.x, lane = tid & 63;
   static_assert(sizeof(PackedTaps) % 16 == 0 && sizeof(PackedTaps) / 16 <= DMVR_SEARCH_WG, "one 16-byte word per thread");
   if (tid < sizeof(PackedTaps) / 16)
-    reinterpret_cast<uint4*>(&s_taps)[tid] = reinterpret_cast<const uint4*>(&c_packed_taps)[tid];
+    lds_put(reinterpret_cast<uint4*>(&s_taps)[tid], reinterpret_cast<const uint4*>(&c_packed_taps)[tid], make_uint4(~0u, ~0u, ~0u, ~0u));
   const int n_surv = (int)(*w.count >> 32);
   const RefPool pool = t.pool;
   // items alternate lists and the stride is even, so every item of a thread has the list tid & 1
@@ -694,15 +706,15 @@ __global__ void __launch_bounds__(DMVR_SEARCH_WG) __attribute__((amdgpu_waves_pe
     const int slot0 = __builtin_amdgcn_readfirstlane(u.slot[0]), slot1 = __builtin_amdgcn_readfirstlane(u.slot[1]);
     const uint32_t off_y[2] = {t.ref[slot0].off_y, t.ref[slot1].off_y};
     const int stride_y[2] = {t.ref[slot0].stride_y, t.ref[slot1].stride_y};
-    if (tid < 8) (&s_box[0][0])[tid] = (tid & 1) ? INT_MIN : INT_MAX;
-    if (tid == 0) s_cost[N_OFF / 2] = w.ccost[s];
+    if (tid < 8) lds_put((&s_box[0][0])[tid], (tid & 1) ? INT_MIN : INT_MAX, 0);
+    if (tid == 0) lds_put(s_cost[N_OFF / 2], w.ccost[s], 0u);
     __syncthreads();  // s_taps staged; the previous sub-PU's LDS reads and decision are done
     // 1. positions of the (offset, sub-block, list) items and the in-range box of this thread's list
     int xmin = INT_MAX, xmax = INT_MIN, ymin = INT_MAX, ymax = INT_MIN;
     const mm_int2* src_pos = pos + w.surv_base[k];
     for (int i = tid; i < n_items; i += DMVR_SEARCH_WG) {
       const mm_int2 q = src_pos[i];
-      s_pos[i] = q;
+      lds_put(s_pos[i], q, mm_int2{INT_MAX, INT_MAX});
       const int xPos = q.x >> 4, yPos = q.y >> 4;
       if (!sb_out_of_range(xPos, yPos, geo.W, geo.H, geo.maxCUw, geo.maxCUh, 4, 4)) {
         xmin = min(xmin, xPos);
@@ -742,7 +754,7 @@ __global__ void __launch_bounds__(DMVR_SEARCH_WG) __attribute__((amdgpu_waves_pe
           typedef uint32_t u4a4 __attribute__((ext_vector_type(4), aligned(4)));
           const u4a4 q = *reinterpret_cast<const u4a4*>(src + ((long)r * stride_y[l] + 8 * c) * 2);
           uint32_t* d = &s_win[l][r * DMVR_WIN_STRIDE + 4 * c];
-          d[0] = q.x;
+          lds_put(d[0], q.x, ~0u);
           d[1] = q.y;
           d[2] = q.z;
           d[3] = q.w;
@@ -778,7 +790,7 @@ __global__ void __launch_bounds__(DMVR_SEARCH_WG) __attribute__((amdgpu_waves_pe
         v = dmvr_sad_rows02(p[0], p[1]);
       }
       for (int d = 1; d < n; d <<= 1) v += __shfl_xor(v, d);  // n-lane segments (n divides 64)
-      if (oe < (N_OFF - 1) * n && (oe & (n - 1)) == 0) s_cost[dmvr_outer_offset(oe >> log2n)] = v;
+      if (oe < (N_OFF - 1) * n && (oe & (n - 1)) == 0) lds_put(s_cost[dmvr_outer_offset(oe >> log2n)], v, 0u);
     }
     __syncthreads();
     // 4. the decision and the refined MVs
@@ -804,7 +816,7 @@ constexpr int MVP_BLOCK = 256;
 constexpr int MVP_KEYS = NUM_MODELS;
 __device__ __forceinline__ void mvp_regroup(int key, int* s_cnt, int* s_perm, int* n_work) {
   const int tid = threadIdx.x;
-  if (tid < MVP_KEYS) s_cnt[tid] = 0;
+  if (tid < MVP_KEYS) lds_put(s_cnt[tid], 0, 0);
   __syncthreads();
   int rank = 0;
   if (key >= 0) rank = atomicAdd(&s_cnt[key], 1);
@@ -813,13 +825,13 @@ __device__ __forceinline__ void mvp_regroup(int key, int* s_cnt, int* s_perm, in
     int acc = 0;
     for (int k = 0; k < MVP_KEYS; k++) {
       const int c = s_cnt[k];
-      s_cnt[k] = acc;
+      lds_put(s_cnt[k], acc, 0);
       acc += c;
     }
-    s_cnt[MVP_KEYS] = acc;
+    lds_put(s_cnt[MVP_KEYS], acc, 0);
   }
   __syncthreads();
-  if (key >= 0) s_perm[s_cnt[key] + rank] = tid;
+  if (key >= 0) lds_put(s_perm[s_cnt[key] + rank], tid, 0);
   __syncthreads();
   *n_work = s_cnt[MVP_KEYS];
 }
@@ -848,7 +860,7 @@ __global__ void __launch_bounds__(MVP_BLOCK) k_mvp_bucket(const mm_mvp_query* __
                                                           int* __restrict__ local) {
   __shared__ unsigned s_h[MVP_BINS], s_base[MVP_BINS];
   const int tid = threadIdx.x, i = blockIdx.x * MVP_BLOCK + tid, sub = blockIdx.x % MVP_SUBS;
-  for (int b = tid; b < MVP_BINS; b += MVP_BLOCK) s_h[b] = 0u;
+  for (int b = tid; b < MVP_BINS; b += MVP_BLOCK) lds_put(s_h[b], 0u, 0u);
   if (blockIdx.x == 0)
     for (int b = tid; b < MVP_COUNTERS; b += MVP_BLOCK) next_bins[b] = 0u;
   __syncthreads();
@@ -860,7 +872,7 @@ __global__ void __launch_bounds__(MVP_BLOCK) k_mvp_bucket(const mm_mvp_query* __
   }
   __syncthreads();
   for (int b = tid; b < MVP_BINS; b += MVP_BLOCK)
-    if (s_h[b]) s_base[b] = atomicAdd(&bins[b * MVP_SUBS + sub], s_h[b]);
+    if (s_h[b]) lds_put(s_base[b], atomicAdd(&bins[b * MVP_SUBS + sub], s_h[b]), 0u);
   __syncthreads();
   if (i < n) local[i] = (int)(s_base[key] + rank);
 }
@@ -869,7 +881,7 @@ __global__ void __launch_bounds__(MVP_BLOCK) k_mvp_place(const mm_mvp_query* __r
                                                          const int* __restrict__ local, int* __restrict__ perm) {
   __shared__ unsigned s_cnt[MVP_COUNTERS], s_key[MVP_BINS];
   const int tid = threadIdx.x, i = blockIdx.x * MVP_BLOCK + tid, sub = blockIdx.x % MVP_SUBS;
-  for (int k = tid; k < MVP_COUNTERS; k += MVP_BLOCK) s_cnt[k] = bins[k];
+  for (int k = tid; k < MVP_COUNTERS; k += MVP_BLOCK) lds_put(s_cnt[k], bins[k], 0u);
   __syncthreads();
   // this workgroup's counter of key b starts after the key's earlier counters (thread b) ...
   if (tid < MVP_BINS) {
@@ -879,15 +891,15 @@ __global__ void __launch_bounds__(MVP_BLOCK) k_mvp_place(const mm_mvp_query* __r
       if (j == sub) s_cnt[tid * MVP_SUBS] = acc;  // (slot j = 0 is read before it is overwritten)
       acc += c;
     }
-    s_key[tid] = acc;
+    lds_put(s_key[tid], acc, 0u);
   }
   __syncthreads();
-  // ... and after all earlier keys (one thread scans the 49 key totals)
+  // ... and after all earlier keys (one thread scans the MVP_BINS = 121 key totals)
   if (tid == 0) {
     unsigned acc = 0;
     for (int b = 0; b < MVP_BINS; b++) {
       const unsigned t = s_key[b];
-      s_key[b] = acc;
+      lds_put(s_key[b], acc, 0u);
       acc += t;
     }
   }
@@ -900,23 +912,21 @@ __global__ void __launch_bounds__(MVP_BLOCK) k_mvp_place(const mm_mvp_query* __r
 
 __global__ void __launch_bounds__(MVP_BLOCK) k_mvp_dev(SeqConst sc, const mm_mvp_query* __restrict__ q, int n,
                                                        const int* __restrict__ order, uint32_t active, mmmvp::EpiTable et,
-                                                       int32_t* __restrict__ out, unsigned long long* __restrict__ status,
-                                                       unsigned long long* __restrict__ next_status) {
+                                                       int32_t* __restrict__ out, unsigned long long* __restrict__ status) {
   using namespace mmmvp;
   __shared__ mm_mvp_query s_q[MVP_BLOCK];
   __shared__ float s_sx[MVP_BLOCK], s_sy[MVP_BLOCK];
   __shared__ int s_perm[MVP_BLOCK], s_cnt[MVP_KEYS + 1], s_ok[MVP_BLOCK], s_qi[MVP_BLOCK];
   __shared__ unsigned long long s_status;
   const int tid = threadIdx.x, i0 = blockIdx.x * MVP_BLOCK, i = i0 + tid;
-  if (tid == 0) s_status = 0;
-  if (blockIdx.x == 0 && tid == 0) *next_status = 0ull;
+  if (tid == 0) lds_put(s_status, 0ull, 0ull);
   __syncthreads();  // s_status is zeroed before any wave's atomicMax (waves 1-3 may run ahead of wave 0)
   int key = -1;
   if (i < n) {
     const int qi = order ? order[i] : i;  // the query this thread converts (model order)
-    s_qi[tid] = qi;
+    lds_put(s_qi[tid], qi, 0);
     const mm_mvp_query x = q[qi];
-    s_q[tid] = x;
+    lds_put(s_q[tid], x, mm_mvp_query{});
     int32_t o[2] = {0, 0};
     int code = mvp_validate(x, active);
     if (code == MM_OK && !mvp_early(x, et, o, &code)) key = x.model_orig;
@@ -938,9 +948,9 @@ __global__ void __launch_bounds__(MVP_BLOCK) k_mvp_dev(SeqConst sc, const mm_mvp
       atomicMax(&s_status, status_word(qk, MM_ERR_NOEPIPOLE));
       out[2 * qk] = out[2 * qk + 1] = 0;
     }
-    s_sx[k] = sx;
+    lds_put(s_sx[k], sx, __int_as_float(0x7fc00000));
     s_sy[k] = sy;
-    s_ok[k] = ok ? 1 : 0;
+    lds_put(s_ok[k], ok ? 1 : 0, 0);
   }
   __syncthreads();
   const int key2 = (key >= 0 && s_ok[tid]) ? s_q[tid].model_desired : -1;
@@ -1005,21 +1015,23 @@ struct RefHost {
   int slot = -1;  // picture slot in the context's reference pool (-1: own allocation, e.g. originals)
 };
 
+struct mm_ctx;
+static void retire_buffer(mm_ctx* c, void* p);
+
 template <typename T>
 struct DevBuf {
   T* p = nullptr;
   size_t cap = 0;
   // fresh (optional): set when the buffer was (re)allocated by this call
-  hipError_t ensure(size_t n, bool* fresh = nullptr) {
+  hipError_t ensure(mm_ctx* c, size_t n, bool* fresh = nullptr) {
     if (fresh) *fresh = false;
     if (n <= cap && p) return hipSuccess;
-    // Growing replaces a buffer that work still queued on any of the context's streams may use
-    // (the host runs pictures ahead of the GPU): drain the device first.  Buffers only grow, so
-    // this happens a few times per context.
-    if (p) {
-      (void)hipDeviceSynchronize();
-      (void)hipFree(p);
-    }
+    // Growing replaces a buffer that work still queued on the context's streams may use (the host
+    // runs pictures ahead of the GPU).  Nothing waits here: the old allocation is retired behind
+    // events on the context's streams and freed once they have passed (retire_buffer / reap), so
+    // other contexts and streams of the process never stall on one context's growth.  Buffers only
+    // grow, so this happens a few times per context.
+    if (p) retire_buffer(c, p);
     p = nullptr;
     cap = 0;
     size_t want = std::max<size_t>(n, 1);
@@ -1082,6 +1094,10 @@ struct PlanSlot {
 struct mm_epipole_list {
   mmepi::EpipoleList* l;
   bool owned;
+  // mm_mvp_convert_host: the available entries in key order (the device table's layout), rebuilt
+  // when the list's version moves
+  std::vector<mmmvp::EpiDev> host;
+  unsigned long long host_version = ~0ull;
 };
 
 struct mm_ctx {
@@ -1147,8 +1163,14 @@ struct mm_ctx {
   DevBuf<int> d_dmvr_surv_s, d_dmvr_surv_base, d_dmvr_surv_tbase, d_dmvr_surv_tchunk;
   // MM-MVP: the device copy of the epipole list (refreshed when its version moves, staged through a
   // pinned buffer on the context stream), the host-buffer API's query / result buffers and the
-  // deferred status words (ping-pong: a call's block 0 zeroes the next call's word)
-  DevBuf<mmmvp::EpiDev> d_epi;
+  // deferred status word (sticky until mm_mvp_status reads it)
+  // Two device tables alternate per list version: a refresh writes the table the current version
+  // does not use, after the conversions that read it (two versions back) have completed on the MVP
+  // stream (ev_epi_done), so a refresh never rewrites a table an in-flight conversion reads.
+  DevBuf<mmmvp::EpiDev> d_epi[2];
+  int epi_buf = 0;                                   // table of the current version
+  bool epi_used[2] = {false, false};                 // ev_epi_done[b] recorded
+  hipEvent_t ev_epi_done[2] = {nullptr, nullptr};    // MVP-stream conversions reading table b are done
   mmmvp::EpiDev* h_epi = nullptr;
   size_t h_epi_cap = 0;
   hipEvent_t ev_epi = nullptr;
@@ -1159,11 +1181,10 @@ struct mm_ctx {
   bool epi_fresh = false;  // an epipole-table copy on the context stream the MVP stream has not waited for
   DevBuf<mm_mvp_query> d_mvp_q;
   DevBuf<int32_t> d_mvp_out;
-  DevBuf<unsigned long long> d_mvp_status;
+  DevBuf<unsigned long long> d_mvp_status;  // sticky: every conversion since the last mm_mvp_status
   DevBuf<unsigned> d_mvp_bins;  // 2 x MVP_COUNTERS key counters (alternating sorted calls)
   int mvp_sort_par = 0;
   DevBuf<int> d_mvp_local, d_mvp_perm;
-  int mvp_par = 0;
   bool mvp_pending = false;
   DevBuf<int> d_me_off, d_me_chunk;
   bool stage_timing = false;
@@ -1172,7 +1193,53 @@ struct mm_ctx {
   bool call_timing = true;
   bool timed = false;
   hipEvent_t ev_stage[3] = {nullptr, nullptr, nullptr};  // after planning, setup, reprojection
+  // buffers replaced by DevBuf growth, freed once the events recorded on the context's streams at
+  // retirement have completed (reap: mm_synchronize, mm_destroy)
+  struct Retired {
+    void* p;
+    hipEvent_t ev[3];
+  };
+  std::vector<Retired> grave;
 };
+
+static hipStream_t mvp_stream_of(const mm_ctx* c) { return c->mvp_on_own ? c->mvp_stream : c->stream; }
+
+static void retire_buffer(mm_ctx* c, void* p) {
+  mm_ctx::Retired r{p, {nullptr, nullptr, nullptr}};
+  const hipStream_t ss[3] = {c->stream, c->aux, c->mvp_on_own ? c->mvp_stream : nullptr};
+  for (int k = 0; k < 3; k++) {
+    if (k > 0 && !ss[k]) continue;
+    if (hipEventCreateWithFlags(&r.ev[k], hipEventDisableTiming) != hipSuccess ||
+        hipEventRecord(r.ev[k], ss[k]) != hipSuccess) {
+      // cannot fence the old buffer: fall back to draining this context's streams
+      for (int j = 0; j < 3; j++)
+        if (j == 0 || ss[j]) (void)hipStreamSynchronize(ss[j]);
+      break;
+    }
+  }
+  c->grave.push_back(r);
+}
+
+// Frees the retired buffers whose fences have passed (all of them when `wait`).
+static void reap(mm_ctx* c, bool wait) {
+  std::vector<mm_ctx::Retired> keep;
+  for (auto& r : c->grave) {
+    bool done = true;
+    for (auto e : r.ev)
+      if (e && !wait && hipEventQuery(e) != hipSuccess) done = false;
+    if (!done) {
+      keep.push_back(r);
+      continue;
+    }
+    for (auto e : r.ev)
+      if (e) {
+        (void)hipEventSynchronize(e);
+        (void)hipEventDestroy(e);
+      }
+    (void)hipFree(r.p);
+  }
+  c->grave.swap(keep);
+}
 
 static int read_status(mm_ctx* c, int* first_bad);
 
@@ -1194,7 +1261,7 @@ static int fail(mm_ctx* c, int code, const std::string& msg) {
 
 template <typename T>
 static int upload(mm_ctx* c, DevBuf<T>& d, const std::vector<T>& h) {
-  HIPCHK(c, d.ensure(h.size()));
+  HIPCHK(c, d.ensure(c, h.size()));
   if (!h.empty()) HIPCHK(c, hipMemcpyAsync(d.p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, c->stream));
   return MM_OK;
 }
@@ -1217,8 +1284,8 @@ static int upload_jobs(mm_ctx* c) {
   RCCHK(upload(c, c->d_job_off, c->plan.job_off));
   RCCHK(upload(c, c->d_job_chunk, c->plan.job_chunk));
   RCCHK(upload(c, c->d_ged, c->plan.ged));
-  HIPCHK(c, c->d_setup.ensure(c->plan.jobs.size()));
-  HIPCHK(c, c->d_reproj.ensure(2 * (size_t)c->plan.n_elems));
+  HIPCHK(c, c->d_setup.ensure(c, c->plan.jobs.size()));
+  HIPCHK(c, c->d_reproj.ensure(c, 2 * (size_t)c->plan.n_elems));
   return MM_OK;
 }
 
@@ -1275,12 +1342,7 @@ int mm_create(const mm_seq_params* p, int device, mm_ctx** out_ctx) {
   mm_ctx* c = new mm_ctx();
   c->prm = *p;
   c->device = device;
-  c->sc.Wf = (float)p->width;
-  c->sc.Hf = (float)p->height;
-  c->sc.off = p->mm_offset4x4 == 4 ? 1.5f : (float)p->mm_offset4x4;
-  c->sc.focal = (float)(1. / std::tan(M_PI / p->height));  // Projection.h:127-130
-  c->sc.res = (float)(M_PI / p->height);                    // MVReprojection.cpp:27,33,39
-  c->sc.ged_flavor = p->ged_flavor;
+  c->sc = seq_const(*p);
   c->geo.W = p->width;
   c->geo.H = p->height;
   c->geo.chroma = p->chroma_format == 1;
@@ -1315,6 +1377,8 @@ int mm_create(const mm_seq_params* p, int device, mm_ctx** out_ctx) {
       hipEventCreateWithFlags(&c->ev_gate[1], GATE) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_plan, SYNC) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_epi, SYNC) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_epi_done[0], SYNC) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_epi_done[1], SYNC) != hipSuccess ||
       hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
       hipEventRecord(c->ev_gate[0], c->stream) != hipSuccess || hipEventRecord(c->ev_gate[1], c->stream) != hipSuccess) {
     mm_destroy(c);
@@ -1354,10 +1418,10 @@ int mm_create(const mm_seq_params* p, int device, mm_ctx** out_ctx) {
     tc.tan_grid = nullptr;
     hipLaunchKernelGGL(k_tan_grid, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, c->stream, c->sc, tc, c->tan_grid);
   }
-  if (c->d_status.ensure(2) != hipSuccess || hipMemsetAsync(c->d_status.p, 0, 2 * sizeof(unsigned long long), c->stream) != hipSuccess ||
-      c->d_mvp_status.ensure(2) != hipSuccess ||
-      hipMemsetAsync(c->d_mvp_status.p, 0, 2 * sizeof(unsigned long long), c->stream) != hipSuccess ||
-      c->d_mvp_bins.ensure(2 * MVP_COUNTERS) != hipSuccess ||
+  if (c->d_status.ensure(c, 2) != hipSuccess || hipMemsetAsync(c->d_status.p, 0, 2 * sizeof(unsigned long long), c->stream) != hipSuccess ||
+      c->d_mvp_status.ensure(c, 1) != hipSuccess ||
+      hipMemsetAsync(c->d_mvp_status.p, 0, sizeof(unsigned long long), c->stream) != hipSuccess ||
+      c->d_mvp_bins.ensure(c, 2 * MVP_COUNTERS) != hipSuccess ||
       hipMemsetAsync(c->d_mvp_bins.p, 0, 2 * MVP_COUNTERS * sizeof(unsigned), c->stream) != hipSuccess ||
       hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) {
     mm_destroy(c);
@@ -1405,17 +1469,20 @@ int mm_destroy(mm_ctx* c) {
   c->d_mvp_bins.release();
   c->d_mvp_local.release();
   c->d_mvp_perm.release();
-  c->d_epi.release();
+  for (int b = 0; b < 2; b++) {
+    c->d_epi[b].release();
+    if (c->ev_epi_done[b]) (void)hipEventDestroy(c->ev_epi_done[b]);
+  }
   if (c->h_epi) (void)hipHostFree(c->h_epi);
   if (c->ev_epi) (void)hipEventDestroy(c->ev_epi);
   c->d_me_off.release();
   c->d_me_chunk.release();
   for (auto& e : c->ev_stage)
     if (e) (void)hipEventDestroy(e);
-  if (c->aux) {
-    (void)hipStreamSynchronize(c->aux);
-    (void)hipStreamDestroy(c->aux);
-  }
+  if (c->aux) (void)hipStreamSynchronize(c->aux);
+  if (c->mvp_on_own) (void)hipStreamSynchronize(c->mvp_stream);
+  reap(c, true);
+  if (c->aux) (void)hipStreamDestroy(c->aux);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   for (auto& e : c->ev_gate)
@@ -1438,6 +1505,7 @@ int mm_synchronize(mm_ctx* c) {
   if (!c) return MM_ERR_ARG;
   const int rc = read_status(c, nullptr);
   const int rm = read_mvp_status(c, nullptr);
+  reap(c, false);
   return rc ? rc : rm;
 }
 
@@ -1711,43 +1779,43 @@ static int ensure_slot_buffers(mm_ctx* c, PlanSlot& S, int n, bool dmvr) {
   k.dmvr_elems = dmvr ? (int)std::min<long>((long)N_OFF * area_sb, (long)subs * N_OFF * 16) : 0;
   S.caps = k;
   if (dmvr) {
-    HIPCHK(c, S.dmvr_sub.ensure(k.subs));
-    HIPCHK(c, S.dmvr_off.ensure(k.subs));
-    HIPCHK(c, S.dmvr_chunk.ensure((size_t)k.dmvr_elems / 64 + 1));
-    HIPCHK(c, c->d_dmvr_setup.ensure((size_t)k.subs * N_OFF * 2));
-    HIPCHK(c, c->d_dmvr_mvd.ensure(2 * (size_t)k.subs));
-    HIPCHK(c, c->d_dmvr_pos.ensure(2 * (size_t)k.dmvr_elems));
-    HIPCHK(c, c->d_dmvr_count.ensure(1));
-    HIPCHK(c, c->d_dmvr_ccost.ensure(k.subs));
-    HIPCHK(c, c->d_dmvr_surv_s.ensure(k.subs));
-    HIPCHK(c, c->d_dmvr_surv_base.ensure(k.subs));
-    HIPCHK(c, c->d_dmvr_surv_tbase.ensure(k.subs));
-    HIPCHK(c, c->d_dmvr_surv_tchunk.ensure(2 * (size_t)k.dmvr_elems / 8 / 64 + 1));
+    HIPCHK(c, S.dmvr_sub.ensure(c, k.subs));
+    HIPCHK(c, S.dmvr_off.ensure(c, k.subs));
+    HIPCHK(c, S.dmvr_chunk.ensure(c, (size_t)k.dmvr_elems / 64 + 1));
+    HIPCHK(c, c->d_dmvr_setup.ensure(c, (size_t)k.subs * N_OFF * 2));
+    HIPCHK(c, c->d_dmvr_mvd.ensure(c, 2 * (size_t)k.subs));
+    HIPCHK(c, c->d_dmvr_pos.ensure(c, 2 * (size_t)k.dmvr_elems));
+    HIPCHK(c, c->d_dmvr_count.ensure(c, 1));
+    HIPCHK(c, c->d_dmvr_ccost.ensure(c, k.subs));
+    HIPCHK(c, c->d_dmvr_surv_s.ensure(c, k.subs));
+    HIPCHK(c, c->d_dmvr_surv_base.ensure(c, k.subs));
+    HIPCHK(c, c->d_dmvr_surv_tbase.ensure(c, k.subs));
+    HIPCHK(c, c->d_dmvr_surv_tchunk.ensure(c, 2 * (size_t)k.dmvr_elems / 8 / 64 + 1));
     S.dmvr_ensured = true;
   }
   bool fresh_jobs = false;
-  HIPCHK(c, S.jobs.ensure(k.jobs, &fresh_jobs));
+  HIPCHK(c, S.jobs.ensure(c, k.jobs, &fresh_jobs));
   if (fresh_jobs) HIPCHK(c, hipMemsetAsync(S.jobs.p, 0, S.jobs.cap * sizeof(JobDev), c->stream));
-  HIPCHK(c, S.job_off.ensure(k.jobs));
-  HIPCHK(c, S.job_chunk.ensure(k.elems / 64 + 1));
-  HIPCHK(c, S.setup.ensure(k.jobs));
-  HIPCHK(c, S.meta.ensure(1));
-  HIPCHK(c, S.blk.ensure((size_t)((n + PLAN_BLOCK - 1) / PLAN_BLOCK) * N_KEYS));
-  HIPCHK(c, S.blkq.ensure((size_t)((n + PLACE_BLOCK - 1) / PLACE_BLOCK) * N_KEYS));
+  HIPCHK(c, S.job_off.ensure(c, k.jobs));
+  HIPCHK(c, S.job_chunk.ensure(c, k.elems / 64 + 1));
+  HIPCHK(c, S.setup.ensure(c, k.jobs));
+  HIPCHK(c, S.meta.ensure(c, 1));
+  HIPCHK(c, S.blk.ensure(c, (size_t)((n + PLAN_BLOCK - 1) / PLAN_BLOCK) * N_KEYS));
+  HIPCHK(c, S.blkq.ensure(c, (size_t)((n + PLACE_BLOCK - 1) / PLACE_BLOCK) * N_KEYS));
   // The records k_reproj/k_mc exchange are zeroed once when allocated: every record a plan
   // counts is written before it is read (classify_pu decides counts and emission alike), and a
   // record that never was written still holds in-picture values (position 0, slot 0), never
   // uninitialised memory that k_mc would use as a destination offset.
   bool fresh = false;
-  HIPCHK(c, S.mc_meta.ensure(k.sb, &fresh));
+  HIPCHK(c, S.mc_meta.ensure(c, k.sb, &fresh));
   if (fresh) HIPCHK(c, hipMemsetAsync(S.mc_meta.p, 0, S.mc_meta.cap * sizeof(mm_int2), c->stream));
   for (int l = 0; l < 2; l++) {
-    HIPCHK(c, S.mc_lpos[l].ensure(k.sb, &fresh));
+    HIPCHK(c, S.mc_lpos[l].ensure(c, k.sb, &fresh));
     if (fresh) HIPCHK(c, hipMemsetAsync(S.mc_lpos[l].p, 0, S.mc_lpos[l].cap * sizeof(uint32_t), c->stream));
-    HIPCHK(c, S.mc_cpos[l].ensure(k.sb, &fresh));
+    HIPCHK(c, S.mc_cpos[l].ensure(c, k.sb, &fresh));
     if (fresh) HIPCHK(c, hipMemsetAsync(S.mc_cpos[l].p, 0, S.mc_cpos[l].cap * sizeof(uint32_t), c->stream));
     for (int q = 0; q < 2; q++) {  // touched only by the sub-blocks whose positions are far
-      HIPCHK(c, S.mc_far[l][q].ensure(k.sb, &fresh));
+      HIPCHK(c, S.mc_far[l][q].ensure(c, k.sb, &fresh));
       if (fresh) HIPCHK(c, hipMemsetAsync(S.mc_far[l][q].p, 0, S.mc_far[l][q].cap * sizeof(mm_int2), c->stream));
     }
   }
@@ -2005,7 +2073,7 @@ int mm_pred_prepare(mm_ctx* c, int cur_poc, const mm_pu_desc* pus, int n) {
   if (!c || n < 0 || (n > 0 && !pus)) return MM_ERR_ARG;
   HIPCHK(c, hipSetDevice(c->device));
   c->prepared = false;
-  HIPCHK(c, c->d_pu_in.ensure(n));
+  HIPCHK(c, c->d_pu_in.ensure(c, n));
   if (n) HIPCHK(c, hipMemcpyAsync(c->d_pu_in.p, pus, (size_t)n * sizeof(mm_pu_desc), hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->prep_poc = cur_poc;
@@ -2091,10 +2159,10 @@ int mm_sad_window(mm_ctx* c, int cur_poc, const mm_me_block* blocks, int n, int 
     RCCHK(upload(c, c->d_me_blocks, bt.blocks));
     RCCHK(upload(c, c->d_me_off, bt.blk_off));
     const long n_chunks = (bt.n_elems + 63) / 64;
-    HIPCHK(c, c->d_me_chunk.ensure((size_t)std::max<long>(n_chunks, 1)));
+    HIPCHK(c, c->d_me_chunk.ensure(c, (size_t)std::max<long>(n_chunks, 1)));
     hipLaunchKernelGGL(k_me_chunks, dim3((unsigned)((n_chunks + 255) / 256)), dim3(256), 0, c->stream, c->d_me_off.p,
                        (int)bt.blocks.size(), bt.n_elems, c->d_me_chunk.p);
-    HIPCHK(c, c->d_setup.ensure(bt.n_jobs));
+    HIPCHK(c, c->d_setup.ensure(c, bt.n_jobs));
     hipLaunchKernelGGL(k_me_setup, dim3((bt.n_jobs + 255) / 256), dim3(256), 0, c->stream, c->sc, w, c->d_me_blocks.p,
                        bt.n_jobs, t, c->d_setup.p);
     const int ne = (int)bt.n_elems;
@@ -2142,6 +2210,13 @@ static int sync_epi_table(mm_ctx* c) {
   std::vector<mmmvp::EpiDev> e;
   epi_entries(c->epipoles, &e);
   HIPCHK(c, hipEventSynchronize(c->ev_epi));  // the staging buffer may still feed the previous copy
+  const int nb = c->epi_buf ^ 1;                // the table the current version does not use
+  // its last readers (conversions of two versions back, on the MVP stream) must be done before the
+  // context stream rewrites it; conversions on the context stream itself are ordered anyway
+  if (c->epi_used[nb]) {
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_epi_done[nb], 0));
+    c->epi_used[nb] = false;
+  }
   if (e.size() > c->h_epi_cap) {
     if (c->h_epi) (void)hipHostFree(c->h_epi);
     c->h_epi = nullptr;
@@ -2150,29 +2225,36 @@ static int sync_epi_table(mm_ctx* c) {
     HIPCHK(c, hipHostMalloc(reinterpret_cast<void**>(&c->h_epi), cap * sizeof(mmmvp::EpiDev), hipHostMallocDefault));
     c->h_epi_cap = cap;
   }
-  if (e.size() > c->d_epi.cap || !c->d_epi.p) {
-    HIPCHK(c, hipStreamSynchronize(c->stream));  // growth frees the buffer queued kernels read
-    HIPCHK(c, c->d_epi.ensure(std::max<size_t>(64, 2 * e.size())));
-  }
+  HIPCHK(c, c->d_epi[nb].ensure(c, std::max<size_t>(64, 2 * e.size())));  // growth retires the old table
   if (!e.empty()) {
     std::copy(e.begin(), e.end(), c->h_epi);
-    HIPCHK(c, hipMemcpyAsync(c->d_epi.p, c->h_epi, e.size() * sizeof(mmmvp::EpiDev), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_epi[nb].p, c->h_epi, e.size() * sizeof(mmmvp::EpiDev), hipMemcpyHostToDevice,
+                             c->stream));
     HIPCHK(c, hipEventRecord(c->ev_epi, c->stream));
     c->epi_fresh = true;
   }
+  // the previous version's table: its readers are the conversions issued on the MVP stream so far
+  if (c->mvp_on_own) {
+    HIPCHK(c, hipEventRecord(c->ev_epi_done[c->epi_buf], c->mvp_stream));
+    c->epi_used[c->epi_buf] = true;
+  }
+  c->epi_buf = nb;
   c->epi_n = (int)e.size();
   c->epi_version = c->epipoles.version();
   return MM_OK;
 }
 
-static hipStream_t mvp_stream_of(const mm_ctx* c) { return c->mvp_on_own ? c->mvp_stream : c->stream; }
 static int read_mvp_status(mm_ctx* c, int* first_bad) {
   if (first_bad) *first_bad = -1;
   HIPCHK(c, hipStreamSynchronize(mvp_stream_of(c)));
   if (!c->mvp_pending) return MM_OK;
   c->mvp_pending = false;
   unsigned long long w = 0;
-  HIPCHK(c, hipMemcpy(&w, c->d_mvp_status.p + (c->mvp_par ^ 1), sizeof(w), hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(&w, c->d_mvp_status.p, sizeof(w), hipMemcpyDeviceToHost));
+  if (w) {  // sticky word: cleared only here, after the conversions that may have set it are done
+    HIPCHK(c, hipMemsetAsync(c->d_mvp_status.p, 0, sizeof(w), mvp_stream_of(c)));
+    HIPCHK(c, hipStreamSynchronize(mvp_stream_of(c)));
+  }
   return decode_status(c, w, first_bad, "MVP query");
 }
 
@@ -2181,8 +2263,8 @@ int mm_mvp_convert_device(mm_ctx* c, const mm_mvp_query* d_q, int n, int32_t* d_
   if (n == 0) return MM_OK;
   HIPCHK(c, hipSetDevice(c->device));
   RCCHK(sync_epi_table(c));
-  const mmmvp::EpiTable et{c->d_epi.p, c->epi_n};
-  unsigned long long* st = c->d_mvp_status.p + c->mvp_par;
+  const mmmvp::EpiTable et{c->d_epi[c->epi_buf].p, c->epi_n};
+  unsigned long long* st = c->d_mvp_status.p;  // sticky (read_mvp_status clears it)
   const hipStream_t ms = mvp_stream_of(c);
   if (c->mvp_on_own && c->epi_fresh) HIPCHK(c, hipStreamWaitEvent(ms, c->ev_epi, 0));  // the table copy
   c->epi_fresh = false;
@@ -2196,8 +2278,8 @@ int mm_mvp_convert_device(mm_ctx* c, const mm_mvp_query* d_q, int n, int32_t* d_
   if (sort) {
     // the sort buffers are shared by the calls of the context: growing them drains the device
     // (DevBuf::ensure), so a conversion still running on the MVP stream keeps its buffers
-    HIPCHK(c, c->d_mvp_local.ensure(n));
-    HIPCHK(c, c->d_mvp_perm.ensure(n));
+    HIPCHK(c, c->d_mvp_local.ensure(c, n));
+    HIPCHK(c, c->d_mvp_perm.ensure(c, n));
   }
   if (c->timed) HIPCHK(c, hipEventRecord(c->ev0, ms));
   if (sort) {
@@ -2208,12 +2290,40 @@ int mm_mvp_convert_device(mm_ctx* c, const mm_mvp_query* d_q, int n, int32_t* d_
     c->mvp_sort_par ^= 1;
   }
   hipLaunchKernelGGL(k_mvp_dev, dim3(nb), dim3(MVP_BLOCK), 0, ms, c->sc, d_q, n, sort ? c->d_mvp_perm.p : nullptr,
-                     c->prm.active_models, et, d_mv_out, st, c->d_mvp_status.p + (c->mvp_par ^ 1));
+                     c->prm.active_models, et, d_mv_out, st);
   HIPCHK(c, hipGetLastError());
   if (c->timed) HIPCHK(c, hipEventRecord(c->ev1, ms));
-  c->mvp_par ^= 1;  // read_mvp_status reads the word of this call (mvp_par ^ 1 from now on)
   c->mvp_pending = true;
   return MM_OK;
+}
+
+// motionVectorInDesiredMotionModel one query at a time on the calling host thread, for the
+// candidates VTM converts in decoding order (spatial merge / AMVP candidates: the neighbour's final
+// MV, UnitTools.cpp:2930-2992, 3134-3167): the same csrc/mm_mvp.h bodies as k_mvp_dev, compiled
+// for the host.  No device work and no context: the sequence parameters and an EpipoleList handle
+// (a context's own list through mm_get_epipole_list, or a standalone one) are the inputs.
+int mm_mvp_convert_host(const mm_seq_params* p, mm_epipole_list* e, const mm_mvp_query* q, int n, int32_t* mv_out,
+                        int* first_bad) {
+  if (first_bad) *first_bad = -1;
+  if (!p || n < 0 || (n > 0 && (!q || !mv_out)) || p->width <= 0 || p->height <= 0) return MM_ERR_ARG;
+  const SeqConst sc = seq_const(*p);
+  mmmvp::EpiTable et{nullptr, 0};
+  if (e) {
+    if (e->host_version != e->l->version()) {
+      epi_entries(*e->l, &e->host);
+      e->host_version = e->l->version();
+    }
+    et = mmmvp::EpiTable{e->host.data(), (int)e->host.size()};
+  }
+  int rc = MM_OK;
+  for (int i = 0; i < n; i++) {
+    const int code = mmmvp::mvp_query(sc, q[i], p->active_models, et, mv_out + 2 * i);
+    if (code && rc == MM_OK) {  // the lowest failing query, as mm_mvp_status reports it
+      rc = code;
+      if (first_bad) *first_bad = i;
+    }
+  }
+  return rc;
 }
 
 int mm_set_mvp_stream(mm_ctx* c, void* s) {
@@ -2235,8 +2345,8 @@ int mm_mvp_convert(mm_ctx* c, const mm_mvp_query* q, int n, int32_t* mv_out) {
   if (!c || n < 0 || (n > 0 && (!q || !mv_out))) return MM_ERR_ARG;
   if (n == 0) return MM_OK;
   HIPCHK(c, hipSetDevice(c->device));
-  HIPCHK(c, c->d_mvp_q.ensure(n));
-  HIPCHK(c, c->d_mvp_out.ensure(2 * (size_t)n));
+  HIPCHK(c, c->d_mvp_q.ensure(c, n));
+  HIPCHK(c, c->d_mvp_out.ensure(c, 2 * (size_t)n));
   HIPCHK(c, hipMemcpyAsync(c->d_mvp_q.p, q, (size_t)n * sizeof(mm_mvp_query), hipMemcpyHostToDevice, mvp_stream_of(c)));
   RCCHK(mm_mvp_convert_device(c, c->d_mvp_q.p, n, c->d_mvp_out.p));
   HIPCHK(c, hipMemcpyAsync(mv_out, c->d_mvp_out.p, 2 * (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost,

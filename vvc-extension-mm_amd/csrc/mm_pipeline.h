@@ -7,6 +7,7 @@
 #include <cstddef>
 #include "mm_filter.h"
 #include "mm_models.h"
+#include "mm_probe.h"
 
 namespace mmpipe {
 using namespace mmmod;
@@ -209,49 +210,34 @@ MM_HD int find_item(const int* offsets, const int* chunk_start, int g, int n_ite
 }
 
 #if defined(__HIP__)
-// Kernel arguments are read with uniform (scalar) loads only.  Per-lane (vector) loads of kernel-
-// argument memory returned stale words on MI355X when launches were queued back to back -- the
-// MM-DMVR search's per-lane copy of PicTables::ref faulted on another launch's words
-// (profiles/r04_kernarg_fault.txt) -- so a table a kernel indexes per lane is copied into LDS by
-// wave 0: lane k of each 64-word chunk selects word k among the chunk's scalar loads.  The caller
-// synchronises the workgroup before reading `lds`.
+// Tables that a kernel indexes per lane (the GED rotations, the reference table) are copied from
+// the kernel arguments into LDS by the first threads of the workgroup; every caller then
+// synchronises the workgroup (__syncthreads) before any thread reads `lds`.  The round-4 MM-DMVR
+// search faulted because its threads read a staged reference table before that barrier
+// (profiles/r04_kernarg_fault.txt, correction); DESIGN.md 4.6 audits every staging kernel and the
+// MM_RACE_PROBE build (mm_probe.h) checks them.  Round 4's replacement -- scalar loads of the words
+// with a per-lane select -- measured equal for k_mc and 1-3 us slower for k_setup_dev
+// (profiles/r05_ab_staging_and_mc_split.txt), so the plain per-lane copy stays.
 template <int NW>
 __device__ __forceinline__ void stage_arg_words(const uint32_t* arg, uint32_t* lds) {
-  if (threadIdx.x >= 64) return;
-  const int lane = threadIdx.x;
-#pragma unroll
-  for (int c = 0; c < NW; c += 64) {
-    uint32_t v = 0;
-#pragma unroll
-    for (int k = 0; k < 64; k++) {
-      if (c + k < NW) {
-        const uint32_t w = arg[c + k];  // uniform address: a scalar load
-        v = lane == k ? w : v;
-      }
-    }
-    if (c + lane < NW) lds[c + lane] = v;
-  }
+  for (int k = threadIdx.x; k < NW; k += blockDim.x) lds_put(lds[k], arg[k], 0x7fc00000u);  // poison: NaN
 }
 // The device fields of a picture's reference table (RefDev stride_y, stride_c, off_y, off_cb; the
-// host plane pointers are not used on the device) for NS slots, rebuilt in LDS from the packed
-// pool-slot numbers and the pool's uniform layout: four scalar loads, a few VALU ops in lanes 0..NS-1.
+// host plane pointers are not used on the device) for NS slots, from the packed pool-slot numbers
+// and the pool's uniform layout (lanes 0..NS-1).
 template <int NS>
 __device__ __forceinline__ void stage_ref_table(const uint32_t* pool_slot4, const RefPool& pool, RefDev* lds) {
   static_assert(NS % 4 == 0 && NS <= 64, "four slots per packed word");
   if (threadIdx.x >= NS) return;
   const int lane = threadIdx.x;
-  uint32_t w = 0;
-#pragma unroll
-  for (int k = 0; k < NS / 4; k++) {
-    const uint32_t v = pool_slot4[k];  // uniform address: a scalar load
-    w = (lane >> 2) == k ? v : w;
-  }
-  const uint32_t ps = (w >> (8 * (lane & 3))) & 255u;
+  const uint32_t ps = (pool_slot4[lane >> 2] >> (8 * (lane & 3))) & 255u;
   RefDev& r = lds[lane];
   r.stride_y = pool.stride_y;
   r.stride_c = pool.stride_c;
-  r.off_y = ps * pool.pic_bytes + pool.y0;
-  r.off_cb = ps * pool.pic_bytes + pool.cb0;
+  // probe poison: the pool's last picture slot (inside the pool, the wrong picture)
+  const uint32_t last = pool.bytes - pool.pic_bytes;
+  lds_put(r.off_y, ps * pool.pic_bytes + pool.y0, last + pool.y0);
+  lds_put(r.off_cb, ps * pool.pic_bytes + pool.cb0, last + pool.cb0);
 }
 
 // The same lookup for a whole wavefront whose lanes hold g = g0 + lane (g0 % 64 == 0): one

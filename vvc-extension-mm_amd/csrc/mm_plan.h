@@ -11,6 +11,7 @@
 #pragma once
 #include <algorithm>
 #include <array>
+#include <cmath>
 #include <map>
 #include <string>
 #include <tuple>
@@ -44,6 +45,18 @@ struct SeqInfo {
 };
 
 inline SeqInfo seq_info(const mm_seq_params& p) { return {p, p.width, p.height, p.chroma_format == 1}; }
+
+// The sequence constants of MVReprojection::init (MVReprojection.cpp:7-39, Projection.h:127-130)
+inline SeqConst seq_const(const mm_seq_params& p) {
+  SeqConst sc;
+  sc.Wf = (float)p.width;
+  sc.Hf = (float)p.height;
+  sc.off = p.mm_offset4x4 == 4 ? 1.5f : (float)p.mm_offset4x4;  // MVReprojection.cpp:10
+  sc.focal = (float)(1. / std::tan(M_PI / p.height));          // Projection.h:127-130
+  sc.res = (float)(M_PI / p.height);                           // MVReprojection.cpp:27,33,39
+  sc.ged_flavor = p.ged_flavor;
+  return sc;
+}
 
 inline bool is_ged(int m) { return m >= GEODESIC_X && m <= GEODESIC_CAMPOSE; }
 

@@ -26,6 +26,10 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libmm360.so")
+# MM360_LIB: a diagnostic build of the same library (tools/race_probe.sh runs the GPU suite on the
+# MM_RACE_PROBE variant); unset, the in-tree product library
+if os.environ.get("MM360_LIB"):
+    LIB_PATH = os.path.abspath(os.environ["MM360_LIB"])
 
 # MotionModelID (TypeDef.h:865-879)
 CLASSIC, MPA_FRONT_BACK, MPA_LEFT_RIGHT, MPA_TOP_BOTTOM = 0, 1, 2, 3
@@ -54,7 +58,7 @@ EXPORTED_SYMBOLS = (
     "mm_set_stripes", "mm_set_plan_ahead", "mm_pred_list", "mm_derive_effective_blocks", "mm_epipole_list_create",
     "mm_epipole_list_destroy", "mm_get_epipole_list", "mm_epipole_add", "mm_epipole_make_available", "mm_epipole_has",
     "mm_epipole_find", "mm_epipole_derive_predictor", "mm_epipole_count", "mm_mvp_convert_device", "mm_mvp_status", "mm_set_dmvr",
-    "mm_set_mvp_stream",
+    "mm_set_mvp_stream", "mm_mvp_convert_host",
 )
 
 BCW_DEFAULT = 2  # CommonDef.h:348-349; g_BcwWeights = {-2, 3, 4, 5, 10} (Rom.cpp:203)
@@ -187,6 +191,7 @@ def load_library() -> ctypes.CDLL:
         "mm_epipole_find": (c_int, [vp, c_int, c_int, POINTER(c_int32)]),
         "mm_epipole_derive_predictor": (c_int, [vp, c_int, POINTER(c_int32)]),
         "mm_epipole_count": (c_int, [vp]),
+        "mm_mvp_convert_host": (c_int, [POINTER(SeqParams), vp, vp, c_int, vp, POINTER(c_int)]),
     }
     default_lib = os.path.abspath(LIB_PATH) == os.path.join(os.path.dirname(_HERE), "lib", "libmm360.so")
     for name, (res, args) in sig.items():
@@ -262,6 +267,22 @@ class EpipoleList:
 
     def count(self) -> int:
         return int(self.lib.mm_epipole_count(self.h))
+
+
+def mvp_convert_host(params: SeqParams, queries: np.ndarray, epipoles: Optional[EpipoleList] = None) -> np.ndarray:
+    """mm_mvp_convert_host: motionVectorInDesiredMotionModel query by query on this host thread
+    (the spatial merge / AMVP candidates VTM converts in decoding order, UnitTools.cpp:2930-2992,
+    3134-3167), with the same bodies as the device conversion.  No GPU.  int32 [n, 2] MVs; raises
+    MMError with the lowest failing query's code."""
+    lib = load_library()
+    q = np.ascontiguousarray(queries, dtype=MVP_QUERY_DTYPE)
+    out = np.zeros((max(len(q), 1), 2), dtype=np.int32)
+    bad = c_int(-1)
+    rc = lib.mm_mvp_convert_host(byref(params), epipoles.h if epipoles is not None else None,
+                                 c_void_p(q.ctypes.data), len(q), c_void_p(out.ctypes.data), byref(bad))
+    if rc != MM_OK:
+        raise MMError(rc, f"mm_mvp_convert_host: query {bad.value}")
+    return out[:len(q)]
 
 
 def _ptr(a) -> int:
