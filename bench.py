@@ -248,7 +248,8 @@ def bench_pictures(args, cfg, params, rank, world, local, dist):
     achieved = alg_step / (kernel_ms * 1e-3) / 1e9
     mvp = None
     if args.config == "C3" and not args.no_mvp:
-        mvp = mvp_per_picture(ctx, cfg, int(np.mean([len(p) for _, p, _ in pictures])))
+        mvp = mvp_per_picture(ctx, cfg, int(np.mean([len(p) for _, p, _ in pictures])), params,
+                              [(cur, -1, W.GED_EPIPOLE_Q24) for cur, _, _ in pictures])
         mvp["in_loop"] = mvp_in_loop(args, ctx, cfg, pictures, d_pus, outs, area)
 
     cpu, bit_exact, mism = None, None, None
@@ -309,7 +310,7 @@ def dmvr_record(args, cfg, params, share=0.3, steps=12, warmup=3):
                     "search) and k_setup_dev; not part of value"}
 
 
-def mvp_per_picture(ctx, cfg, n_pus, reps=10):
+def mvp_per_picture(ctx, cfg, n_pus, params, epipoles, reps=10):
     """MM-MVP (mm_mvp_convert_device) beside the C3 number, outside its timed
     region: one conversion per PU and list (2 x PUs queries, the seeded query mix tiled), queries
     and results resident in HBM, stream-ordered on the context stream; device time of each call
@@ -332,15 +333,34 @@ def mvp_per_picture(ctx, cfg, n_pus, reps=10):
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / reps
     ctx.mvp_status()
+    got = d_out.cpu().numpy()  # the last timed call's results
     ctx.mvp_convert(q)  # host-buffer form (warm-up of its buffers)
     host = float("inf")
     for _ in range(3):
         t0 = time.perf_counter()
         ctx.mvp_convert(q)
         host = min(host, time.perf_counter() - t0)
+    # the host per-query form (mm_mvp_convert_host: the spatial merge / AMVP candidates, converted one at
+    # a time in decoding order, UnitTools.cpp:2930-2992, 3134-3167) on this thread: the picture's
+    # queries in one call, so the time per query is the conversion's own cost (a C++ decoder calls it
+    # per candidate; a ctypes call per query from Python would time the binding instead)
+    epi = ctx.epipole_list()
+    mm360.mvp_convert_host(params, q[:1000], epi)
+    t0 = time.perf_counter()
+    host_mv = mm360.mvp_convert_host(params, q, epi)
+    host_us = (time.perf_counter() - t0) / len(q) * 1e6
+    # check (after timing): the timed device conversions and the host form against the oracle
+    from oracle.oracle import Oracle
+    want = Oracle(params, epipoles).mvp(q)
+    bad = int((got != want).any(axis=1).sum())
+    bad_host = int((host_mv != want).any(axis=1).sum())
     return {"queries_per_picture": int(len(q)), "ms_per_picture": round(wall * 1e3, 4),
             "kernel_ms": round(float(np.mean(dev)), 4), "host_buffer_call_ms": round(host * 1e3, 4),
-            "note": "device-resident queries (mm_mvp_convert_device), back-to-back calls; not part of value"}
+            "bit_exact": bad == 0 and bad_host == 0, "mismatching_queries": bad + bad_host,
+            "bit_exact_sample": "the last timed device call's MVs and the host per-query form's, vs the oracle",
+            "host_per_query_us": round(host_us, 3), "host_per_query_cores": 1,
+            "note": "device-resident queries (mm_mvp_convert_device), back-to-back calls; host_per_query_us: "
+                    "mm_mvp_convert_host on one host thread (spatial candidates); not part of value"}
 
 
 def mvp_in_loop(args, ctx, cfg, pictures, d_pus, outs, area):

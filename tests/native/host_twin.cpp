@@ -369,12 +369,15 @@ extern "C" int twin_sad_window(const mm_seq_params* p, int n_epi, const int32_t*
     const int nb = (int)bt.blocks.size();
 #pragma omp parallel for schedule(static, 256)
     for (long g = 0; g < bt.n_elems; g++) {
-      int idx;
       const int bi = find_item(bt.blk_off.data(), bt.chunk.data(), (int)g, nb);
-      uint32_t v = me_sad_thread((int)g, bi, t.sc, t.geo, taps, w, bt.blocks.data(), setups.data(), c, tab.ref, org,
-                                 org_stride, &idx);
+      MeElem el;
+      int j;
+      me_elem_init((int)g, bi, t.sc, w, bt.blocks.data(), setups.data(), c, org, org_stride, &el, &j);
+      for (int i = 0; i < w.side; i++) {
+        const uint32_t v = me_cand_sad(el, i, j, bi, t.sc, t.geo, taps, w, bt.blocks.data(), setups.data(), tab.ref);
 #pragma omp atomic
-      sads[idx] += v;
+        sads[bt.blocks[bi].sad_off + j * w.side + i] += v;
+      }
     }
   }
   return 0;

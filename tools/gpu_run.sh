@@ -19,9 +19,12 @@ for step in "$@"; do
   case $step in
     tests) run gpu_tests 900 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread ;;
     race_probe) run race_probe 900 env MM360_LIB=tmp_variants/probe/libmm360.so python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread ;;
+    probe_ctl)  # positive control: the probe build with the s_ged barriers removed must FAIL (wrong pictures)
+      run probe_ctl 300 bash -c 'MM360_LIB=tmp_variants/probe_ctl/libmm360.so python -u -m pytest tests/test_gpu.py -q -k "pred_full_frame_vs_oracle or pred_uniform_per_model" --timeout 120 --timeout-method thread; rc=$?; echo "pytest rc=$rc (1 = tests failed as expected)"; test $rc -eq 1' ;;
     abb=*)  # abb=<rounds>=<v1,v2,...>: alternating headline runs of library variants (default = in-tree)
       rounds=$(echo "$step" | cut -d= -f2); vs=$(echo "$step" | cut -d= -f3 | tr ',' ' ')
       run "abb_$(echo "$vs" | tr ' ' '_')" 900 bash tools/ab_bench.sh "$rounds" $vs ;;
+    example) run example 120 vvc-extension-mm_amd/lib/example_decode ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     bench_c4) run bench_c4 600 python bench.py --config C4 ;;
@@ -34,6 +37,7 @@ for step in "$@"; do
     c4_gloo2) run c4_gloo2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --dist-backend gloo --steps 6 --warmup 2 ;;
     per_model) run per_model 900 bash tools/per_model.sh ;;
     ubench) run ubench 300 bash -c "tools/ubench/load_check && tools/ubench/valu_rate2" ;;
+    prof_r5) run prof_r5 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r5 -o run --output-format csv -- python3 bench.py --steps 12 --warmup 4 --no-cpu-baseline --no-mvp --no-c5 --no-dmvr ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 12 --warmup 4 --no-cpu-baseline --no-mvp --no-c5 --no-dmvr ;;
     pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 --no-mvp --no-c5 --no-dmvr ;;
     pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 --no-mvp --no-c5 --no-dmvr ;;

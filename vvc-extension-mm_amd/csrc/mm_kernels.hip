@@ -453,6 +453,9 @@ constexpr int MC_BLOCKS_PER_WG = 1;
 constexpr bool KERNEL_EVENTS = true;
 constexpr bool GATE_NO_FENCE = true;
 constexpr bool PLAN_AHEAD_HOST_WAIT = true;  // see launch_stripe
+#ifndef MM_REPROJ_AHEAD
+#define MM_REPROJ_AHEAD 1  // see launch_stripe
+#endif
 
 // --------------------------------------------------------------------------------------------
 // Encoder candidate windows (mm_sad_window, mm_me.h)
@@ -469,8 +472,9 @@ __global__ void __launch_bounds__(256) k_me_setup(SeqConst sc, MeWindow w, const
   me_setup_thread(i, sc, w, blocks, s_ged, out);
 }
 
-// thread per (block, candidate, sub-block); the sub-block SADs of one candidate are summed
-// across the lanes that hold it (segmented shuffle scan) and added to sads[] by its last lane.
+// thread per (block, window row j, sub-block e) looping over the row's candidates (mm_me.h
+// me_elem_init / me_cand_sad); per candidate the sub-block SADs of a block are summed across the
+// lanes that hold it (segmented shuffle scan) and added to sads[] by its last lane.
 // chunk c of a batch's elements -> the block holding element 64 c (binary search of the block
 // offsets); the device form of mm_plan.h build_chunks
 __global__ void __launch_bounds__(256) k_me_chunks(const int* __restrict__ off, int n_items, long n_elems,
@@ -503,20 +507,27 @@ __global__ void __launch_bounds__(256) k_me_sad(SeqConst sc, Geometry geo, MeWin
   if (g - lane >= n_elems) return;  // whole wave past the end
   const int bi = wave_find_item(blk_off, chunk, g, n_blocks);
   const bool active = g < n_elems;
-  int idx = -1 - lane;  // inactive lanes: distinct keys that never merge
-  uint32_t v = 0;
+  const Taps taps{c_luma_taps, c_chroma_taps, &c_packed_taps, t.pool};
+  MeElem el;
+  int j = 0, key = -1 - lane;  // inactive lanes: distinct keys that never merge
   if (active) {
-    const Taps taps{c_luma_taps, c_chroma_taps, &c_packed_taps, t.pool};
-    v = me_sad_thread(g, bi, sc, geo, taps, w, blocks, setups, cache, s_ref, org, org_stride, &idx);
+    me_elem_init(g, bi, sc, w, blocks, setups, cache, org, org_stride, &el, &j);
+    key = blocks[bi].sad_off + j * w.side;
   }
+#pragma unroll 1
+  for (int i = 0; i < w.side; i++) {  // uniform trip count (shuffles below)
+    uint32_t v = 0;
+    if (active) v = me_cand_sad(el, i, j, bi, sc, geo, taps, w, blocks, setups, s_ref);
+    const int idx = active ? key + i : key;
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t vu = __shfl_up(v, d);
-    const int iu = __shfl_up(idx, d);
-    if (lane >= d && iu == idx) v += vu;
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t vu = __shfl_up(v, d);
+      const int iu = __shfl_up(idx, d);
+      if (lane >= d && iu == idx) v += vu;
+    }
+    const int inext = __shfl_down(idx, 1);
+    if (active && (lane == 63 || inext != idx)) atomicAdd(&sads[idx], v);
   }
-  const int inext = __shfl_down(idx, 1);
-  if (active && (lane == 63 || inext != idx)) atomicAdd(&sads[idx], v);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -1871,24 +1882,6 @@ static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables
     hipLaunchKernelGGL(k_dmvr_search_dev, dim3(std::max(1, std::min(DMVR_SEARCH_GRID, k.subs))), dim3(DMVR_SEARCH_WG),
                        0, st, geo, S.dmvr_sub.p, c->d_dmvr_pos.p, t, dw, S.jobs.p, mvd);
   }
-  if (back && KERNEL_EVENTS) {  // plan-ahead: ev_plan completes with k_setup_dev
-    hipExtLaunchKernelGGL(k_setup_dev, dim3(gs), dim3(256), 0, st, nullptr, c->ev_plan, 0, c->sc, S.meta.p, S.jobs.p, t,
-                          S.setup.p);
-  } else {
-    hipLaunchKernelGGL(k_setup_dev, dim3(gs), dim3(256), 0, st, c->sc, S.meta.p, S.jobs.p, t, S.setup.p);
-    if (back) HIPCHK(c, hipEventRecord(c->ev_plan, st));
-  }
-  if (back) {  // plan-ahead: reprojection and interpolation on the context stream
-    // The host waits for this picture's planning (bound to k_setup_dev) before it issues the context
-    // stream's wait: the event is then complete, so the runtime issues no cross-queue barrier packet
-    // between the previous picture's k_mc_dev and this k_reproj_dev (C3 0.178-0.180 -> 0.173-0.175 ms
-    // per picture, profiles/r03_ab_hostsync.txt).  The planning waits only for the k_mc_dev of two
-    // calls back, so the host still runs about one picture ahead of the GPU.
-    if (PLAN_AHEAD_HOST_WAIT) HIPCHK(c, hipEventSynchronize(c->ev_plan));
-    HIPCHK(c, hipStreamWaitEvent(st_back, c->ev_plan, 0));
-    st = st_back;
-  }
-  if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[1], st));
   McRec mc;
   mc.meta = S.mc_meta.p;
   for (int l = 0; l < 2; l++) {
@@ -1896,8 +1889,41 @@ static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables
     mc.cpos[l] = S.mc_cpos[l].p;
     for (int q = 0; q < 2; q++) mc.far[l][q] = S.mc_far[l][q].p;
   }
-  hipLaunchKernelGGL(k_reproj_dev, dim3(gr), dim3(256), 0, st, c->sc, S.meta.p, S.jobs.p, S.job_off.p, S.job_chunk.p,
-                     S.setup.p, make_cache(c), mc);
+  // reprojection ahead (plan-ahead, no MM-DMVR): k_reproj_dev also runs on the auxiliary stream, so
+  // it overlaps the previous picture's k_mc_dev -- VALU-bound reprojection beside the texture-path-
+  // bound interpolation.  Its McRec writes go to this call's plan slot, whose previous reader (the
+  // k_mc_dev of two calls back) the slot gate already orders before the planning.
+  const bool reproj_ahead = back && MM_REPROJ_AHEAD;
+  if (back && KERNEL_EVENTS) {  // plan-ahead: ev_plan completes with k_setup_dev (or k_reproj_dev)
+    if (reproj_ahead) {
+      hipLaunchKernelGGL(k_setup_dev, dim3(gs), dim3(256), 0, st, c->sc, S.meta.p, S.jobs.p, t, S.setup.p);
+      hipExtLaunchKernelGGL(k_reproj_dev, dim3(gr), dim3(256), 0, st, nullptr, c->ev_plan, 0, c->sc, S.meta.p, S.jobs.p,
+                            S.job_off.p, S.job_chunk.p, S.setup.p, make_cache(c), mc);
+    } else {
+      hipExtLaunchKernelGGL(k_setup_dev, dim3(gs), dim3(256), 0, st, nullptr, c->ev_plan, 0, c->sc, S.meta.p, S.jobs.p,
+                            t, S.setup.p);
+    }
+  } else {
+    hipLaunchKernelGGL(k_setup_dev, dim3(gs), dim3(256), 0, st, c->sc, S.meta.p, S.jobs.p, t, S.setup.p);
+    if (reproj_ahead)
+      hipLaunchKernelGGL(k_reproj_dev, dim3(gr), dim3(256), 0, st, c->sc, S.meta.p, S.jobs.p, S.job_off.p, S.job_chunk.p,
+                         S.setup.p, make_cache(c), mc);
+    if (back) HIPCHK(c, hipEventRecord(c->ev_plan, st));
+  }
+  if (back) {  // plan-ahead: (reprojection and) interpolation on the context stream
+    // The host waits for this picture's planning (bound to k_setup_dev / k_reproj_dev) before it issues
+    // the context stream's wait: the event is then complete, so the runtime issues no cross-queue
+    // barrier packet between the previous picture's k_mc_dev and this picture's next kernel (C3
+    // 0.178-0.180 -> 0.173-0.175 ms per picture, profiles/r03_ab_hostsync.txt).  The planning waits
+    // only for the k_mc_dev of two calls back, so the host still runs about one picture ahead.
+    if (PLAN_AHEAD_HOST_WAIT) HIPCHK(c, hipEventSynchronize(c->ev_plan));
+    HIPCHK(c, hipStreamWaitEvent(st_back, c->ev_plan, 0));
+    st = st_back;
+  }
+  if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[1], st));
+  if (!reproj_ahead)
+    hipLaunchKernelGGL(k_reproj_dev, dim3(gr), dim3(256), 0, st, c->sc, S.meta.p, S.jobs.p, S.job_off.p, S.job_chunk.p,
+                       S.setup.p, make_cache(c), mc);
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[2], st));
   // mc_done (plan-ahead): the slot's gate, complete when this k_mc is
   hipEvent_t stop = KERNEL_EVENTS ? mc_done : nullptr;

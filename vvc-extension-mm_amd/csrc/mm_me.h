@@ -27,7 +27,7 @@ struct MeBlockDev {
   int ged_idx;         // GED rotation table index, -1 if not GED
   int sub_shift;       // 0 or 1
   int n, rows;         // luma 4x4 sub-blocks, Eigen rows (h / 4)
-  int elem_off;        // first flat element of this block in the batch (C * n per block)
+  int elem_off;        // first thread of this block in the batch (side * n per block: window row x sub-block)
   int sad_off;         // sads index of candidate 0
 };
 
@@ -52,34 +52,67 @@ MM_HD void me_setup_thread(int t, const SeqConst& sc, const MeWindow& w, const M
   block_setup(&out[t], sc, b.model, true, b.x, b.y, b.w, b.h, mvh, mvv, b.ged_idx >= 0 ? &ged[b.ged_idx] : nullptr);
 }
 
-// thread per (block, candidate, sub-block) element: reprojection, 4x4 luma prediction and its
-// SAD contribution.  Returns the (subShift-scaled) SAD of this sub-block and the sads index.
-MM_HD uint32_t me_sad_thread(int g, int bi, const SeqConst& sc, const Geometry& geo, const Taps& taps,
-                             const MeWindow& w, const MeBlockDev* blocks, const BlockSetup* setups,
-                             const MpaCache& cache, const RefDev* refs, const int16_t* org, int org_stride,
-                             int* sad_index) {
+// One luma 4x4 sub-block e of a block against every candidate of one window row j (a thread of
+// k_me_sad): what does not depend on the candidate is done once -- the element's grid point, its
+// frame-cache / trig-table entries, the model's MV-independent head (mm_models.h motion_head: TAN's
+// tangent-plane coordinates about the block centre, GED's rotated spherical coordinates, the sphere
+// point of ROT / 3DT) and the original samples the SAD reads -- and per candidate only the model's
+// tail, the 8-tap prediction and the SAD (me_cand_sad).  head + tail == model_motion_element, so the
+// results are those of a full reprojection per candidate.
+struct MeElem {
+  float gx, gy, px, py;
+  int packet, mpa, vip;
+  MotionHead head;
+  int col, row;
+  int16_t org[16];  // the sub-block's original samples (rows 0..3, or the even rows for subShift 1)
+};
+// flat thread g of a batch: block bi, window row j, element e (threads of a block: side x n, e fastest)
+MM_HD void me_elem_init(int g, int bi, const SeqConst& sc, const MeWindow& w, const MeBlockDev* blocks,
+                        const BlockSetup* setups, const MpaCache& cache, const int16_t* org, int org_stride, MeElem* el,
+                        int* j_out) {
   const MeBlockDev& b = blocks[bi];
   const int local = g - b.elem_off;
-  const int c = local / b.n, e = local - c * b.n;
-  *sad_index = b.sad_off + c;
-  const BlockSetup& s = setups[bi * w.C + c];
+  const int j = local / b.n, e = local - j * b.n;
+  *j_out = j;
   // Eigen column-major element e of the block's (rows x cols) grid
   const int col = e / b.rows, row = e - col * b.rows;
-  const float gx = (float)(b.x + 4 * col) + sc.off, gy = (float)(b.y + 4 * row) + sc.off;
-  const bool mpa = b.model >= MPA_FRONT_BACK && b.model <= MPA_TOP_BOTTOM;
+  el->col = col;
+  el->row = row;
+  el->gx = (float)(b.x + 4 * col) + sc.off;
+  el->gy = (float)(b.y + 4 * row) + sc.off;
+  el->mpa = b.model >= MPA_FRONT_BACK && b.model <= MPA_TOP_BOTTOM;
   float px = 0.0f, py = 0.0f;
   bool vip = false;
-  if (mpa) {
-    mpa_lookup(cache, b.model, (b.x >> 2) + col, (b.y >> 2) + row, &px, &py, &vip);
-  }
-  const bool packet = packet_lane(e, b.n);
-  const GridSphere pg = grid_point(cache, b.model, (b.x >> 2) + col, (b.y >> 2) + row, packet);
+  if (el->mpa) mpa_lookup(cache, b.model, (b.x >> 2) + col, (b.y >> 2) + row, &px, &py, &vip);
+  el->px = px;
+  el->py = py;
+  el->vip = vip ? 1 : 0;
+  el->packet = packet_lane(e, b.n) ? 1 : 0;
+  const GridSphere pg = grid_point(cache, b.model, (b.x >> 2) + col, (b.y >> 2) + row, el->packet != 0);
+  // the head needs a setup that is not the zero-MV identity: at most one candidate of the window has
+  // a zero MV, so candidate 0 or 1 of the row
+  const BlockSetup* s0 = &setups[(long)bi * w.C + (long)j * w.side];
+  if (s0->identity && w.side > 1) s0 = s0 + 1;
+  el->head = motion_head(sc, *s0, el->gx, el->gy, Math{el->packet != 0}, pg);
+  const int16_t* o = org + (long)(b.y + 4 * row) * org_stride + b.x + 4 * col;
+  for (int r = 0; r < 4; r++)
+    for (int k = 0; k < 4; k++) el->org[r * 4 + k] = o[(long)r * org_stride + k];
+}
+
+// The (subShift-scaled) SAD of the element's sub-block for candidate i of its row j.
+MM_HD uint32_t me_cand_sad(const MeElem& el, int i, int j, int bi, const SeqConst& sc, const Geometry& geo,
+                           const Taps& taps, const MeWindow& w, const MeBlockDev* blocks, const BlockSetup* setups,
+                           const RefDev* refs) {
+  const MeBlockDev& b = blocks[bi];
+  const BlockSetup& s = setups[(long)bi * w.C + (long)j * w.side + i];
+  float mx, my;
+  motion_tail(sc, s, el.head, el.gx, el.gy, Math{el.packet != 0}, el.mpa != 0, el.px, el.py, el.vip != 0, &mx, &my);
   int32_t fx, fy;
-  reproject_element(sc, s, gx, gy, packet, mpa, px, py, vip, 0, &fx, &fy, pg);
+  reproject_finish(sc, el.gx, el.gy, mx, my, el.packet != 0, 0, &fx, &fy);
   const int xPos = fx >> 4, yPos = fy >> 4, xFrac = fx & 15, yFrac = fy & 15;
   int16_t p[16];
   if (xPos < 0 || yPos < 0 || xPos >= geo.W - 4 || yPos >= geo.H - 4) {  // maxCUWidth = 0
-    for (int i = 0; i < 16; i++) p[i] = 0;
+    for (int k = 0; k < 16; k++) p[k] = 0;
   } else {
     const RefDev r = refs[b.slot];
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -99,12 +132,11 @@ MM_HD uint32_t me_sad_thread(int g, int bi, const SeqConst& sc, const Geometry& 
   }
   // RdCost::xGetSAD over this sub-block's rows of the block (rows 4*row + r; subShift 1 keeps
   // the even block rows, which are the even rows of every sub-block)
-  const int16_t* o = org + (long)(b.y + 4 * row) * org_stride + b.x + 4 * col;
   const int rstep = 1 << b.sub_shift;
   uint32_t sum = 0;
   for (int r = 0; r < 4; r += rstep)
     for (int k = 0; k < 4; k++) {
-      const int d = (int)o[(long)r * org_stride + k] - (int)p[r * 4 + k];
+      const int d = (int)el.org[r * 4 + k] - (int)p[r * 4 + k];
       sum += (uint32_t)(d < 0 ? -d : d);
     }
   return sum << b.sub_shift;

@@ -237,7 +237,7 @@ inline int build_pic_tables(const SeqInfo& s, const EpipoleMap& epi, int cur_poc
 // Batches of blocks with at most ME_BATCH_JOBS (block, candidate) jobs each; every block is
 // validated as the reference's CHECKs / preconditions would (geometry, model, reference,
 // epipole) before anything runs.
-constexpr long ME_BATCH_JOBS = 1L << 20;
+constexpr long ME_BATCH_JOBS = 1L << 22;  // 224 MB of setups; C5: ~3.8 K blocks, 2 M k_me_sad threads per batch
 
 struct MeBatch {
   std::vector<mmme::MeBlockDev> blocks;
@@ -304,7 +304,7 @@ inline int plan_me_window(const SeqInfo& s, const mmdev::PicTables& t, const mm_
     cur.blocks.push_back(d);
     cur.blk_off.push_back(d.elem_off);
     cur.n_jobs += w.C;
-    cur.n_elems += (long)w.C * nsb;
+    cur.n_elems += (long)w.side * nsb;  // k_me_sad thread per (window row, sub-block)
   }
   if (!cur.blocks.empty()) batches->push_back(std::move(cur));
   if (host_chunks)

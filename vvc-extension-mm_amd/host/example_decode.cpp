@@ -8,6 +8,7 @@
 // predictions agree.  Exit 0 and "OK" on success; exit 2 when no HIP device is present.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdio>
 #include <vector>
 
@@ -29,6 +30,23 @@ int main() {
     rep.init(&ctx);
     mm360::FixedPair f = rep.reprojectMotionVectorSubblocks(32, 16, 16, 8, 37, -21, MM_MPA_FRONT_BACK, 0, 8, 0);
     if (f.rows != 2 || f.cols != 4) return 1;
+
+    // MM-MVP per candidate, as the merge / AMVP builders call it in decoding order
+    // (MVReprojection::motionVectorInDesiredMotionModel -> mm_mvp_convert_host), timed per call
+    const int32_t e1[3] = {1 << 24, 0, 0};
+    ctx.setEpipole(8, -1, e1);
+    const int n_calls = 20000;
+    long mv_sum = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < n_calls; i++) {
+      const int m0 = MM_MPA_FRONT_BACK + i % 3, m1 = MM_MPA_FRONT_BACK + (i / 3) % 3;
+      const auto mv = rep.motionVectorInDesiredMotionModel(4 * (i % 60) + 2, 4 * ((i / 60) % 30) + 2, 37 + i % 50,
+                                                           -21 + i % 40, m0, m1, 4, 4, 8, 0, 8, 16, 16 * (i % 14), 16,
+                                                           16, 16, 16 * (i % 14) + 16, 16, 16, 16);
+      mv_sum += mv.first + mv.second;
+    }
+    const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / n_calls;
+    std::printf("MVP host per-call latency %.3f us (%d calls, checksum %ld)\n", us, n_calls, mv_sum);
 
     mm360::InterPredictionMM pred(&ctx);
     for (int by = 0; by < H; by += 16)

@@ -18,6 +18,7 @@
 #include <cstdint>
 #include <stdexcept>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/mm360.h"
@@ -148,6 +149,26 @@ class MVReprojectionGPU {
       out.y[i] = xy[2 * i + 1];
     }
     return out;
+  }
+
+  // motionVectorInDesiredMotionModel (MVReprojection.cpp:168-217), same argument order; the
+  // returned pair is the Mv (hor, ver).  For the call sites that convert one candidate at a time in
+  // decoding order -- the spatial merge and AMVP candidates take the neighbour's final MV
+  // (UnitTools.cpp:2930-2992, 3134-3167) -- on this host thread, with the library's own model
+  // bodies (mm_mvp_convert_host); no device round trip.  The collocated (TMVP) candidates of a
+  // whole picture (UnitTools.cpp:2267-2304) can instead be batched through mm_mvp_convert_device.
+  std::pair<int32_t, int32_t> motionVectorInDesiredMotionModel(
+      int posX, int posY, int32_t mvHor, int32_t mvVer, int modelOrig, int modelDesired, int shiftHor, int shiftVer,
+      int curPOCOrig, int refPOCOrig, int curPOCDesired, int refPOCDesired, int candX, int candY, int candW, int candH,
+      int curX, int curY, int curW, int curH) const {
+    const mm_mvp_query q{posX,       posY,       mvHor,         mvVer,         modelOrig, modelDesired, shiftHor,
+                         shiftVer,   curPOCOrig, refPOCOrig,    curPOCDesired, refPOCDesired, candX, candY,
+                         candW,      candH,      curX,          curY,          curW,      curH};
+    int32_t mv[2] = {0, 0};
+    check(ctx_->get(),
+          mm_mvp_convert_host(&ctx_->params(), mm_get_epipole_list(ctx_->get()), &q, 1, mv, nullptr),
+          "motionVectorInDesiredMotionModel");
+    return {mv[0], mv[1]};
   }
 
  private:
