@@ -88,8 +88,12 @@ def cpu_threads():
     return max(1, min(16, n))  # the GPU box's CPU share is 16 threads per GPU
 
 
-def picture_set(cfg, n, frame0=0, uniform_model=None, coherent=False, dmvr_share=0.0):
-    """n pictures: (cur_poc, PU list, {poc: planes}) with disjoint reference pairs."""
+def picture_set(cfg, n, frame0=0, uniform_model=None, coherent=False, dmvr_share=0.0, dmvr_correlated=False):
+    """n pictures: (cur_poc, PU list, {poc: planes}) with disjoint reference pairs.
+    dmvr_correlated: both references of a picture carry the same content and the MM_PUF_DMVR PUs
+    point both lists at the same place (mv1 = mv0; 30 % of them a quarter sample off in one
+    component), so their two predictions agree and the centre cost ends most searches early
+    (InterPrediction.cpp:2516-2525), as on content with true bi-directional motion."""
     out = []
     for f in range(n):
         base = POC_STRIDE * (frame0 + f)
@@ -102,6 +106,14 @@ def picture_set(cfg, n, frame0=0, uniform_model=None, coherent=False, dmvr_share
             pus["mv"][:, 1, :] = (-37, 91)
         pus["ref_poc"] = np.where(pus["ref_poc"] >= 0, pus["ref_poc"] + base, -1)
         refs = {base + p: W.ref_planes(cfg.width, cfg.height, base + p) for p in W.REF_POCS}
+        if dmvr_correlated:
+            p0, p1 = (base + p for p in W.REF_POCS)
+            refs[p1] = tuple(x.copy() for x in refs[p0])
+            d = np.flatnonzero(W.dmvr_flagged(pus))
+            rng = np.random.default_rng(0x4D4D8000 + frame0 + f)
+            pus["mv"][d, 1, :] = pus["mv"][d, 0, :]
+            off = d[rng.random(len(d)) < 0.3]
+            pus["mv"][off, 1, rng.integers(0, 2, size=len(off))] += rng.choice([-4, 4], size=len(off))
         out.append((base + W.CUR_POC, pus, refs))
     return out
 
@@ -198,7 +210,8 @@ def cpu_baseline_and_check(args, cfg, params, pictures, gpu_out, n_checked=None)
 def bench_pictures(args, cfg, params, rank, world, local, dist):
     """C3 (and C2 / uniform-model variants): rotating pictures, one per step."""
     pictures = picture_set(cfg, args.pictures, frame0=rank * args.pictures, uniform_model=args.uniform_model,
-                           coherent=args.coherent_mv, dmvr_share=args.dmvr_share)
+                           coherent=args.coherent_mv, dmvr_share=args.dmvr_share,
+                           dmvr_correlated=getattr(args, "dmvr_correlated", False))
     ctx = new_ctx(params, local, pictures)
     if args.dmvr_share > 0:
         ctx.set_dmvr(True)
@@ -290,7 +303,7 @@ def bench_pictures(args, cfg, params, rank, world, local, dist):
     return None
 
 
-def dmvr_record(args, cfg, params, share=0.3, steps=12, warmup=3):
+def dmvr_record(args, cfg, params, share=0.3, steps=12, warmup=3, correlated=False):
     """C3 with MM-DMVR beside the headline: the same rotating pictures with
     `share` of the DMVR-eligible bi leaves flagged MM_PUF_DMVR (merge / mvRefine PUs), so that each
     picture runs the centre costs, the survivors' 24-offset search and the refined prediction inside
@@ -299,9 +312,14 @@ def dmvr_record(args, cfg, params, share=0.3, steps=12, warmup=3):
     a = argparse.Namespace(**vars(args))
     a.dmvr_share, a.steps, a.warmup, a.kernel_steps = share, steps, warmup, 2
     a.no_mvp, a.cpu_seconds, a.uniform_model, a.coherent_mv = True, 0.5, None, False
+    a.dmvr_correlated = correlated
     line = bench_pictures(a, cfg, params, 0, 1, 0, None)
     cpu = line["cpu_baseline"] or {}
-    return {"workload": line["config"]["workload"], "share": share, "value": line["value"], "unit": "Mpixels/s",
+    wl = line["config"]["workload"]
+    if correlated:
+        wl += (" [correlated references: both lists read the same content at the same place (mv1 = mv0, 30 % "
+               "a quarter sample off), so the centre cost ends most searches]")
+    return {"workload": wl, "share": share, "value": line["value"], "unit": "Mpixels/s",
             "ms_per_picture": line["ms_per_step"], "steps": steps, "stages_ms": line["stages_ms"],
             "bit_exact": line["bit_exact"], "mismatching_samples": line["mismatching_samples"],
             "bit_exact_sample": f"the {min(a.pictures, steps)} timed pictures vs the oracle",
@@ -774,6 +792,8 @@ def main():
                     help="C4 rehearsal on one GPU: per-rank stripe MC times for N = 2, 4, 8 + modelled all-gather")
     ap.add_argument("--coherent-mv", action="store_true",
                     help="experiment: one MV for every PU and list (spatially coherent motion)")
+    ap.add_argument("--dmvr-correlated", action="store_true",
+                    help="with --dmvr-share: both references and both lists' MVs of the DMVR PUs agree (early exits)")
     ap.add_argument("--dmvr-share", type=float, default=0.0,
                     help="C2/C3: this share of the DMVR-eligible bi leaves are merge/mvRefine PUs that run MM-DMVR "
                          "inside the picture's launch sequence (mm_set_dmvr, MM_PUF_DMVR)")
@@ -814,6 +834,7 @@ def main():
         if line is not None:
             if args.config == "C3" and world == 1 and args.dmvr_share == 0 and not args.no_dmvr:
                 line["dmvr"] = dmvr_record(args, cfg, params)
+                line["dmvr_correlated"] = dmvr_record(args, cfg, params, correlated=True)
             if args.config == "C3" and world == 1 and not args.no_c5:
                 line["c5"] = c5_record(args)
             print(json.dumps(line), flush=True)

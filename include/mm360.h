@@ -18,6 +18,7 @@
  *                       (addAvg / addWeightedAvg (BCW) / copyClip)
  *                                                         SRC/InterPrediction.cpp:1584-1679,
  *                                                         SRC/Buffer.cpp:398-424, 551-658
+ *   mm_pred_device_multi <- the same over several independent pictures in one launch chain
  *   mm_pred_list     <- InterPrediction::xPredInterBlkMM 1:1 per list: one reference list of every
  *                       PU, bi=true (14-bit, rndRes=false) or bi=false (clipped), InterPrediction.cpp:683-856
  *   mm_filter        <- InterpolationFilter::filterHor/filterVer  SRC/InterpolationFilter.h:123-128
@@ -240,6 +241,28 @@ int mm_pred(mm_ctx* ctx, int cur_poc, const mm_pu_desc* pus, int n, int16_t* dst
 int mm_pred_device(mm_ctx* ctx, int cur_poc, const mm_pu_desc* d_pus, int n, int16_t* dst_y,
                    ptrdiff_t dst_stride_y, int16_t* dst_cb, int16_t* dst_cr,
                    ptrdiff_t dst_stride_c);
+
+/* Several independent pictures in ONE launch chain: the pictures of one call must not reference
+ * each other's output (the leaves of a random-access temporal layer, or the CTU-row stripes of
+ * different pictures on one GPU, cfg/encoder_randomaccess_vtm.cfg:20-51).  Each picture has its
+ * own current POC (GEODESIC_CAMPOSE epipoles of (cur_poc, ref)), device PU list and destination
+ * planes; all read the context's resident references.  The planning, setup, reprojection and
+ * interpolation of all pictures share their launches, so small pictures or stripes no longer pay
+ * the per-call launch chain each.  Same semantics as mm_pred_device per picture (plan-ahead,
+ * deferred status; the status's PU index counts through the pictures' lists in call order).
+ * 1 <= n_pics <= MM_MAX_PICS; MM_PUF_DMVR PUs only with n_pics == 1. */
+#define MM_MAX_PICS 4
+typedef struct mm_pic_job {
+  int32_t cur_poc;
+  const mm_pu_desc* d_pus;     /* device memory */
+  int32_t n;
+  int16_t* dst_y;
+  ptrdiff_t dst_stride_y;
+  int16_t* dst_cb;
+  int16_t* dst_cr;
+  ptrdiff_t dst_stride_c;
+} mm_pic_job;
+int mm_pred_device_multi(mm_ctx* ctx, const mm_pic_job* pics, int n_pics);
 
 /* Waits for the context stream and returns the deferred status of the last device-planned
  * call (MM_OK or the code of the lowest failing PU, whose index goes to *first_bad_pu). */

@@ -101,15 +101,38 @@ extern "C" int twin_reproject(const mm_seq_params* p, int n_epi, const int32_t* 
 // The device-planned prediction path (mm_devplan.h + mm_pipeline.h bodies), run sequentially,
 // including the MM-DMVR search of MM_PUF_DMVR PUs (mm_dmvr.h bodies) between placement and setup.
 // mvd (optional): the refined deltas of the DMVR sub-PUs in placement order.
+static DstPlanes one_dst(int16_t* dy, int sdy, int16_t* dcb, int16_t* dcr, int sdc) {
+  DstPlanes d{};
+  for (int q = 0; q < MM_MAX_PICS; q++) {
+    d.y[q] = dy;
+    d.cb[q] = dcb;
+    d.cr[q] = dcr;
+    d.sy[q] = sdy;
+    d.sc[q] = sdc;
+  }
+  return d;
+}
+
+// pic_base (optional): PUs [pic_base[q], pic_base[q + 1]) belong to picture q of a multi-picture call
+static int twin_pred_segs(const Twin& t, const mmdev::PicTables& tab, const mm_pu_desc* pus, int n,
+                          const int* pic_base, const DstPlanes& dst, int hp = 0, int store = 3,
+                          std::vector<int32_t>* mvd = nullptr);
 static int twin_pred_list(const Twin& t, const mmdev::PicTables& tab, const mm_pu_desc* pus, int n, int16_t* dy,
                           int sdy, int16_t* dcb, int16_t* dcr, int sdc, int hp = 0, int store = 3,
                           std::vector<int32_t>* mvd = nullptr) {
+  return twin_pred_segs(t, tab, pus, n, nullptr, one_dst(dy, sdy, dcb, dcr, sdc), hp, store, mvd);
+}
+static int twin_pred_segs(const Twin& t, const mmdev::PicTables& tab, const mm_pu_desc* pus, int n,
+                          const int* pic_base, const DstPlanes& dst, int hp, int store, std::vector<int32_t>* mvd) {
   using namespace mmdev;
   using namespace mmdmvr;
   std::vector<PuPlan> plans(n);
   PlanCounters cnt{};
   for (int i = 0; i < n; i++) {
-    classify_pu(pus[i], tab, &plans[i]);
+    int q = 0;
+    if (pic_base)
+      while (q + 1 < tab.n_pics && i >= pic_base[q + 1]) q++;
+    classify_pu(pus[i], tab, &plans[i], q);
     if (plans[i].code) return plans[i].code;
     cnt.pu_tot[plans[i].key] += pu_count(plans[i]);
     for (int k = 0; k < 4; k++)
@@ -180,9 +203,9 @@ static int twin_pred_list(const Twin& t, const mmdev::PicTables& tab, const mm_p
 #pragma omp parallel for schedule(static, 256)
   for (int g = 0; g < m.n_sb; g++)
     if (geo.hp)
-      mc_thread_rec<true>(g, geo, taps, mc, tab.ref, dy, sdy, dcb, dcr, sdc);
+      mc_thread_rec<true>(g, geo, taps, mc, tab.ref, dst);
     else
-      mc_thread_rec<false>(g, geo, taps, mc, tab.ref, dy, sdy, dcb, dcr, sdc);
+      mc_thread_rec<false>(g, geo, taps, mc, tab.ref, dst);
   return 0;
 }
 
@@ -216,9 +239,9 @@ extern "C" int twin_mc_subblock(const mm_seq_params* p, int use, int bcw, int hp
   Geometry geo = t.geo;
   geo.hp = hp;
   if (hp)
-    mc_thread_rec<true>(0, geo, taps, mc, refs, out_y, 4, out_cb, out_cr, 2);
+    mc_thread_rec<true>(0, geo, taps, mc, refs, one_dst(out_y, 4, out_cb, out_cr, 2));
   else
-    mc_thread_rec<false>(0, geo, taps, mc, refs, out_y, 4, out_cb, out_cr, 2);
+    mc_thread_rec<false>(0, geo, taps, mc, refs, one_dst(out_y, 4, out_cb, out_cr, 2));
   return 0;
 }
 
@@ -242,6 +265,37 @@ extern "C" int twin_pred(const mm_seq_params* p, int n_epi, const int32_t* epi, 
   int rc = build_pic_tables(seq_info(*p), em, cur_poc, refs, &tab, &err);
   if (rc) return rc;
   return twin_pred_list(t, tab, pus, n, dy, sdy, dcb, dcr, sdc);
+}
+
+// mm_pred_device_multi twin: n_pics pictures (cur_pocs[q], PUs [pic_base[q], pic_base[q + 1]) of
+// `pus`) planned and predicted as ONE list, each into its own planes (dys[q], dcbs[q], dcrs[q]).
+extern "C" int twin_pred_multi(const mm_seq_params* p, int n_epi, const int32_t* epi, int n_pics,
+                               const int32_t* cur_pocs, const mm_pu_desc* pus, const int32_t* pic_base, int n_refs,
+                               const int32_t* pocs, const int16_t* const* ys, const int16_t* const* cbs,
+                               const int16_t* const* crs, int stride_y, int stride_c, int16_t* const* dys, int sdy,
+                               int16_t* const* dcbs, int16_t* const* dcrs, int sdc) {
+  using namespace mmdev;
+  Twin t;
+  make_twin(p, &t);
+  EpipoleMap em = epi_of(n_epi, epi);
+  std::vector<std::pair<int, RefDev>> refs;
+  for (int i = 0; i < n_refs; i++)
+    refs.emplace_back(pocs[i], RefDev{ys[i], cbs ? cbs[i] : nullptr, crs ? crs[i] : nullptr, stride_y, stride_c, 0u, 0u});
+  std::sort(refs.begin(), refs.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+  PicTables tab;
+  std::string err;
+  int rc = build_pic_tables(seq_info(*p), em, cur_pocs, n_pics, refs, &tab, &err);
+  if (rc) return rc;
+  DstPlanes d{};
+  for (int q = 0; q < MM_MAX_PICS; q++) {
+    const int k = q < n_pics ? q : 0;
+    d.y[q] = dys[k];
+    d.cb[q] = dcbs[k];
+    d.cr[q] = dcrs[k];
+    d.sy[q] = sdy;
+    d.sc[q] = sdc;
+  }
+  return twin_pred_segs(t, tab, pus, pic_base[n_pics], pic_base, d);
 }
 
 // mm_pred_list twin: one list of every PU, 14-bit (hp = 1) or clipped (hp = 0).

@@ -37,6 +37,9 @@ def load():
                                     c_int]
     lib.twin_sad_window.argtypes = [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
                                     c_void_p, c_int, c_void_p, c_int, c_void_p]
+    lib.twin_pred_multi.argtypes = [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
+                                    c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p,
+                                    c_int]
     lib.twin_mc_subblock.argtypes = [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                                      c_int, c_void_p, c_void_p, c_void_p]
     return lib
@@ -81,6 +84,29 @@ def predict(params, cur_poc, pus, refs, W, H, epipoles=(), dmvr=False):
     if rc:
         raise RuntimeError(f"twin predict failed: {rc}")
     return dy, dcb, dcr
+
+
+def predict_multi(params, pictures, refs, W, H, epipoles=()):
+    """mm_pred_device_multi twin: pictures = [(cur_poc, pus)], predicted as one list; planes per picture."""
+    lib = load()
+    allp = np.ascontiguousarray(np.concatenate([p for _, p in pictures]))
+    base = np.cumsum([0] + [len(p) for _, p in pictures]).astype(np.int32)
+    cur = np.array([c for c, _ in pictures], dtype=np.int32)
+    pocs = sorted(refs)
+    arrs = [[np.ascontiguousarray(refs[p][k]) for p in pocs] for k in range(3)]
+    ptrs = [(c_void_p * len(pocs))(*[a.ctypes.data for a in arrs[k]]) for k in range(3)]
+    outs = [(np.zeros((H, W), np.int16), np.zeros((H // 2, W // 2), np.int16), np.zeros((H // 2, W // 2), np.int16))
+            for _ in pictures]
+    dp = [(c_void_p * len(outs))(*[o[k].ctypes.data for o in outs]) for k in range(3)]
+    pa = np.array(pocs, dtype=np.int32)
+    n_epi, ea = _epi(epipoles)
+    rc = lib.twin_pred_multi(ctypes.addressof(params), n_epi, c_void_p(ea.ctypes.data), len(pictures),
+                             c_void_p(cur.ctypes.data), c_void_p(allp.ctypes.data), c_void_p(base.ctypes.data),
+                             len(pocs), c_void_p(pa.ctypes.data), ptrs[0], ptrs[1], ptrs[2], arrs[0][0].shape[1],
+                             arrs[1][0].shape[1], dp[0], W, dp[1], dp[2], W // 2)
+    if rc:
+        raise RuntimeError(f"twin predict_multi failed: {rc}")
+    return outs
 
 
 def predict_list(params, cur_poc, pus, list_, hp, refs, W, H, epipoles=()):

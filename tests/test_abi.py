@@ -48,6 +48,10 @@ def test_struct_layouts_match_header():
     n_fields = sum(len(re.findall(r"\w+\s*(?:,|;)", l.split("/*")[0])) for l in body.splitlines() if ";" in l)
     assert ctypes.sizeof(mm360.SeqParams) == 4 * n_fields == 36
     assert mm360.BLOCK_DTYPE.itemsize == 40 and mm360.PU_DTYPE.itemsize == 64
+    # mm_pic_job (mm_pred_device_multi): natural C alignment on LP64
+    assert ctypes.sizeof(mm360.PicJob) == 64
+    assert [getattr(mm360.PicJob, f).offset for f in ("cur_poc", "d_pus", "n", "dst_y", "dst_stride_y", "dst_cb",
+                                                      "dst_cr", "dst_stride_c")] == [0, 8, 16, 24, 32, 40, 48, 56]
 
 
 def test_product_has_no_oracle_dependency():

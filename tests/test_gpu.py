@@ -395,6 +395,45 @@ def test_pred_contexts_in_flight_together():
                     assert np.array_equal(got, x), (k, r, plane_mismatch(name, got, x))
 
 
+@pytest.mark.parametrize("plan_ahead", [False, True])
+def test_pred_device_multi_pictures_vs_oracle(plan_ahead):
+    """mm_pred_device_multi: three independent C2 pictures (own current POC, camera-pose epipole,
+    PU list and planes) in ONE launch chain == the oracle picture by picture; twice, so plan-ahead
+    reuses its slots; then a failing PU in the third picture is reported with its index counted
+    through the pictures' lists."""
+    from test_multi_picture import _pictures
+    cfg = W.CONFIGS["C2"]
+    models = tuple(cfg.models) + (mm360.GEODESIC_CAMPOSE,)
+    params = mm360.seq_params(cfg.width, cfg.height, models)
+    pics, refs, epis = _pictures(cfg, 3)
+    for _, pus in pics:
+        pus["model"][::7] = mm360.GEODESIC_CAMPOSE
+    orc = Oracle(params, epis)
+    want = [orc.predict(cur, pus, refs, cfg.width, cfg.height) for cur, pus in pics]
+    with _ctx(params, epis) as ctx:
+        ctx.set_plan_ahead(plan_ahead)
+        for poc, (y, cb, cr) in refs.items():
+            ctx.upload_ref(poc, torch.from_numpy(y).cuda(), torch.from_numpy(cb).cuda(), torch.from_numpy(cr).cuda())
+        d_lists = [mm360.pus_to_device(p) for _, p in pics]
+        torch.cuda.synchronize()
+        for rnd in range(2):
+            outs = [_planes(cfg, -3) for _ in pics]
+            ctx.predict_device_multi([(cur, d, *o) for (cur, _), d, o in zip(pics, d_lists, outs)])
+            assert ctx.status() == (mm360.MM_OK, -1)
+            for q, (o, w) in enumerate(zip(outs, want)):
+                for name, t, x in zip(("y", "cb", "cr"), o, w):
+                    got = t.cpu().numpy()
+                    assert np.array_equal(got, x), (rnd, q, plane_mismatch(name, got, x))
+        bad = pics[2][1].copy()
+        bad["x"][5] = 3  # not 4x4 aligned
+        d_bad = mm360.pus_to_device(bad)
+        outs = [_planes(cfg, 0) for _ in pics]
+        ctx.predict_device_multi([(pics[0][0], d_lists[0], *outs[0]), (pics[1][0], d_lists[1], *outs[1]),
+                                  (pics[2][0], d_bad, *outs[2])])
+        code, first = ctx.status()
+        assert code == mm360.MM_ERR_ARG and first == len(pics[0][1]) + len(pics[1][1]) + 5, (code, first)
+
+
 def test_pred_plan_ahead_rotating_pictures():
     """mm_set_plan_ahead: three different PU lists predicted back to back (twice round, so each
     plan slot is reused while the other picture's kernels may still run; a smaller list first, so

@@ -25,6 +25,11 @@ for step in "$@"; do
       rounds=$(echo "$step" | cut -d= -f2); vs=$(echo "$step" | cut -d= -f3 | tr ',' ' ')
       run "abb_$(echo "$vs" | tr ' ' '_')" 900 bash tools/ab_bench.sh "$rounds" $vs ;;
     example) run example 120 vvc-extension-mm_amd/lib/example_decode ;;
+    c5ab=*)  # c5ab=<v1,v2,...>: C5 (Mcandidates/s) of library variants (default = in-tree), one run each
+      for v in $(echo "$step" | cut -d= -f2 | tr ',' ' '); do
+        L=tmp_variants/$v/libmm360.so; [ "$v" = default ] && L=vvc-extension-mm_amd/lib/libmm360.so
+        run "c5_$v" 600 python bench.py --config C5 --steps 2 --warmup 1 --no-cpu-baseline --lib "$L"
+      done ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     bench_c4) run bench_c4 600 python bench.py --config C4 ;;

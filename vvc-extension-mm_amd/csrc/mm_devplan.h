@@ -26,6 +26,10 @@ using mmdmvr::N_OFF;
 using mmdmvr::SubPuDev;
 
 constexpr int MAX_SLOTS = 16;  // reference pictures addressable by one picture (2 lists x 8)
+// Pictures one launch chain predicts together (mm_pred_device_multi): independent pictures -- the
+// leaves of a random-access temporal layer -- share the planning, setup, reprojection and
+// interpolation launches; each PU carries its picture index (PuPlan::seg, McRec meta bits 14-15).
+constexpr int MAX_PICS = MM_MAX_PICS;
 // PU buckets: N_BANDS vertical strips of the picture (by the PU's left column), or one bucket.
 // Inside a bucket PUs keep the list's (decode, raster-CTU) order -- k_plan_place places them with
 // a block-wide scan per bucket -- so the sub-block enumeration k_mc reads is spatial, and k_mc
@@ -61,7 +65,7 @@ constexpr int DMVR_KEY = N_PU_KEYS + N_JOB_KEYS;  // one bucket of MM-DMVR sub-P
 struct PicTables {
   int n_slots;
   int poc[MAX_SLOTS];
-  int ged_cam[MAX_SLOTS];  // GED table index of GEODESIC_CAMPOSE for (cur, poc[s]), -1 = no epipole
+  int8_t ged_cam[MAX_PICS][MAX_SLOTS];  // GED table index of GEODESIC_CAMPOSE for (cur of picture q, poc[s]), -1: none
   RefDev ref[MAX_SLOTS];
   M3 ged[3 + MAX_SLOTS];   // [0..2] GEODESIC_X/Y/Z, [3+s] CAMPOSE of slot s
   int W, H, chroma;
@@ -71,7 +75,32 @@ struct PicTables {
   int dmvr;                // MM_PUF_DMVR PUs allowed (mm_set_dmvr: the picture's DMVR enable)
   RefPool pool;            // the context's reference pool (device interior filters)
   uint32_t pool_slot4[MAX_SLOTS / 4];  // pool slot of table slot s: byte s % 4 of word s / 4 (device)
+  int n_pics;              // pictures of the call (mm_pred_device_multi; 1 otherwise)
 };
+
+// The PU lists of a call's pictures (device pointers), one index space: picture q holds PUs
+// [base[q], base[q + 1]).  Read by select, never by a per-lane index into the kernel argument.
+struct PuSegs {
+  const mm_pu_desc* p[MAX_PICS];
+  int base[MAX_PICS + 1];
+  int n_pics;
+};
+// picture of PU index i (uniform loop)
+MM_HD int pu_seg(const PuSegs& s, int i) {
+  int q = 0;
+#pragma unroll
+  for (int k = 1; k < MAX_PICS; k++) q += (k < s.n_pics && i >= s.base[k]) ? 1 : 0;
+  return q;
+}
+MM_HD mm_pu_desc load_pu(const PuSegs& s, int i, int q) {
+  const mm_pu_desc* p = s.p[0];
+#pragma unroll
+  for (int k = 1; k < MAX_PICS; k++) p = q == k ? s.p[k] : p;
+  int b = s.base[0];
+#pragma unroll
+  for (int k = 1; k < MAX_PICS; k++) b = q == k ? s.base[k] : b;
+  return p[i - b];
+}
 
 // Offsets of everything k_plan_place produced; written by k_plan_place's first thread.
 struct PlanMeta {
@@ -96,6 +125,7 @@ struct JobPlan {
 
 struct PuPlan {
   int code;     // MM_OK or the error this PU raises
+  int seg;      // picture of the call (mm_pred_device_multi)
   int cls;      // 0 bi, 1 uni L0, 2 uni L1
   int key;      // PU bucket (pu_key)
   int n_sb;     // luma 4x4 sub-blocks (of the whole PU)
@@ -128,8 +158,9 @@ MM_HD bool mpa_chroma_aliases(const PicTables& t, int model, int w, int h) {
 
 // Classification of one PU: argument checks (the reference CHECKs sizes and models), slot and GED lookup,
 // and the list of reprojection jobs it needs.
-MM_HD void classify_pu(const mm_pu_desc& u, const PicTables& t, PuPlan* p) {
+MM_HD void classify_pu(const mm_pu_desc& u, const PicTables& t, PuPlan* p, int seg = 0) {
   p->code = MM_OK;
+  p->seg = seg;
   for (int k = 0; k < 4; k++) p->job[k].valid = 0;
   p->cls = 0;
   p->key = 0;
@@ -183,11 +214,14 @@ MM_HD void classify_pu(const mm_pu_desc& u, const PicTables& t, PuPlan* p) {
       p->code = MM_ERR_MODEL;
       return;
     }
-    int s = -1, cam = -1;  // the table is read at uniform indices only (kernel argument: scalar loads)
+    int s = -1, cam = -1;  // the tables are read at uniform indices (no per-lane index into the argument)
     for (int k = 0; k < t.n_slots; k++)
       if (t.poc[k] == u.ref_poc[l]) {
         s = k;
-        cam = t.ged_cam[k];
+        int c = t.ged_cam[0][k];
+#pragma unroll
+        for (int q = 1; q < MAX_PICS; q++) c = seg == q ? t.ged_cam[q][k] : c;
+        cam = c;
       }
     if (s < 0) {
       p->code = MM_ERR_NOREF;
@@ -305,7 +339,8 @@ MM_HD void emit_pu(const mm_pu_desc& u, const PuPlan& p, int sb_off, const int* 
                    SubPuDev* subs = nullptr, int* sub_off = nullptr, int* sub_chunk = nullptr) {
   const int primary = p.cls == 2 ? 1 : 0;
   const int meta_hi = (p.slot[0] < 0 ? 0 : p.slot[0]) | ((p.slot[1] < 0 ? 0 : p.slot[1]) << 4) | (p.bcw << 8) |
-                      (p.slot[0] >= 0 ? MM_META_USE0 : 0) | (p.slot[1] >= 0 ? MM_META_USE1 : 0);
+                      (p.slot[0] >= 0 ? MM_META_USE0 : 0) | (p.slot[1] >= 0 ? MM_META_USE1 : 0) |
+                      (p.seg << MM_META_SEG_SHIFT);
   const int n_sb_sub = (p.sub_w / 4) * (p.sub_h / 4);
   for (int s = 0; s < p.n_items; s++) {
     const int x = u.x + (s % p.sx) * p.sub_w, y = u.y + (s / p.sx) * p.sub_h;

@@ -124,7 +124,7 @@ constexpr int N_KEYS = DMVR_KEY + 1;  // one row of `blk`: PU buckets, job bucke
 
 // status: the picture's validation word (0 = ok, else ~((pu_index << 8) | code) of the lowest
 // failing PU, combined with atomicMax over every stripe of the picture).
-__global__ void __launch_bounds__(PLAN_BLOCK) k_plan_count(const mm_pu_desc* __restrict__ pus, int n, int pu_base,
+__global__ void __launch_bounds__(PLAN_BLOCK) k_plan_count(const PuSegs pus, int n, int pu_base,
                                                     const PicTables t, unsigned long long* __restrict__ status,
                                                     unsigned long long* __restrict__ blk,
                                                     unsigned long long* __restrict__ blkq, int n_quarters) {
@@ -135,9 +135,10 @@ __global__ void __launch_bounds__(PLAN_BLOCK) k_plan_count(const mm_pu_desc* __r
   __syncthreads();
   const int i = blockIdx.x * blockDim.x + tid;
   if (i < n) {
-    const mm_pu_desc u = pus[i];
+    const int pic = pu_seg(pus, i);
+    const mm_pu_desc u = load_pu(pus, i, pic);
     PuPlan p;
-    classify_pu(u, t, &p);
+    classify_pu(u, t, &p, pic);
     if (p.code != MM_OK) {
       atomicMax(&s_status, status_word(pu_base + i, p.code));
     } else {
@@ -164,7 +165,7 @@ __global__ void __launch_bounds__(PLAN_BLOCK) k_plan_count(const mm_pu_desc* __r
 
 // `next_status` is the other word of the picture ping-pong pair: the first stripe's block 0 zeroes
 // it for the next picture, so no memset launch precedes k_plan_count.
-__global__ void __launch_bounds__(PLACE_BLOCK) k_plan_place(const mm_pu_desc* __restrict__ pus, int n, const PicTables t,
+__global__ void __launch_bounds__(PLACE_BLOCK) k_plan_place(const PuSegs pus, int n, const PicTables t,
                                                      unsigned long long* __restrict__ status,
                                                      unsigned long long* __restrict__ next_status,
                                                      const unsigned long long* __restrict__ blk, int n_blocks,
@@ -290,8 +291,9 @@ __global__ void __launch_bounds__(PLACE_BLOCK) k_plan_place(const mm_pu_desc* __
   mm_pu_desc u;
   unsigned long long lp = 0, lj[4] = {0, 0, 0, 0}, ld = 0;
   if (i < n) {
-    u = pus[i];
-    classify_pu(u, t, &p);
+    const int pic = pu_seg(pus, i);
+    u = load_pu(pus, i, pic);
+    classify_pu(u, t, &p, pic);
     if (p.code == MM_OK) {
 #pragma unroll
       for (int k = 0; k < 4; k++)
@@ -413,19 +415,23 @@ __global__ void __launch_bounds__(256) k_reproj_dev(SeqConst sc, const PlanMeta*
 static_assert(N_BANDS == 8, "one band per XCD");
 template <bool UNI_HP>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k_mc_dev(Geometry geo, const PlanMeta* __restrict__ meta, McRec mc,
-                                                const PicTables t, int16_t* __restrict__ dst_y, int dsy,
-                                                int16_t* __restrict__ dst_cb, int16_t* __restrict__ dst_cr, int dsc) {
+                                                const PicTables t, const DstPlanes dst) {
   const int band = blockIdx.x & 7, stride = (int)(gridDim.x >> 3) * 256;
   const int n_sb = meta->n_sb;  // (second guard: a band never reaches past the plan's sub-blocks)
   const int b0 = meta->band[band], b1 = min(meta->band[band + 1], n_sb);
   __shared__ PackedTaps s_taps;
   __shared__ RefDev s_ref[MAX_SLOTS];
+  __shared__ DstPlanes s_dst;  // the pictures' planes, indexed per lane at the stores
   static_assert(sizeof(PackedTaps) % 16 == 0 && sizeof(PackedTaps) / 16 <= 256, "one 16-byte word per thread");
   const int first = b0 + (int)(blockIdx.x >> 3) * 256;
   if (first >= b1) return;  // whole workgroup past the band's end
   if (threadIdx.x < sizeof(PackedTaps) / 16)
     lds_put(reinterpret_cast<uint4*>(&s_taps)[threadIdx.x], reinterpret_cast<const uint4*>(&c_packed_taps)[threadIdx.x], make_uint4(~0u, ~0u, ~0u, ~0u));
   stage_ref_table<MAX_SLOTS>(t.pool_slot4, t.pool, s_ref);
+  // (probe poison 0: a store through an unstaged plane pointer would fault rather than read garbage,
+  // so the plane words get no poison store; the probe checks the taps and reference table)
+  for (int k = threadIdx.x; k < (int)(sizeof(DstPlanes) / 4); k += blockDim.x)
+    reinterpret_cast<uint32_t*>(&s_dst)[k] = reinterpret_cast<const uint32_t*>(&dst)[k];
   __syncthreads();
   const Taps taps{c_luma_taps, c_chroma_taps, &s_taps, t.pool};
   // s_ref: each lane looks its slots' pool offsets up in LDS; indexing the kernel-argument copy
@@ -437,7 +443,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k
     const int gn = g + stride;
     McIn nxt;
     if (gn - (int)threadIdx.x < b1) nxt = mc_rec_load(mc, min(gn, b1 - 1));
-    if (g < b1) mc_thread_in<UNI_HP>(g, cur, geo, taps, mc, s_ref, dst_y, dsy, dst_cb, dst_cr, dsc);
+    if (g < b1) mc_thread_in<UNI_HP>(g, cur, geo, taps, mc, s_ref, s_dst);
     cur = nxt;
   }
 }
@@ -493,7 +499,10 @@ __global__ void __launch_bounds__(256) k_me_chunks(const int* __restrict__ off, 
   chunk[c] = lo;
 }
 
-__global__ void __launch_bounds__(256) k_me_sad(SeqConst sc, Geometry geo, MeWindow w,
+#ifndef MM_ME_WAVES
+#define MM_ME_WAVES 4  // waves per SIMD of k_me_sad (its body alone would take 162 VGPRs: 3 waves)
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MM_ME_WAVES))) k_me_sad(SeqConst sc, Geometry geo, MeWindow w,
                                                 const MeBlockDev* __restrict__ blocks, int n_blocks,
                                                 const int* __restrict__ blk_off, const int* __restrict__ chunk,
                                                 int n_elems, const BlockSetup* __restrict__ setups, MpaCache cache,
@@ -1074,6 +1083,7 @@ struct PlanSlot {
   DevBuf<SubPuDev> dmvr_sub;  // MM-DMVR sub-PU records (k_plan_place) and their element offsets / chunks
   DevBuf<int> dmvr_off, dmvr_chunk;
   int n_ensured = 0;  // largest stripe size the buffers were sized for (they only grow)
+  int pics_ensured = 1;  // pictures per call the sub-block capacity covers (mm_pred_device_multi)
   bool dmvr_ensured = false;
   PlanCaps caps{};
   void release() {
@@ -1778,9 +1788,10 @@ static int round_grid(long v) { return (int)((v + 8 * XCD_RUN - 1) / (8 * XCD_RU
 // With MM-DMVR a PU is placed as up to 64 sub-PUs (128x128 / 16x16); a sub-PU covers at least 128
 // luma samples (PU::checkDMVRCondition), so the picture bounds them by W * H / 128, and their cost
 // elements (N_OFF per luma sub-block) by N_OFF times the picture's sub-blocks.
-static int ensure_slot_buffers(mm_ctx* c, PlanSlot& S, int n, bool dmvr) {
+static int ensure_slot_buffers(mm_ctx* c, PlanSlot& S, int n, bool dmvr, int pics = 1) {
   PlanCaps k;
-  const long area_sb = (long)(c->geo.W / 4) * (c->geo.H / 4);
+  pics = std::max(pics, S.pics_ensured);  // (buffers only grow)
+  const long area_sb = (long)(c->geo.W / 4) * (c->geo.H / 4) * pics;  // each picture predicts each sample once
   const int subs = dmvr ? (int)std::min<long>((long)n * 64, (long)c->geo.W * c->geo.H / 128) : 0;
   k.pus = n + subs;
   k.jobs = 4 * k.pus;
@@ -1831,18 +1842,21 @@ static int ensure_slot_buffers(mm_ctx* c, PlanSlot& S, int n, bool dmvr) {
     }
   }
   S.n_ensured = std::max(S.n_ensured, n);
+  S.pics_ensured = pics;
   return MM_OK;
 }
-static bool slot_fits(const PlanSlot& S, int n, bool dmvr) { return n <= S.n_ensured && (!dmvr || S.dmvr_ensured); }
+static bool slot_fits(const PlanSlot& S, int n, bool dmvr, int pics = 1) {
+  return n <= S.n_ensured && pics <= S.pics_ensured && (!dmvr || S.dmvr_ensured);
+}
 
 // One stripe (PUs [base, base + n) of the picture's list) through k_plan_count + k_plan_place +
 // k_setup_dev + k_reproj_dev + k_mc_dev on `st`.  Stage events only in single-stripe timing mode.
 // status: the picture's status word; next_status (first stripe only): the word to zero for the
 // next picture.
 static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables& t, const Geometry& geo,
-                         const mm_pu_desc* d_in, int n, int base, unsigned long long* status,
-                         unsigned long long* next_status, int16_t* dy, ptrdiff_t sdy, int16_t* dcb, int16_t* dcr,
-                         ptrdiff_t sdc, bool plan_ahead = false, bool want_mvd = false, hipEvent_t mc_done = nullptr) {
+                         const PuSegs& d_in, int n, int base, unsigned long long* status,
+                         unsigned long long* next_status, const DstPlanes& dst, bool plan_ahead = false,
+                         bool want_mvd = false, hipEvent_t mc_done = nullptr) {
   // plan-ahead: `st` is the auxiliary stream for the planning kernels; the rest runs on the
   // context stream (which may be the null stream, so a flag, not a null handle, says so)
   hipStream_t st_back = c->stream;
@@ -1928,11 +1942,9 @@ static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables
   // mc_done (plan-ahead): the slot's gate, complete when this k_mc is
   hipEvent_t stop = KERNEL_EVENTS ? mc_done : nullptr;
   if (geo.hp)
-    hipExtLaunchKernelGGL(k_mc_dev<true>, dim3(gm), dim3(256), 0, st, nullptr, stop, 0, geo, S.meta.p, mc, t, dy, (int)sdy, dcb,
-                          dcr, (int)sdc);
+    hipExtLaunchKernelGGL(k_mc_dev<true>, dim3(gm), dim3(256), 0, st, nullptr, stop, 0, geo, S.meta.p, mc, t, dst);
   else
-    hipExtLaunchKernelGGL(k_mc_dev<false>, dim3(gm), dim3(256), 0, st, nullptr, stop, 0, geo, S.meta.p, mc, t, dy, (int)sdy,
-                          dcb, dcr, (int)sdc);
+    hipExtLaunchKernelGGL(k_mc_dev<false>, dim3(gm), dim3(256), 0, st, nullptr, stop, 0, geo, S.meta.p, mc, t, dst);
   if (mc_done && !KERNEL_EVENTS) HIPCHK(c, hipEventRecord(mc_done, st));
   HIPCHK(c, hipGetLastError());
   return MM_OK;
@@ -1947,15 +1959,15 @@ static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables
 // only_list / hp / store: mm_pred_list (-1 / 0 / 3 for the normal prediction).
 // dmvr: MM_PUF_DMVR PUs allowed (the context's mm_set_dmvr, or mm_pred_dmvr); want_mvd: keep the
 // refined delta of every DMVR sub-PU, in placement order, in d_dmvr_mvd.
-static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, int n, int16_t* dy, ptrdiff_t sdy,
-                              int16_t* dcb, int16_t* dcr, ptrdiff_t sdc, int only_list = -1, int hp = 0,
-                              int store = 3, bool may_plan_ahead = false, bool dmvr = false,
-                              bool want_mvd = false) {
+static int launch_pictures(mm_ctx* c, const mm_pic_job* pics, int n_pics, int only_list = -1, int hp = 0,
+                           int store = 3, bool may_plan_ahead = false, bool dmvr = false, bool want_mvd = false) {
   std::vector<std::pair<int, RefDev>> refs;
   refs = ref_slots(c);
   PicTables t;
   std::string err;
-  int rc = build_pic_tables(seq_info(c->prm), c->epipoles, cur_poc, refs, &t, &err);
+  int cur[MAX_PICS];
+  for (int q = 0; q < n_pics; q++) cur[q] = pics[q].cur_poc;
+  int rc = build_pic_tables(seq_info(c->prm), c->epipoles, cur, n_pics, refs, &t, &err);
   if (rc) return fail(c, rc, err);
   RCCHK(device_tables(c, &t));
   t.only_list = only_list;
@@ -1963,31 +1975,65 @@ static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, in
   Geometry geo = c->geo;
   geo.hp = hp;
   geo.store = store;
-  geo.vec_store = (!dy || ((uintptr_t)dy % 8 == 0 && sdy % 4 == 0)) &&
-                  (!geo.chroma || !dcb || ((uintptr_t)dcb % 4 == 0 && (uintptr_t)dcr % 4 == 0 && sdc % 2 == 0));
-  // one stripe under stage timing, and with DMVR (its setup / cost buffers are the context's)
-  const int K = (c->stage_timing || dmvr) ? 1 : std::max(1, std::min(c->n_stripes, (n + PLAN_BLOCK - 1) / PLAN_BLOCK));
+  // destinations of the pictures (unused entries repeat picture 0's, so every pointer is valid)
+  DstPlanes dst{};
+  int n = 0;
+  geo.vec_store = 1;
+  for (int q = 0; q < MAX_PICS; q++) {
+    const mm_pic_job& p = pics[q < n_pics ? q : 0];
+    dst.y[q] = p.dst_y;
+    dst.cb[q] = p.dst_cb;
+    dst.cr[q] = p.dst_cr;
+    dst.sy[q] = (int)p.dst_stride_y;
+    dst.sc[q] = (int)p.dst_stride_c;
+    if (q < n_pics) {
+      n += p.n;
+      const bool vy = !p.dst_y || ((uintptr_t)p.dst_y % 8 == 0 && p.dst_stride_y % 4 == 0);
+      const bool vc = !geo.chroma || !p.dst_cb ||
+                      ((uintptr_t)p.dst_cb % 4 == 0 && (uintptr_t)p.dst_cr % 4 == 0 && p.dst_stride_c % 2 == 0);
+      if (!(vy && vc)) geo.vec_store = 0;
+    }
+  }
+  // one stripe under stage timing, with DMVR (its setup / cost buffers are the context's) and for
+  // several pictures
+  const int K = (c->stage_timing || dmvr || n_pics > 1)
+                    ? 1
+                    : std::max(1, std::min(c->n_stripes, (n + PLAN_BLOCK - 1) / PLAN_BLOCK));
   const int per = (n + K - 1) / K;
+  // PU lists of stripe s of a single picture, or of every picture
+  auto segs_of = [&](int base, int m) {
+    PuSegs g{};
+    g.n_pics = K > 1 ? 1 : n_pics;
+    int acc = 0;
+    for (int q = 0; q < MAX_PICS; q++) {
+      const mm_pic_job& p = pics[q < g.n_pics ? q : 0];
+      g.p[q] = K > 1 ? p.d_pus + base : p.d_pus;
+      g.base[q] = acc;
+      if (q < g.n_pics) acc += K > 1 ? m : p.n;
+    }
+    g.base[MAX_PICS] = acc;
+    return g;
+  };
   unsigned long long* status = c->d_status.p + c->pic_par;
   unsigned long long* next_status = c->d_status.p + (c->pic_par ^ 1);
   if (may_plan_ahead && c->plan_ahead && K == 1 && !c->stage_timing) {
     // Plan-ahead: planning + setup of this picture on `aux`, gated only by the k_mc_dev of the
     // slot's previous user (two calls back), so they overlap the previous picture's kernels.
-    if (!slot_fits(c->slot[0], per, dmvr) || !slot_fits(c->slot[1], per, dmvr)) {
+    if (!slot_fits(c->slot[0], per, dmvr, n_pics) || !slot_fits(c->slot[1], per, dmvr, n_pics)) {
       // growing frees buffers the other stream may still use, and zeroes on the context stream
       HIPCHK(c, hipStreamSynchronize(c->aux));
       HIPCHK(c, hipStreamSynchronize(c->stream));
-      for (int s = 0; s < 2; s++) RCCHK(ensure_slot_buffers(c, c->slot[s], per, dmvr));
+      for (int s = 0; s < 2; s++) RCCHK(ensure_slot_buffers(c, c->slot[s], per, dmvr, n_pics));
       HIPCHK(c, hipStreamSynchronize(c->stream));
     } else {
-      for (int s = 0; s < 2; s++) RCCHK(ensure_slot_buffers(c, c->slot[s], per, dmvr));  // caps only
+      for (int s = 0; s < 2; s++) RCCHK(ensure_slot_buffers(c, c->slot[s], per, dmvr, n_pics));  // caps only
     }
     // the slot's previous user (two calls back) has finished its k_mc_dev
     HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_gate[c->ahead_par], 0));
     c->timed = c->call_timing;
     if (c->timed) HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-    RCCHK(launch_stripe(c, c->slot[c->ahead_par], c->aux, t, geo, d_in, n, 0, status, next_status, dy, sdy, dcb, dcr,
-                        sdc, true, want_mvd, c->ev_gate[c->ahead_par]));
+    RCCHK(launch_stripe(c, c->slot[c->ahead_par], c->aux, t, geo, segs_of(0, n), n, 0, status, next_status, dst, true,
+                        want_mvd, c->ev_gate[c->ahead_par]));
     c->ahead_par ^= 1;
     if (c->timed) HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     c->last_status = status;
@@ -1997,8 +2043,8 @@ static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, in
   }
   for (int s = 0; s < std::min(K, 2); s++) {
     // growth of buffers a plan-ahead call on the auxiliary stream may still use
-    if (!slot_fits(c->slot[s], per, dmvr)) HIPCHK(c, hipStreamSynchronize(c->aux));
-    RCCHK(ensure_slot_buffers(c, c->slot[s], per, dmvr));
+    if (!slot_fits(c->slot[s], per, dmvr, n_pics)) HIPCHK(c, hipStreamSynchronize(c->aux));
+    RCCHK(ensure_slot_buffers(c, c->slot[s], per, dmvr, n_pics));
   }
   // each event a call records costs the context stream ~4 us (profiles/r03_ab_event_scope.txt)
   c->timed = c->call_timing || c->stage_timing;
@@ -2010,8 +2056,8 @@ static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, in
   for (int s = 0; s < K; s++) {
     const int base = s * per, m = std::min(per, n - base);
     if (m <= 0) break;
-    RCCHK(launch_stripe(c, c->slot[s & 1], (s & 1) ? c->aux : c->stream, t, geo, d_in + base, m, base, status,
-                        s == 0 ? next_status : nullptr, dy, sdy, dcb, dcr, sdc, false, want_mvd));
+    RCCHK(launch_stripe(c, c->slot[s & 1], (s & 1) ? c->aux : c->stream, t, geo, segs_of(base, m), m, base, status,
+                        s == 0 ? next_status : nullptr, dst, false, want_mvd));
   }
   if (K > 1) {
     HIPCHK(c, hipEventRecord(c->ev_join, c->aux));
@@ -2028,6 +2074,14 @@ static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, in
   c->pic_par ^= 1;
   c->status_pending = true;
   return MM_OK;
+}
+// one picture
+static int launch_device_plan(mm_ctx* c, int cur_poc, const mm_pu_desc* d_in, int n, int16_t* dy, ptrdiff_t sdy,
+                              int16_t* dcb, int16_t* dcr, ptrdiff_t sdc, int only_list = -1, int hp = 0,
+                              int store = 3, bool may_plan_ahead = false, bool dmvr = false,
+                              bool want_mvd = false) {
+  const mm_pic_job p{cur_poc, d_in, n, dy, sdy, dcb, dcr, sdc};
+  return launch_pictures(c, &p, 1, only_list, hp, store, may_plan_ahead, dmvr, want_mvd);
 }
 
 int mm_set_plan_ahead(mm_ctx* c, int on) {
@@ -2082,6 +2136,22 @@ int mm_pred_device(mm_ctx* c, int cur_poc, const mm_pu_desc* d_pus, int n, int16
   if (n == 0) return MM_OK;
   HIPCHK(c, hipSetDevice(c->device));
   return launch_device_plan(c, cur_poc, d_pus, n, dy, sdy, dcb, dcr, sdc, -1, 0, 3, true, c->dmvr);
+}
+
+int mm_pred_device_multi(mm_ctx* c, const mm_pic_job* pics, int n_pics) {
+  if (!c || n_pics < 1 || n_pics > MAX_PICS || !pics) return MM_ERR_ARG;
+  long n = 0;
+  for (int q = 0; q < n_pics; q++) {
+    const mm_pic_job& p = pics[q];
+    if (p.n < 0 || (p.n > 0 && !p.d_pus) || !p.dst_y || (c->geo.chroma && (!p.dst_cb || !p.dst_cr))) return MM_ERR_ARG;
+    n += p.n;
+  }
+  if (n > INT32_MAX / 2) return MM_ERR_ARG;
+  if (n == 0) return MM_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (n_pics == 1)
+    return launch_pictures(c, pics, 1, -1, 0, 3, true, c->dmvr);
+  return launch_pictures(c, pics, n_pics, -1, 0, 3, true, false);  // MM-DMVR: one picture per call
 }
 
 int mm_set_dmvr(mm_ctx* c, int on) {

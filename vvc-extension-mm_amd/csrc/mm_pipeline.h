@@ -55,9 +55,10 @@ struct alignas(8) mm_int2 {
 };
 // Per-luma-sub-block inputs of k_mc, written by the reprojection of a device-planned picture in
 // the order k_mc reads them (sub-block g of the enumeration):
-//   meta[g]    = (ox | oy << 16, slot0 | slot1 << 4 | bcw << 8 | use0 << 12 | use1 << 13): output
-//                position of the luma 4x4 sub-block, reference slot per list, BCW index, the lists
-//                the sub-block uses -- written by the PU's primary job;
+//   meta[g]    = (ox | oy << 16, slot0 | slot1 << 4 | bcw << 8 | use0 << 12 | use1 << 13 | pic << 14):
+//                output position of the luma 4x4 sub-block, reference slot per list, BCW index, the
+//                lists the sub-block uses, the picture of a multi-picture call -- written by the PU's
+//                primary job;
 //   lpos[l][g] = the list-l luma position in 1/16 pel relative to the sub-block origin
 //                (16 ox, 16 oy), as two int16 (x lo, y hi) -- written by the luma job;
 //   cpos[l][g] = the 4:2:0 chroma position in 1/32 pel relative to (32 (ox / 2), 32 (oy / 2)),
@@ -83,6 +84,19 @@ MM_HD uint32_t pack_rel(int32_t fx, int32_t fy, int32_t bx, int32_t by) {
 #define MM_META_PRIMARY (1 << 16)
 #define MM_META_USE0 (1 << 12)
 #define MM_META_USE1 (1 << 13)
+#define MM_META_SEG_SHIFT 14  // bits 14-15: the picture of a multi-picture call (mm_pred_device_multi)
+#ifndef MM_MAX_PICS
+#define MM_MAX_PICS 4  // include/mm360.h
+#endif
+
+// The destination planes of a call's pictures (device pointers; picture q of mm_pred_device_multi,
+// q = 0 for a single picture), picked by the sub-block's picture index with selects.
+struct DstPlanes {
+  int16_t* y[MM_MAX_PICS];
+  int16_t* cb[MM_MAX_PICS];
+  int16_t* cr[MM_MAX_PICS];
+  int sy[MM_MAX_PICS], sc[MM_MAX_PICS];
+};
 
 // w1 = g_BcwWeights[bcw] (Rom.cpp:203 {-2, 3, 4, 5, 10}) as nibbles of w1 + 2; w0 = 8 - w1
 MM_HD int bcw_w1(int bcw) { return (int)((0xC7650u >> (4 * bcw)) & 15u) - 2; }
@@ -442,8 +456,11 @@ MM_HD McIn mc_rec_load(const McRec& mc, int g) {
 
 template <bool HP>
 MM_HD void mc_rec_impl(int g, const McIn& in, const Geometry& geo, const Taps& taps, const McRec& mc,
-                       const RefDev* refs, int16_t* dst_y, int dsy, int16_t* dst_cb, int16_t* dst_cr, int dsc) {
+                       const RefDev* refs, const DstPlanes& dst) {
   const mm_int2 meta = in.meta;
+  // the picture's planes: `dst` is an LDS copy on the device (k_mc_dev), so a per-lane index reads LDS
+  // at the store, and no plane pointer is held in registers through the filter
+  const int pic = (meta.y >> MM_META_SEG_SHIFT) & (MM_MAX_PICS - 1);
   const bool used[2] = {(meta.y & MM_META_USE0) != 0, (meta.y & MM_META_USE1) != 0};
   const int ox = meta.x & 0xffff, oy = meta.x >> 16;
   mm_int4 P[2];  // (luma x, y in 1/16 pel, chroma x, y in 1/32 pel) per list
@@ -507,7 +524,7 @@ MM_HD void mc_rec_impl(int g, const McIn& in, const Geometry& geo, const Taps& t
         const int a = pa ? pl[1][i] : pl[0][i];
         o[c] = HP ? (int16_t)a : weighted_avg(a, pl[1][i], wa, wb, geo.bd);
       }
-      store_row<4>(dst_y + (long)(oy + r) * dsy + ox, o, geo.vec_store);
+      store_row<4>(dst.y[pic] + (long)(oy + r) * dst.sy[pic] + ox, o, geo.vec_store);
     }
   }
   if (!geo.chroma || !(geo.store & 2)) return;
@@ -554,8 +571,8 @@ MM_HD void mc_rec_impl(int g, const McIn& in, const Geometry& geo, const Taps& t
       ob[c] = HP ? (int16_t)ab : weighted_avg(ab, pcb[1][i], wa, wb, geo.bd);
       orr[c] = HP ? (int16_t)ar : weighted_avg(ar, pcr[1][i], wa, wb, geo.bd);
     }
-    store_row<2>(dst_cb + (long)(cy + r) * dsc + cx, ob, geo.vec_store);
-    store_row<2>(dst_cr + (long)(cy + r) * dsc + cx, orr, geo.vec_store);
+    store_row<2>(dst.cb[pic] + (long)(cy + r) * dst.sc[pic] + cx, ob, geo.vec_store);
+    store_row<2>(dst.cr[pic] + (long)(cy + r) * dst.sc[pic] + cx, orr, geo.vec_store);
   }
 }
 
@@ -563,13 +580,13 @@ MM_HD void mc_rec_impl(int g, const McIn& in, const Geometry& geo, const Taps& t
 // a separate kernel instance, so the picture path's register allocation does not carry it.
 template <bool UNI_HP = false>
 MM_HD void mc_thread_rec(int g, const Geometry& geo, const Taps& taps, const McRec& mc, const RefDev* refs,
-                         int16_t* dst_y, int dsy, int16_t* dst_cb, int16_t* dst_cr, int dsc) {
-  mc_rec_impl<UNI_HP>(g, mc_rec_load(mc, g), geo, taps, mc, refs, dst_y, dsy, dst_cb, dst_cr, dsc);
+                         const DstPlanes& dst) {
+  mc_rec_impl<UNI_HP>(g, mc_rec_load(mc, g), geo, taps, mc, refs, dst);
 }
 template <bool UNI_HP = false>
 MM_HD void mc_thread_in(int g, const McIn& in, const Geometry& geo, const Taps& taps, const McRec& mc,
-                        const RefDev* refs, int16_t* dst_y, int dsy, int16_t* dst_cb, int16_t* dst_cr, int dsc) {
-  mc_rec_impl<UNI_HP>(g, in, geo, taps, mc, refs, dst_y, dsy, dst_cb, dst_cr, dsc);
+                        const RefDev* refs, const DstPlanes& dst) {
+  mc_rec_impl<UNI_HP>(g, in, geo, taps, mc, refs, dst);
 }
 
 }  // namespace mmpipe

@@ -202,15 +202,23 @@ class Planner {
 // fixed epipoles (MVReprojection.cpp:44-52) and the camera-pose epipole of (cur_poc, slot POC)
 // when the epipole list has one (EpipoleList.cpp:19-36; a PU that needs a missing one raises
 // MM_ERR_NOEPIPOLE on the device).
-inline int build_pic_tables(const SeqInfo& s, const EpipoleMap& epi, int cur_poc,
+// The per-call tables of n_pics pictures (cur_pocs[q]) predicted by one launch chain against the
+// context's resident references: the slots are shared, the GEODESIC_CAMPOSE rotation of (cur of
+// picture q, reference s) is ged[ged_cam[q][s]]; equal epipoles share one rotation entry.
+inline int build_pic_tables(const SeqInfo& s, const EpipoleMap& epi, const int* cur_pocs, int n_pics,
                             const std::vector<std::pair<int, RefDev>>& refs, mmdev::PicTables* t,
                             std::string* err) {
   if ((int)refs.size() > mmdev::MAX_SLOTS) {
     *err = "more than " + std::to_string(mmdev::MAX_SLOTS) + " resident reference pictures";
     return MM_ERR_ARG;
   }
+  if (n_pics < 1 || n_pics > mmdev::MAX_PICS) {
+    *err = "1.." + std::to_string(mmdev::MAX_PICS) + " pictures per call";
+    return MM_ERR_ARG;
+  }
   *t = mmdev::PicTables{};
   t->n_slots = (int)refs.size();
+  t->n_pics = n_pics;
   t->W = s.W;
   t->H = s.H;
   t->chroma = s.chroma ? 1 : 0;
@@ -219,18 +227,37 @@ inline int build_pic_tables(const SeqInfo& s, const EpipoleMap& epi, int cur_poc
   t->only_list = -1;
   const V3 fixed[3] = {{1.0f, 0.0f, 0.0f}, {0.0f, 1.0f, 0.0f}, {0.0f, 0.0f, 1.0f}};
   for (int i = 0; i < 3; i++) t->ged[i] = ged_rotation(fixed[i]);
+  for (int q = 0; q < mmdev::MAX_PICS; q++)
+    for (int k = 0; k < mmdev::MAX_SLOTS; k++) t->ged_cam[q][k] = -1;
+  std::vector<std::array<int32_t, 3>> used;  // epipoles of ged[3 ..]
   for (int k = 0; k < t->n_slots; k++) {
     t->poc[k] = refs[k].first;
     t->ref[k] = refs[k].second;
-    std::array<int32_t, 3> q;
-    t->ged_cam[k] = -1;
-    if (find_epipole(epi, cur_poc, refs[k].first, &q)) {
-      V3 e = {fixed_to_float(q[0], 24), fixed_to_float(q[1], 24), fixed_to_float(q[2], 24)};
-      t->ged[3 + k] = ged_rotation(e);
-      t->ged_cam[k] = 3 + k;
+    for (int q = 0; q < n_pics; q++) {
+      std::array<int32_t, 3> e;
+      if (!find_epipole(epi, cur_pocs[q], refs[k].first, &e)) continue;
+      int idx = -1;
+      for (size_t u = 0; u < used.size(); u++)
+        if (used[u] == e) idx = 3 + (int)u;
+      if (idx < 0) {
+        if ((int)used.size() == mmdev::MAX_SLOTS) {
+          *err = "more than " + std::to_string(mmdev::MAX_SLOTS) + " distinct camera-pose epipoles in one call";
+          return MM_ERR_ARG;
+        }
+        used.push_back(e);
+        idx = 3 + (int)used.size() - 1;
+        V3 v = {fixed_to_float(e[0], 24), fixed_to_float(e[1], 24), fixed_to_float(e[2], 24)};
+        t->ged[idx] = ged_rotation(v);
+      }
+      t->ged_cam[q][k] = (int8_t)idx;
     }
   }
   return MM_OK;
+}
+inline int build_pic_tables(const SeqInfo& s, const EpipoleMap& epi, int cur_poc,
+                            const std::vector<std::pair<int, RefDev>>& refs, mmdev::PicTables* t,
+                            std::string* err) {
+  return build_pic_tables(s, epi, &cur_poc, 1, refs, t, err);
 }
 
 // ---- encoder candidate windows (mm_sad_window) ---------------------------------------------
@@ -273,11 +300,11 @@ inline int plan_me_window(const SeqInfo& s, const mmdev::PicTables& t, const mm_
     }
     int ged = -1;
     if (b.model == GEODESIC_CAMPOSE) {
-      if (t.ged_cam[slot] < 0) {
+      if (t.ged_cam[0][slot] < 0) {
         *err = "ME block " + std::to_string(i) + ": no epipole for (curPOC, refPOC)";
         return MM_ERR_NOEPIPOLE;
       }
-      ged = t.ged_cam[slot];
+      ged = t.ged_cam[0][slot];
     } else if (b.model >= GEODESIC_X && b.model <= GEODESIC_Z) {
       ged = b.model - GEODESIC_X;
     }

@@ -58,7 +58,7 @@ EXPORTED_SYMBOLS = (
     "mm_set_stripes", "mm_set_plan_ahead", "mm_pred_list", "mm_derive_effective_blocks", "mm_epipole_list_create",
     "mm_epipole_list_destroy", "mm_get_epipole_list", "mm_epipole_add", "mm_epipole_make_available", "mm_epipole_has",
     "mm_epipole_find", "mm_epipole_derive_predictor", "mm_epipole_count", "mm_mvp_convert_device", "mm_mvp_status", "mm_set_dmvr",
-    "mm_set_mvp_stream", "mm_mvp_convert_host",
+    "mm_set_mvp_stream", "mm_mvp_convert_host", "mm_pred_device_multi",
 )
 
 BCW_DEFAULT = 2  # CommonDef.h:348-349; g_BcwWeights = {-2, 3, 4, 5, 10} (Rom.cpp:203)
@@ -103,6 +103,16 @@ assert PU_MOTION_DTYPE.itemsize == 80
 PU_MERGE, PU_SUBPU, PU_CIIP, PU_SMVD, PU_MMVD, PU_MVREFINE = 0x1, 0x2, 0x4, 0x8, 0x10, 0x20
 PU_WEIGHTED, PU_LONGTERM, PU_REF_SCALED, PU_MMVD_ENC2 = 0x40, 0x80, 0x100, 0x200
 PUF_DMVR = 0x1  # mm_pu_desc.flags: MM_PUF_DMVR
+
+
+MAX_PICS = 4  # MM_MAX_PICS: pictures per mm_pred_device_multi call
+
+
+class PicJob(ctypes.Structure):
+    """mm_pic_job: one picture of mm_pred_device_multi (device PU list and destination planes)."""
+    _fields_ = [("cur_poc", c_int32), ("d_pus", c_void_p), ("n", c_int32), ("dst_y", c_void_p),
+                ("dst_stride_y", ctypes.c_ssize_t), ("dst_cb", c_void_p), ("dst_cr", c_void_p),
+                ("dst_stride_c", ctypes.c_ssize_t)]
 
 
 class ToolFlags(ctypes.Structure):
@@ -192,6 +202,7 @@ def load_library() -> ctypes.CDLL:
         "mm_epipole_derive_predictor": (c_int, [vp, c_int, POINTER(c_int32)]),
         "mm_epipole_count": (c_int, [vp]),
         "mm_mvp_convert_host": (c_int, [POINTER(SeqParams), vp, vp, c_int, vp, POINTER(c_int)]),
+        "mm_pred_device_multi": (c_int, [vp, vp, c_int]),
     }
     default_lib = os.path.abspath(LIB_PATH) == os.path.join(os.path.dirname(_HERE), "lib", "libmm360.so")
     for name, (res, args) in sig.items():
@@ -476,6 +487,28 @@ class MMContext:
                                             c_void_p(_ptr(dst_cb)) if dst_cb is not None else None,
                                             c_void_p(_ptr(dst_cr)) if dst_cr is not None else None,
                                             dst_cb.stride(0) if dst_cb is not None else 0))
+
+    def predict_device_multi(self, pictures):
+        """mm_pred_device_multi: independent pictures in one launch chain.  pictures = [(cur_poc,
+        d_pus, dst_y, dst_cb, dst_cr)] (CUDA tensors / raw device addresses with strides given as
+        (ptr, stride) pairs are not accepted here: tensors only), at most MAX_PICS."""
+        assert 1 <= len(pictures) <= MAX_PICS
+        jobs = (PicJob * len(pictures))()
+        for q, (cur, d_pus, dy, dcb, dcr) in enumerate(pictures):
+            jobs[q] = PicJob(cur, _ptr(d_pus), d_pus.numel() * d_pus.element_size() // PU_DTYPE.itemsize,
+                             _ptr(dy), dy.stride(0), _ptr(dcb) if dcb is not None else None,
+                             _ptr(dcr) if dcr is not None else None, dcb.stride(0) if dcb is not None else 0)
+        self._check(self.lib.mm_pred_device_multi(self.h, jobs, len(pictures)))
+
+    def predict_device_multi_raw(self, pictures):
+        """mm_pred_device_multi into raw device addresses: pictures = [(cur_poc, d_pus, ptr_y, stride_y,
+        ptr_cb, ptr_cr, stride_c)]."""
+        assert 1 <= len(pictures) <= MAX_PICS
+        jobs = (PicJob * len(pictures))()
+        for q, (cur, d_pus, py, sy, pcb, pcr, sc) in enumerate(pictures):
+            jobs[q] = PicJob(cur, _ptr(d_pus), d_pus.numel() * d_pus.element_size() // PU_DTYPE.itemsize,
+                             py, sy, pcb, pcr, sc)
+        self._check(self.lib.mm_pred_device_multi(self.h, jobs, len(pictures)))
 
     def status(self):
         """Deferred validation result of the last device-planned call: (code, first_bad_pu)."""
