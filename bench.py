@@ -482,6 +482,8 @@ def bench_c4(args, cfg, params, rank, world, local, dist):
         ctx.run_raw(*ptrs[s % 2])
 
     def gather(b):
+        if world == 1:
+            return None  # the whole picture is already here
         if args.dist_backend == "nccl":
             return P.allgather_packed(bufs[b], lay, async_op=True)
         host = bufs[b].cpu()  # gloo rehearsal: host staging, synchronous
@@ -499,6 +501,26 @@ def bench_c4(args, cfg, params, rank, world, local, dist):
         return G.DependencyLoop(gop_name, n_bufs, lambda k, poc, rr, b: ctx.run_raw(*ptrs[b]), gather,
                                 lambda h: h.wait(), start=start, ref_waits=ref_waits, gather_all=gather_all)
 
+    d_mine = mm360.pus_to_device(mine)
+
+    def batched_loop(gop_name, max_pics=2):
+        """The RA loop with the independent pictures that follow each other in decode order (the
+        highest-layer leaves: 1 3, 5 7, ...) predicted together by mm_pred_device_multi: one launch
+        chain per batch; dependencies and all-gathers as in loop_for.  Returns the time of `steps`
+        pictures after `warmup` pictures."""
+        lp = loop_for(gop_name)
+        start = lp.k
+
+        def pb(items):
+            ctx.predict_device_multi_raw([(cur, d_mine, *ptrs[b]) for _, _, _, b in items])
+
+        def run_until(target):
+            while lp.k < target:
+                lp.step_batch(min(max_pics, target - lp.k), pb)
+
+        run_until(start + args.warmup)
+        return timed(1, 0, lambda s: run_until(start + args.warmup + args.steps), dist)
+
     t_mc = timed(args.steps, args.warmup, mc_only, dist)
     results = {}
     for name, gop_name, ref_waits, gather_all in (("ra32", "ra32", True, False), ("ra32_all", "ra32", True, True),
@@ -508,6 +530,7 @@ def bench_c4(args, cfg, params, rank, world, local, dist):
             continue
         lp = loop_for(gop_name, ref_waits, gather_all)
         results[name] = timed(args.steps, args.warmup, lambda s: lp.step(), dist)
+    results["ra32_batched"] = batched_loop("ra32")
     t_e2e = results["ra32"]
     # one more picture into buffer 0, all-gathered, for the bit-exact check below
     mc_only(0)
@@ -552,6 +575,9 @@ def bench_c4(args, cfg, params, rank, world, local, dist):
                        "gop": "ra32", "timed_pictures": "decode-order pictures 0..steps-1 of a GOP",
                        "plan_ahead": bool(args.plan_ahead), "parallelism": f"ctu-row stripes x{world}"},
             "ra_gop8": dict(per(results["ra8"]), note="same loop, dyadic hierarchical-B GOP-8 decode order"),
+            "ra32_batched": dict(per(results["ra32_batched"]),
+                                 note="same loop, consecutive independent pictures (the highest-layer leaves 1 3, "
+                                      "5 7, ...) predicted together in one launch chain (mm_pred_device_multi)"),
             "ra32_gather_every_picture": dict(per(results["ra32_all"]),
                                               note="same loop, unreferenced pictures all-gathered too"),
             "independent": dict(per(results["independent"]),
@@ -642,6 +668,27 @@ def bench_c4_emulate(args, cfg, params):
             for c in ctxs:
                 c.synchronize()
                 c.close()
+    # The same with ONE context and ONE launch chain per k stripes (mm_pred_device_multi: the stripes
+    # of k independent pictures planned, reprojected and interpolated together, plan-ahead on)
+    multi = {}
+    cm = new_ctx(params, 0, [(cur, pus, refs)])
+    cm.set_plan_ahead(bool(args.plan_ahead))
+    for n in (4, 8):
+        mine = P.shard_pus(pus, cfg.height, n, 0)
+        d_mine = mm360.pus_to_device(mine)
+        multi[n] = {}
+        for k in (1, 2, 3, 4):
+            outs = [planes(cfg) for _ in range(k)]
+            jobs = [(cur, d_mine, *o) for o in outs]
+            torch.cuda.synchronize()
+            t = timed(args.steps, args.warmup, lambda st: cm.predict_device_multi(jobs), None)
+            cm.synchronize()
+            multi[n][k] = round(t / args.steps / k * 1e3, 4)
+    cm.close()
+    out["multi_picture_stripes"] = {
+        "ms_per_stripe": multi,
+        "note": "rank 0's stripe of k independent pictures predicted by ONE context in ONE launch chain per "
+                "step (mm_pred_device_multi, plan-ahead as set): ms per stripe = elapsed / (steps x k)"}
     out["concurrent_stripes"] = {
         "ms_per_stripe": conc,
         "note": "rank 0's stripe predicted by k contexts at once (own streams and resident references, "

@@ -130,7 +130,7 @@ def _chain_pus(k, poc, refs):
     return pus
 
 
-def _chain_worker(rank, world, port, n_pictures, out_dir):
+def _chain_worker(rank, world, port, n_pictures, out_dir, batch=1):
     """One rank of the C4 decode-order loop (mm360.gop.DependencyLoop) on CPU: every picture is
     predicted FROM the gathered pictures it references, so a missing or early reference wait
     would show up as a wrong picture."""
@@ -156,16 +156,35 @@ def _chain_worker(rank, world, port, n_pictures, out_dir):
         decoded[poc] = planes  # this rank's stripe only, until (and unless) the picture is all-gathered
         cur["poc"] = poc
 
+    buf_poc = {}
+
+    def predict_batch(items):
+        """the batch's pictures (independent) in one mm_pred_device_multi-style call (CPU twin)"""
+        pics = [(poc, P.shard_pus(_chain_pus(k, poc, refs), cfg.height, world, rank)) for k, poc, refs, _ in items]
+        rr = {r: decoded[r] for _, _, refs, _ in items for r in refs}
+        outs = twin.predict_multi(params, pics, rr, cfg.width, cfg.height, epi)
+        for (k, poc, refs, b), planes in zip(items, outs):
+            lay.pack(planes, rank, bufs[b])
+            decoded[poc] = planes
+            buf_poc[b] = poc
+
     def gather(b):
+        poc = buf_poc.get(b, cur.get("poc")) if batch > 1 else cur["poc"]
         t = torch.from_numpy(bufs[b])
         P.allgather_packed(t, lay)
-        decoded[cur["poc"]] = lay.unpack(t.numpy())
-        return ("gathered", cur["poc"])
+        decoded[poc] = lay.unpack(t.numpy())
+        return ("gathered", poc)
 
     waits = []
     loop = G.DependencyLoop("ra8", 2, predict, gather, waits.append)
-    for _ in range(n_pictures):
-        loop.step()
+    if batch > 1:
+        while loop.k < n_pictures:
+            loop.step_batch(min(batch, n_pictures - loop.k), predict_batch)
+    else:
+        for _ in range(n_pictures):
+            loop.step()
+    with open(os.path.join(out_dir, f"batches{rank}.txt"), "w") as f:
+        f.write(str(loop.k))
     out = {f"poc{poc}_{c}": decoded[poc][i] for poc, _, _ in seq for i, c in enumerate(("y", "cb", "cr"))}
     np.savez(os.path.join(out_dir, f"chain{rank}.npz"), **out)
     with open(os.path.join(out_dir, f"trace{rank}.txt"), "w") as f:
@@ -208,14 +227,23 @@ def test_schedule_model():
         assert slow_all["ms_per_picture"] >= 1.0 and 0.5 <= slow_ref["ms_per_picture"] <= 0.61
 
 
-def test_gloo_decode_order_chain(tmp_path):
+@pytest.mark.parametrize("batch", [1, 2])
+def test_gloo_decode_order_chain(tmp_path, batch):
     """C4 decode-order loop, world 2: each picture of an RA GOP-8 sequence is predicted from its
     gathered references; only referenced pictures are all-gathered (every rank then holds exactly
     the unsharded picture), unreferenced ones stay sharded (each rank holds its stripe of it), and
-    each picture waited for the all-gathers of all its references decoded in the sequence."""
+    each picture waited for the all-gathers of all its references decoded in the sequence.
+    batch 2: independent consecutive pictures (the leaves 1 and 3) are predicted together in one
+    multi-picture call (DependencyLoop.step_batch, mm_pred_device_multi's CPU twin)."""
     n = 6
     port = _free_port()
-    mp.spawn(_chain_worker, args=(2, port, n, str(tmp_path)), nprocs=2, join=True)
+    mp.spawn(_chain_worker, args=(2, port, n, str(tmp_path), batch), nprocs=2, join=True)
+    if batch > 1:
+        seq_b = G.decode_sequence(n, "ra8")
+        loop = G.DependencyLoop("ra8", 2, None, None, None)
+        loop.k = 3
+        assert [p for p, _, _ in loop.next_batch(2)] == [1, 3]  # the leaves after 8 4 2 go together
+        assert [p for p, _, _ in seq_b][3:5] == [1, 3]
     import twin
     cfg = GOP_CFG
     params = mm360.seq_params(cfg.width, cfg.height, cfg.models)

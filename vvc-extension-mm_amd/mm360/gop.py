@@ -163,3 +163,52 @@ class DependencyLoop:
         self.trace.append((poc, waited))
         self.k += 1
         return poc
+
+    def next_batch(self, max_pics: int) -> List[Tuple[int, int, List[int]]]:
+        """The pictures from decode position k on that can be predicted together (at most max_pics):
+        none of them references another picture of the batch.  In RA order these are the runs of
+        highest-temporal-layer leaves (GOP-32: 1 3, 5 7, 9 11, ...), which nothing references."""
+        batch: List[Tuple[int, int, List[int]]] = []
+        k = self.k
+        while len(batch) < max_pics:
+            (poc, tid, refs), = decode_sequence(1, self.gop, k)
+            if any(r == p for r in refs for p, _, _ in batch):
+                break
+            batch.append((poc, tid, refs))
+            k += 1
+        return batch
+
+    def step_batch(self, max_pics: int, predict_batch) -> List[int]:
+        """step() for a batch of independent pictures (next_batch): the reference all-gathers of
+        every picture of the batch are waited for, then predict_batch([(k, poc, refs, buf), ...])
+        predicts them together (one launch chain), then each referenced one is all-gathered."""
+        batch = self.next_batch(max_pics)
+        assert len(batch) <= self.n_bufs
+        items = []
+        seen = set()
+        for i, (poc, _, refs) in enumerate(batch):
+            waited = []
+            for r in refs if self.ref_waits else ():
+                h = self.handles.get(r)
+                if h is not None:
+                    if r not in seen:
+                        self.wait(h)
+                        seen.add(r)
+                    waited.append(r)
+            b = (self.k + i) % self.n_bufs
+            if self.buf_handle[b] is not None:
+                self.wait(self.buf_handle[b])
+            items.append((self.k + i, poc, refs, b))
+            self.trace.append((poc, waited))
+        predict_batch(items)
+        for k, poc, _, b in items:
+            h = None
+            if self.gather_all or is_referenced(poc, self.gop):
+                h = self.gather(b)
+                self.gathered.append(poc)
+                self.handles[poc] = h
+            self.buf_handle[b] = h
+        for old in [p for p in self.handles if p < items[-1][1] - 2 * len(GOPS[self.gop])]:
+            del self.handles[old]
+        self.k += len(items)
+        return [poc for _, poc, _, _ in items]
