@@ -403,10 +403,11 @@ int mm_set_stripes(mm_ctx* ctx, int stripes);
  * setup / reprojection / interpolation with the rest of the picture.  Forces one stripe.  With it
  * off, a flagged PU is rejected (MM_ERR_ARG).
  * Device memory: the DMVR work buffers are sized for the largest list the picture can hold, since
- * a device-resident list's DMVR share is unknown to the host -- per context, 56 * 50 bytes per
- * possible sub-PU (W*H/128 of them: the per-offset block setups) plus 16 * 25 bytes per luma 4x4
- * sub-block (the reprojected positions of both lists): about 0.9 GB at 6144x3072, allocated on the
- * first DMVR picture and kept until mm_destroy. */
+ * a device-resident list's DMVR share is unknown to the host -- per plan slot (two), about 310 bytes
+ * per possible sub-PU (W*H/128 of them: the sub-PU record, its centre setups and centre terms, cost,
+ * delta and survivor index): about 45 MB per slot, 90 MB per context at 6144x3072, allocated on the
+ * first DMVR picture and kept until mm_destroy.  The 24 other offsets' setups, positions and costs of
+ * a surviving sub-PU never leave the wave that searches it (round 4: 0.9 GB per context). */
 int mm_set_dmvr(mm_ctx* ctx, int on);
 
 /* Plan-ahead for mm_pred_device (default off): a picture's planning and setup kernels run on the

@@ -165,14 +165,10 @@ static int twin_pred_segs(const Twin& t, const mmdev::PicTables& tab, const mm_p
   const Taps taps{LUMA_T, CHROMA_T, nullptr, RefPool{}};
   MpaCache c = cache_of(t);
   if (m.n_sub) {
-    std::vector<BlockSetup> dset((size_t)m.n_sub * N_OFF * 2);
-#pragma omp parallel for schedule(static)
-    for (int j = 0; j < m.n_sub * N_OFF * 2; j++) dmvr_setup_thread(j, t.sc, subs.data(), tab.ged, dset.data());
     if (mvd) mvd->assign(2 * (size_t)m.n_sub, 0);
 #pragma omp parallel for schedule(dynamic, 4)
     for (int s = 0; s < m.n_sub; s++)
-      dmvr_search_host(s, t.sc, t.geo, taps, subs.data(), dset.data(), c, tab.ref, jobs.data(),
-                       mvd ? mvd->data() : nullptr);
+      dmvr_search_host(s, t.sc, t.geo, taps, subs.data(), tab.ged, c, tab.ref, jobs.data(), mvd ? mvd->data() : nullptr);
   }
   std::vector<BlockSetup> setups(m.n_jobs);
 #pragma omp parallel for schedule(static)

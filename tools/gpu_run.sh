@@ -18,6 +18,8 @@ run() {  # name limit cmd...
 for step in "$@"; do
   case $step in
     tests) run gpu_tests 900 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread ;;
+    tests_k=*)  # tests_k=<pytest -k expression>: a subset of the GPU suite
+      run gpu_tests_k 600 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread -k "${step#tests_k=}" ;;
     race_probe) run race_probe 900 env MM360_LIB=tmp_variants/probe/libmm360.so python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread ;;
     probe_ctl)  # positive control: the probe build with the s_ged barriers removed must FAIL (wrong pictures)
       run probe_ctl 300 bash -c 'MM360_LIB=tmp_variants/probe_ctl/libmm360.so python -u -m pytest tests/test_gpu.py -q -k "pred_full_frame_vs_oracle or pred_uniform_per_model" --timeout 120 --timeout-method thread; rc=$?; echo "pytest rc=$rc (1 = tests failed as expected)"; test $rc -eq 1' ;;
@@ -25,6 +27,11 @@ for step in "$@"; do
       rounds=$(echo "$step" | cut -d= -f2); vs=$(echo "$step" | cut -d= -f3 | tr ',' ' ')
       run "abb_$(echo "$vs" | tr ' ' '_')" 900 bash tools/ab_bench.sh "$rounds" $vs ;;
     example) run example 120 vvc-extension-mm_amd/lib/example_decode ;;
+    dmvrab=*)  # dmvrab=<v1,v2,...>: C3 with a 30 % MM-DMVR share, per library variant (default = in-tree)
+      for v in $(echo "$step" | cut -d= -f2 | tr ',' ' '); do
+        L=tmp_variants/$v/libmm360.so; [ "$v" = default ] && L=vvc-extension-mm_amd/lib/libmm360.so
+        run "dmvr_$v" 600 python bench.py --dmvr-share 0.3 --steps 12 --warmup 3 --no-cpu-baseline --no-mvp --no-c5 --lib "$L"
+      done ;;
     c5ab=*)  # c5ab=<v1,v2,...>: C5 (Mcandidates/s) of library variants (default = in-tree), one run each
       for v in $(echo "$step" | cut -d= -f2 | tr ',' ' '); do
         L=tmp_variants/$v/libmm360.so; [ "$v" = default ] && L=vvc-extension-mm_amd/lib/libmm360.so
@@ -54,6 +61,9 @@ for step in "$@"; do
     pmc=*)  # pmc=<tag>=<counter,counter,...>: one rocprofv3 --pmc pass over a short bench run
       tag=$(echo "$step" | cut -d= -f2); ctrs=$(echo "$step" | cut -d= -f3 | tr ',' ' ')
       run "pmc_$tag" 600 rocprofv3 --pmc $ctrs -d "gpurun_out/pmc_$tag" -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 --no-mvp --no-c5 --no-dmvr ;;
+    pmcd=*)  # pmcd=<tag>=<counter,...>: one rocprofv3 --pmc pass over a short C3 run with a 30 % MM-DMVR share
+      tag=$(echo "$step" | cut -d= -f2); ctrs=$(echo "$step" | cut -d= -f3 | tr ',' ' ')
+      run "pmcd_$tag" 600 rocprofv3 --pmc $ctrs -d "gpurun_out/pmcd_$tag" -o run --output-format csv -- python3 bench.py --dmvr-share 0.3 --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 --no-mvp --no-c5 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

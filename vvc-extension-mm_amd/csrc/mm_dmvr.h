@@ -12,10 +12,10 @@
 //      window border (xDMVRSubPixelErrorSurface :2157-2175, xSubPelErrorSrfc :1996-2048);
 //   4. the sub-PU is predicted as a bi PU at merge0 + mvd / merge1 - mvd (all components, addAvg).
 // Steps 1-3 run here inside the picture's device-planned launch sequence (mm_kernels.hip): the
-// per-offset block setups, the centre cost of every sub-PU (k_dmvr_centre_dev; a sub-PU whose
-// centre ends the search keeps its merge MVs), then for the surviving sub-PUs only -- compacted
-// into a list -- the 24 other offsets' positions and the search (k_dmvr_reproj_dev,
-// k_dmvr_search_dev): the planner (mm_devplan.h) places every sub-PU of an MM_PUF_DMVR PU as a bi PU
+// centre setups and the centre cost of every sub-PU (k_dmvr_setup_dev, k_dmvr_centre_dev; a sub-PU
+// whose centre ends the search keeps its merge MVs), then for the surviving sub-PUs only --
+// compacted into a list -- the 24 other offsets' setups, positions and the search, all inside one
+// workgroup per survivor (k_dmvr_search_dev): the planner (mm_devplan.h) places every sub-PU of an MM_PUF_DMVR PU as a bi PU
 // with its reprojection jobs and a SubPuDev record pointing at them, the search runs on the
 // records, and the search writes the refined MVs into those jobs before k_setup reads them --
 // step 4 is then the ordinary setup / reprojection / interpolation of the picture.
@@ -44,16 +44,36 @@ struct SubPuDev {
 MM_HD int off_x(int i) { return i % 5 - 2; }
 MM_HD int off_y(int i) { return i / 5 - 2; }
 
-// job = (sub-PU s, offset o, list l) -> setups[(s * N_OFF + o) * 2 + l]
-MM_HD void dmvr_setup_thread(int t, const SeqConst& sc, const SubPuDev* sp, const M3* ged, BlockSetup* out) {
-  const int l = t & 1, so = t >> 1, s = so / N_OFF, o = so - s * N_OFF;
-  const SubPuDev& u = sp[s];
+// The block setup of sub-PU u at offset o for list l: reprojectMotionVectorSubblocks of the sub-PU at
+// merge0 + offset (L0) / merge1 - offset (L1), InterPrediction.cpp:2510-2515, 2544-2549.
+MM_HD void dmvr_setup(const SeqConst& sc, const SubPuDev& u, int o, int l, const M3* ged, BlockSetup* out) {
   const int sgn = l ? -1 : 1;
   const int mvh = u.mv[l][0] + sgn * (off_x(o) << 4), mvv = u.mv[l][1] + sgn * (off_y(o) << 4);
-  block_setup(&out[t], sc, u.model, true, u.x, u.y, u.w, u.h, mvh, mvv, u.ged_idx[l] >= 0 ? &ged[u.ged_idx[l]] : nullptr);
+  block_setup(out, sc, u.model, true, u.x, u.y, u.w, u.h, mvh, mvv, u.ged_idx[l] >= 0 ? &ged[u.ged_idx[l]] : nullptr);
 }
-
-MM_HD int dmvr_setup_index(int s, int o, int l) { return (s * N_OFF + o) * 2 + l; }
+// The sub-PU's centre terms for list l (mm_models.h centre_terms): what its 25 offsets' setups share
+MM_HD void dmvr_centre_terms(const SeqConst& sc, const SubPuDev& u, int l, const M3* ged, CentreTerms* ct) {
+  const float cx = (float)u.x + ((float)u.w - 1.0f) / 2.0f, cy = (float)u.y + ((float)u.h - 1.0f) / 2.0f;
+  centre_terms(ct, sc, u.model, cx, cy, u.ged_idx[l] >= 0 ? &ged[u.ged_idx[l]] : nullptr);
+}
+// dmvr_setup from the sub-PU's centre terms: the MV part of the setup only (the same bits)
+MM_HD void dmvr_offset_setup(const SeqConst& sc, const SubPuDev& u, int o, int l, const CentreTerms& ct, const M3* ged,
+                             BlockSetup* out) {
+  const int sgn = l ? -1 : 1;
+  const int mvh = u.mv[l][0] + sgn * (off_x(o) << 4), mvv = u.mv[l][1] + sgn * (off_y(o) << 4);
+  setup_from_centre(out, sc, u.model, true, mv_to_float(mvh), mv_to_float(mvv), ct,
+                    u.ged_idx[l] >= 0 ? &ged[u.ged_idx[l]] : nullptr);
+}
+// k_dmvr_setup_dev thread t: the centre terms of (sub-PU t / 2, list t % 2) and its centre setup,
+// setups[t] (the other offsets' setups are derived from the terms by the search of the survivors)
+MM_HD void dmvr_centre_setup_thread(int t, const SeqConst& sc, const SubPuDev* sp, const M3* ged, BlockSetup* out,
+                                    CentreTerms* cterms) {
+  const SubPuDev& u = sp[t >> 1];
+  CentreTerms ct;
+  dmvr_centre_terms(sc, u, t & 1, ged, &ct);
+  cterms[t] = ct;
+  dmvr_offset_setup(sc, u, N_OFF / 2, t & 1, ct, ged, &out[t]);
+}
 
 // Luma 4x4 sub-block e (Eigen column-major index over the sub-PU) of one list at offset o: its
 // reprojected position (1/16 pel) -- L0 at merge0 + offset, L1 at merge1 - offset, from the
@@ -78,13 +98,13 @@ MM_HD void dmvr_position(const SeqConst& sc, const SubPuDev& u, const BlockSetup
 // the k-th non-centre offset.
 MM_HD int dmvr_outer_offset(int k) { return k < N_OFF / 2 ? k : k + 1; }
 
-// Luma 4x4 sub-block e of list l at n_offs offsets (offset index offs(j) for the j-th): its
+// Luma 4x4 sub-block e of list l at n_offs offsets (the j-th offset's setup: setup_of(j)): its
 // reprojected positions (1/16 pel), out(j, fx, fy).  The element's grid terms and the MV-independent head of its
 // model (motion_head: TAN's tangent-plane coordinates, GED's rotated spherical coordinates) are
 // computed once, the tail per offset: the same operations as dmvr_position per offset.
-template <class Offs, class Out>
-MM_HD void dmvr_positions_offsets(const SeqConst& sc, const SubPuDev& u, const BlockSetup* setups, int s, int l, int e,
-                                  const MpaCache& cache, Offs offs, int n_offs, Out out) {
+template <class Setup, class Out>
+MM_HD void dmvr_positions_offsets(const SeqConst& sc, const SubPuDev& u, int l, int e, const MpaCache& cache,
+                                  Setup setup_of, int n_offs, Out out) {
   const int col = e / u.rows, row = e - col * u.rows;
   const float gx = (float)(u.x + 4 * col) + sc.off, gy = (float)(u.y + 4 * row) + sc.off;
   const bool mpa = u.model >= MPA_FRONT_BACK && u.model <= MPA_TOP_BOTTOM;
@@ -99,7 +119,7 @@ MM_HD void dmvr_positions_offsets(const SeqConst& sc, const SubPuDev& u, const B
   MotionHead h{};
   bool have_head = false;
   for (int j = 0; j < n_offs; j++) {
-    const BlockSetup& b = setups[dmvr_setup_index(s, offs(j), l)];
+    const BlockSetup& b = setup_of(j);
     if (!have_head && !b.identity) {  // a zero-MV setup is the identity and carries no TAN terms
       h = motion_head(sc, b, gx, gy, m, pg);
       have_head = true;
@@ -110,26 +130,6 @@ MM_HD void dmvr_positions_offsets(const SeqConst& sc, const SubPuDev& u, const B
     reproject_finish(sc, gx, gy, mx, my, packet, 0, &fx, &fy);
     out(j, fx, fy);
   }
-}
-
-// Thread t of survivor k in k_dmvr_reproj_dev (6 n threads: t = 2 (part n + e) + l): the positions of
-// sub-block e of list l at the 8 non-centre offsets 8 part .. 8 part + 7, into the survivor's items
-// surv_base[k] + 2 (j n + e) + l.
-MM_HD void dmvr_reproj_thread(int k, int t, const int* surv_s, const int* surv_base, const SeqConst& sc,
-                              const SubPuDev* sp, const BlockSetup* setups, const MpaCache& cache, mm_int2* pos) {
-  const int s = surv_s[k];
-  const SubPuDev& u = sp[s];
-  const int l = t & 1, pe = t >> 1, part = pe / u.n, e = pe - part * u.n;
-  const int j0 = 8 * part;
-  mm_int2* dst = pos + surv_base[k] + 2 * e + l;
-  const int stride = 2 * u.n;
-  dmvr_positions_offsets(sc, u, setups, s, l, e, cache, [&](int j) { return dmvr_outer_offset(j0 + j); }, 8,
-                         [&](int j, int32_t fx, int32_t fy) {
-                           mm_int2 q;
-                           q.x = fx;
-                           q.y = fy;
-                           dst[(long)(j0 + j) * stride] = q;
-                         });
 }
 
 // xDMVRCost's share of one 4x4 sub-block: SAD of its rows 0 and 2 (the sub-PU's even rows, RdCost
@@ -237,9 +237,11 @@ MM_HD void dmvr_apply(int s, const SubPuDev& u, int tdx, int tdy, JobDev* jobs, 
 // offsets, the decision -- the same per-element bodies the device search kernel runs in parallel
 // (mm_kernels.hip k_dmvr_search_dev), with the host's clamped-address filter.
 inline void dmvr_search_host(int s, const SeqConst& sc, const Geometry& geo, const Taps& taps, const SubPuDev* sp,
-                             const BlockSetup* setups, const MpaCache& cache, const RefDev* refs, JobDev* jobs,
-                             int32_t* mvd) {
+                             const M3* ged, const MpaCache& cache, const RefDev* refs, JobDev* jobs, int32_t* mvd) {
   const SubPuDev& u = sp[s];
+  BlockSetup setups[N_OFF][2];
+  for (int o = 0; o < N_OFF; o++)
+    for (int l = 0; l < 2; l++) dmvr_setup(sc, u, o, l, ged, &setups[o][l]);
   uint32_t cost[N_OFF];
   for (int i = 0; i < N_OFF; i++) cost[i] = 0;
   // every offset's positions, as the device computes them (centre: dmvr_position; the 24 others:
@@ -247,9 +249,9 @@ inline void dmvr_search_host(int s, const SeqConst& sc, const Geometry& geo, con
   int32_t pos[N_OFF][16][2][2];
   for (int e = 0; e < u.n; e++)
     for (int l = 0; l < 2; l++) {
-      dmvr_position(sc, u, setups[dmvr_setup_index(s, N_OFF / 2, l)], cache, e, &pos[N_OFF / 2][e][l][0],
-                    &pos[N_OFF / 2][e][l][1]);
-      dmvr_positions_offsets(sc, u, setups, s, l, e, cache, dmvr_outer_offset, N_OFF - 1,
+      dmvr_position(sc, u, setups[N_OFF / 2][l], cache, e, &pos[N_OFF / 2][e][l][0], &pos[N_OFF / 2][e][l][1]);
+      dmvr_positions_offsets(sc, u, l, e, cache, [&](int j) -> const BlockSetup& { return setups[dmvr_outer_offset(j)][l]; },
+                             N_OFF - 1,
                              [&](int j, int32_t fx, int32_t fy) {
                                pos[dmvr_outer_offset(j)][e][l][0] = fx;
                                pos[dmvr_outer_offset(j)][e][l][1] = fy;

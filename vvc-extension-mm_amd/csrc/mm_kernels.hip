@@ -458,7 +458,10 @@ constexpr int MC_BLOCKS_PER_WG = 1;
 // pictures on the context stream (profiles/r03_ab_kernel_events.txt).
 constexpr bool KERNEL_EVENTS = true;
 constexpr bool GATE_NO_FENCE = true;
-constexpr bool PLAN_AHEAD_HOST_WAIT = true;  // see launch_stripe
+#ifndef MM_PLAN_HOST_WAIT
+#define MM_PLAN_HOST_WAIT 0  // see launch_stripe
+#endif
+constexpr bool PLAN_AHEAD_HOST_WAIT = MM_PLAN_HOST_WAIT;
 #ifndef MM_REPROJ_AHEAD
 #define MM_REPROJ_AHEAD 1  // see launch_stripe
 #endif
@@ -548,27 +551,28 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MM_ME_
 using namespace mmdmvr;
 constexpr int DMVR_GRID = 2048;  // workgroups of 256 of the grid-stride setup kernel
 
-// The picture's DMVR survivors (sub-PUs whose centre cost does not end the search) and their items
+// The picture's DMVR survivors (sub-PUs whose centre cost does not end the search)
 struct DmvrWork {
-  unsigned long long* count;  // (survivors << 32) | position items (k_dmvr_centre_dev)
+  unsigned long long* count;  // survivors << 32 (k_dmvr_centre_dev)
   uint32_t* ccost;            // centre cost (xDMVRCost at the merge MVs) per sub-PU
   int* surv_s;                // sub-PU of survivor k
-  int* surv_base;             // first position item of survivor k
-  int* surv_tbase;            // first k_dmvr_reproj_dev thread of survivor k (surv_base / 8)
-  int* surv_tchunk;           // survivor holding reprojection thread 64 c (wave_find_item hints)
+  const CentreTerms* cterms;  // centre terms [2 s + l] (k_dmvr_setup_dev)
 };
 
-// thread per (sub-PU, offset, list) setup; also clears the survivor count for k_dmvr_centre_dev
+// thread per (sub-PU, list): the centre terms and the centre setup (the other 24 offsets' setups are
+// derived from the terms by the search, for the survivors only); also clears the survivor count for
+// k_dmvr_centre_dev
 __global__ void __launch_bounds__(256) k_dmvr_setup_dev(SeqConst sc, const PlanMeta* __restrict__ meta,
                                                         const SubPuDev* __restrict__ sp, const PicTables t,
-                                                        BlockSetup* __restrict__ out, unsigned long long* __restrict__ count) {
+                                                        BlockSetup* __restrict__ out, CentreTerms* __restrict__ cterms,
+                                                        unsigned long long* __restrict__ count) {
   __shared__ M3 s_ged[3 + MAX_SLOTS];  // indexed per lane: staged by stage_arg_words
   stage_arg_words<sizeof(s_ged) / 4>(reinterpret_cast<const uint32_t*>(t.ged), reinterpret_cast<uint32_t*>(s_ged));
   __syncthreads();
   if (blockIdx.x == 0 && threadIdx.x == 0) *count = 0ull;
-  const int n_jobs = meta->n_sub * N_OFF * 2;
+  const int n_jobs = meta->n_sub * 2;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n_jobs; i += gridDim.x * blockDim.x)
-    dmvr_setup_thread(i, sc, sp, s_ged, out);
+    dmvr_centre_setup_thread(i, sc, sp, s_ged, out, cterms);
 }
 
 // The centre cost of every sub-PU (InterPrediction.cpp:2510-2525): 32 lanes per sub-PU, lane
@@ -603,7 +607,7 @@ __global__ void __launch_bounds__(256) k_dmvr_centre_dev(SeqConst sc, Geometry g
     if (s < n_sub) u = sp[s];
     if (s < n_sub && e < u.n) {
       int32_t fx, fy;
-      dmvr_position(sc, u, setups[dmvr_setup_index(s, N_OFF / 2, l)], cache, e, &fx, &fy);
+      dmvr_position(sc, u, setups[2 * s + l], cache, e, &fx, &fy);
       const int xPos = fx >> 4, yPos = fy >> 4;
       if (!sb_out_of_range(xPos, yPos, geo.W, geo.H, geo.maxCUw, geo.maxCUh, 4, 4)) {
         const RefDev& r = s_ref[l ? u.slot[1] : u.slot[0]];
@@ -650,99 +654,119 @@ __global__ void __launch_bounds__(256) k_dmvr_centre_dev(SeqConst sc, Geometry g
       lds_put(s_base[1], (int)(old & 0xffffffffull), 0);
     }
     __syncthreads();
-    if (items) {
-      const int k = s_base[0] + (s_pre[slot] >> 20), ib = s_base[1] + (s_pre[slot] & 0xfffff);
-      w.surv_s[k] = s;
-      w.surv_base[k] = ib;
-      w.surv_tbase[k] = ib / 8;
-      write_chunks(w.surv_tchunk, k, ib / 8, items / 8);
-    }
+    if (items) w.surv_s[s_base[0] + (s_pre[slot] >> 20)] = s;
     __syncthreads();  // s_items / s_pre / s_base reused by the next iteration
   }
 #endif
 }
 
-// thread per (survivor, part, luma 4x4 sub-block, list), 6 n per survivor (mm_dmvr.h
-// dmvr_reproj_thread): the positions of 8 of the 24 non-centre offsets -- the element's grid terms
-// and its model's MV-independent head once, the tail per offset -- 8 bytes each into the survivor's
-// items.
-__global__ void __launch_bounds__(256) k_dmvr_reproj_dev(SeqConst sc, const SubPuDev* __restrict__ sp,
-                                                         const BlockSetup* __restrict__ setups, MpaCache cache,
-                                                         DmvrWork w, mm_int2* __restrict__ pos) {
-  const unsigned long long cnt = *w.count;
-  const int n_surv = (int)(cnt >> 32), n_threads = (int)(cnt & 0xffffffffull) / 8;
-  const int lane = __lane_id();
-  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, n_waves = (gridDim.x * blockDim.x) >> 6;
-  for (int g0 = wave * 64; g0 < n_threads; g0 += n_waves * 64) {
-    const int g = g0 + lane;
-    const int k = wave_find_item(w.surv_tbase, w.surv_tchunk, g, n_surv);
-    if (g < n_threads) dmvr_reproj_thread(k, g - w.surv_tbase[k], w.surv_s, w.surv_base, sc, sp, setups, cache, pos);
-  }
+// The search of one surviving sub-PU per wave (xProcessDMVRProjected, InterPrediction.cpp:2526-2580).
+// Each wave of a workgroup takes its own survivors and its own LDS region; the workgroup shares only
+// the tap tables and the GED rotations.  Lane L = part * 2n + 2 e + l serves luma 4x4 sub-block e of
+// list l at the part's 24 / P offsets (P = 64 / 2n parts: 2 for a 16x16 sub-PU, 4 for 16x8 / 8x16):
+//   0. the 24 non-centre offsets' setups of both lists (lanes 0..47) into the wave's LDS -- only the
+//      MV part, from the centre terms k_dmvr_setup_dev stored (mm_models.h setup_from_centre);
+//   1. the lane's positions at its offsets, kept in registers -- the model's MV-independent head once,
+//      the tail per offset (mm_dmvr.h dmvr_positions_offsets) -- and per list the bounding box of the
+//      in-range windows (wave shuffles);
+//   2. the union of every offset's luma window, per list, staged once into the wave's LDS (16-byte
+//      loads): the 24 x n windows of a list lie within about (dx + 11) x (dy + 11) samples, so each
+//      staged sample serves ~50 window reads; a union larger than the LDS window (strong warping, the
+//      ERP seam) reads the pool directly instead;
+//   3. per offset, rows 0 and 2 of the lane's 14-bit prediction; the L0 lane takes its partner's L1
+//      rows by shuffle for the SAD, summed over the part's n sub-blocks (xor shuffles);
+//   4. the decision (the centre cost from k_dmvr_centre_dev, first strict minimum, error surface) and
+//      the refined MVs into the sub-PU's jobs (lane 0).
+// The phases of one survivor are ordered by wave-level fences only, so a wave waiting on its window
+// loads never holds the others of its workgroup.  C3 at a 30 % share (profiles/r05_ab_dmvr.txt):
+// 0.674-0.685 ms per picture, against 0.689-0.695 for round 4's split (positions written to HBM by a
+// separate reprojection kernel and read back; 0.9 GB of work buffers per context); 0.715-0.730 at 3
+// waves with the setups computed in full here (162 VGPRs, 44 K instructions); 0.77-0.82 for a first
+// form with one survivor per 256-thread workgroup and five workgroup barriers per survivor.
+constexpr int DMVR_WAVES = 4;                  // waves (survivors in flight) per workgroup
+constexpr int DMVR_SEARCH_WG = 64 * DMVR_WAVES;
+constexpr int DMVR_LANE_OFFS = 12;             // offsets per lane of a 16x16 sub-PU (24 / 2 parts)
+#ifndef MM_DMVR_WIN_W
+#define MM_DMVR_WIN_W 40  // a 16x16 sub-PU's 24 offsets span ~(16 + 4 + 11)^2 samples; larger unions read the pool
+#define MM_DMVR_WIN_H 32
+#endif
+constexpr int DMVR_WIN_W = MM_DMVR_WIN_W;  // staged union window per list: samples x rows
+constexpr int DMVR_WIN_H = MM_DMVR_WIN_H;
+constexpr int DMVR_WIN_STRIDE = DMVR_WIN_W / 2 + 1;  // dwords per LDS row: odd, so rows start on different banks
+struct DmvrWaveLds {
+  uint32_t win[2][DMVR_WIN_H * DMVR_WIN_STRIDE];
+  BlockSetup set[N_OFF - 1][2];  // the survivor's 24 non-centre offsets x 2 lists
+  uint32_t cost[N_OFF];
+};
+static_assert(2 * (N_OFF - 1) <= 64, "one lane per (offset, list) setup");
+static_assert((N_OFF - 1) % 4 == 0 && (N_OFF - 1) / 2 == DMVR_LANE_OFFS, "24 offsets split over 2 or 4 parts");
+
+// Orders one wave's LDS accesses (its lanes run in lockstep; LDS serves a wave's accesses in order)
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// The search of one surviving sub-PU per workgroup iteration (xProcessDMVRProjected,
-// InterPrediction.cpp:2526-2580), from the positions k_dmvr_reproj_dev wrote:
-//   1. the 24 non-centre offsets x n luma 4x4 sub-blocks x 2 lists positions into LDS (one 8-byte
-//      load per item), and per list the bounding box of the in-range windows;
-//   2. the union of every offset's luma window, per list, staged once into LDS (16-byte loads): the
-//      24 x n windows of a list lie within about (dx + 11) x (dy + 11) samples, so each staged
-//      sample serves ~50 window reads that would otherwise each be a global load; a union larger
-//      than the LDS window (strong warping, the ERP seam) reads the pool directly instead;
-//   3. rows 0 and 2 of both 14-bit predictions per (offset, sub-block) and their SAD, summed per
-//      offset over its n sub-blocks (xor shuffles inside the n-lane segment);
-//   4. the decision (the centre cost from k_dmvr_centre_dev, first strict minimum, error surface)
-//      and the refined MVs into the sub-PU's jobs.
-// Costs never leave the workgroup.
-constexpr int DMVR_SEARCH_WG = 256;
-constexpr int DMVR_SEARCH_GRID = 2048;  // 8 workgroups per CU, grid-stride over the survivors
-[[maybe_unused]] constexpr int DMVR_MAX_ITEMS = (N_OFF - 1) * 16 * 2;  // position items of a 16x16 sub-PU
-constexpr int DMVR_WIN_W = 64;                   // staged union window per list: samples x rows
-[[maybe_unused]] constexpr int DMVR_WIN_H = 48;
-[[maybe_unused]] constexpr int DMVR_WIN_STRIDE = DMVR_WIN_W / 2 + 1;  // dwords per LDS row: odd, so rows start on different banks
-
-// amdgpu_waves_per_eu(5): 96 instead of 101 VGPRs, 5 waves per SIMD: 195 vs 202 us (profiles/r04_ab_occupancy.txt)
-__global__ void __launch_bounds__(DMVR_SEARCH_WG) __attribute__((amdgpu_waves_per_eu(5))) k_dmvr_search_dev(Geometry geo, const SubPuDev* __restrict__ sp,
-                                                                   const mm_int2* __restrict__ pos, const PicTables t,
-                                                                   DmvrWork w, JobDev* __restrict__ jobs,
-                                                                   int32_t* __restrict__ mvd) {
+#ifndef MM_DMVR_SEARCH_WAVES
+#define MM_DMVR_SEARCH_WAVES 4  // waves per SIMD = workgroups per CU (LDS): 128 VGPRs, spill-free
+#endif
+constexpr int DMVR_SEARCH_GRID = 256 * MM_DMVR_SEARCH_WAVES;  // grid-stride over the survivors
+static_assert(MM_DMVR_SEARCH_WAVES * (sizeof(DmvrWaveLds) * DMVR_WAVES + sizeof(PackedTaps) + 64 * 36) <= 160 * 1024,
+              "the workgroups of one CU fit its LDS");
+__global__ void __launch_bounds__(DMVR_SEARCH_WG) __attribute__((amdgpu_waves_per_eu(MM_DMVR_SEARCH_WAVES))) k_dmvr_search_dev(
+    SeqConst sc, Geometry geo, const SubPuDev* __restrict__ sp, MpaCache cache, const PicTables t, DmvrWork w,
+    JobDev* __restrict__ jobs, int32_t* __restrict__ mvd) {
 #if defined(__HIP_DEVICE_COMPILE__)  // device-only filter paths (mm_filter.h predict_rows02, PtrRows, LdsRows)
   __shared__ PackedTaps s_taps;
-  __shared__ uint32_t s_win[2][DMVR_WIN_H * DMVR_WIN_STRIDE];
-  __shared__ mm_int2 s_pos[DMVR_MAX_ITEMS];  // item 2 * (j * n + e) + l
-  __shared__ int s_box[2][4];                // per list: min / max of the in-range xPos, yPos
-  __shared__ uint32_t s_cost[N_OFF];
+  __shared__ M3 s_ged[3 + MAX_SLOTS];  // indexed per lane: staged by stage_arg_words
+  __shared__ DmvrWaveLds s_wave[DMVR_WAVES];
   const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  DmvrWaveLds& L = s_wave[wv];
   static_assert(sizeof(PackedTaps) % 16 == 0 && sizeof(PackedTaps) / 16 <= DMVR_SEARCH_WG, "one 16-byte word per thread");
   if (tid < sizeof(PackedTaps) / 16)
     lds_put(reinterpret_cast<uint4*>(&s_taps)[tid], reinterpret_cast<const uint4*>(&c_packed_taps)[tid], make_uint4(~0u, ~0u, ~0u, ~0u));
+  stage_arg_words<sizeof(s_ged) / 4>(reinterpret_cast<const uint32_t*>(t.ged), reinterpret_cast<uint32_t*>(s_ged));
+  __syncthreads();  // s_taps, s_ged: the only LDS the waves share
   const int n_surv = (int)(*w.count >> 32);
   const RefPool pool = t.pool;
-  // items alternate lists and the stride is even, so every item of a thread has the list tid & 1
-  for (int k = blockIdx.x; k < n_surv; k += gridDim.x) {
+  for (int k = blockIdx.x * DMVR_WAVES + wv; k < n_surv; k += gridDim.x * DMVR_WAVES) {
     const int s = w.surv_s[k];
     const SubPuDev u = sp[s];
-    const int n = u.n, n_items = 2 * (N_OFF - 1) * n, log2n = 31 - __clz(n);  // n: 8 or 16
+    const int n = u.n, log2n = 31 - __clz(n);                       // n: 8 or 16
+    const int n_offs = DMVR_LANE_OFFS >> (4 - log2n);               // 12 or 6 offsets per lane
+    const int part = lane >> (log2n + 1), e = (lane >> 1) & (n - 1), l = lane & 1;
     // the sub-PU's slots are uniform: scalar loads of the kernel argument's table
     const int slot0 = __builtin_amdgcn_readfirstlane(u.slot[0]), slot1 = __builtin_amdgcn_readfirstlane(u.slot[1]);
     const uint32_t off_y[2] = {t.ref[slot0].off_y, t.ref[slot1].off_y};
     const int stride_y[2] = {t.ref[slot0].stride_y, t.ref[slot1].stride_y};
-    if (tid < 8) lds_put((&s_box[0][0])[tid], (tid & 1) ? INT_MIN : INT_MAX, 0);
-    if (tid == 0) lds_put(s_cost[N_OFF / 2], w.ccost[s], 0u);
-    __syncthreads();  // s_taps staged; the previous sub-PU's LDS reads and decision are done
-    // 1. positions of the (offset, sub-block, list) items and the in-range box of this thread's list
-    int xmin = INT_MAX, xmax = INT_MIN, ymin = INT_MAX, ymax = INT_MIN;
-    const mm_int2* src_pos = pos + w.surv_base[k];
-    for (int i = tid; i < n_items; i += DMVR_SEARCH_WG) {
-      const mm_int2 q = src_pos[i];
-      lds_put(s_pos[i], q, mm_int2{INT_MAX, INT_MAX});
-      const int xPos = q.x >> 4, yPos = q.y >> 4;
-      if (!sb_out_of_range(xPos, yPos, geo.W, geo.H, geo.maxCUw, geo.maxCUh, 4, 4)) {
-        xmin = min(xmin, xPos);
-        xmax = max(xmax, xPos);
-        ymin = min(ymin, yPos);
-        ymax = max(ymax, yPos);
-      }
+    if (lane < 2 * (N_OFF - 1)) {  // 0. the 24 non-centre offsets' setups of both lists
+      BlockSetup b;
+      dmvr_offset_setup(sc, u, dmvr_outer_offset(lane >> 1), lane & 1, w.cterms[2 * s + (lane & 1)], s_ged, &b);
+      lds_put(L.set[lane >> 1][lane & 1], b, BlockSetup{});
     }
+    if (lane == 0) lds_put(L.cost[N_OFF / 2], w.ccost[s], 0u);
+    wave_lds_sync();
+    // 1. this lane's positions, and the in-range box of its list
+    int32_t pfx[DMVR_LANE_OFFS] = {}, pfy[DMVR_LANE_OFFS] = {};
+    int xmin = INT_MAX, xmax = INT_MIN, ymin = INT_MAX, ymax = INT_MIN;
+    dmvr_positions_offsets(sc, u, l, e, cache, [&](int j) -> const BlockSetup& { return L.set[part * n_offs + j][l]; },
+                           n_offs, [&](int j, int32_t fx, int32_t fy) {
+#pragma unroll
+                             for (int q = 0; q < DMVR_LANE_OFFS; q++)
+                               if (q == j) {
+                                 pfx[q] = fx;
+                                 pfy[q] = fy;
+                               }
+                             const int xPos = fx >> 4, yPos = fy >> 4;
+                             if (!sb_out_of_range(xPos, yPos, geo.W, geo.H, geo.maxCUw, geo.maxCUh, 4, 4)) {
+                               xmin = min(xmin, xPos);
+                               xmax = max(xmax, xPos);
+                               ymin = min(ymin, yPos);
+                               ymax = max(ymax, yPos);
+                             }
+                           });
 #pragma unroll
     for (int d = 2; d < 64; d <<= 1) {  // over the lanes of the same list (same parity)
       xmin = min(xmin, __shfl_xor(xmin, d));
@@ -750,75 +774,82 @@ __global__ void __launch_bounds__(DMVR_SEARCH_WG) __attribute__((amdgpu_waves_pe
       ymin = min(ymin, __shfl_xor(ymin, d));
       ymax = max(ymax, __shfl_xor(ymax, d));
     }
-    if (lane < 2 && xmin <= xmax) {
-      atomicMin(&s_box[lane][0], xmin);
-      atomicMax(&s_box[lane][1], xmax);
-      atomicMin(&s_box[lane][2], ymin);
-      atomicMax(&s_box[lane][3], ymax);
-    }
-    __syncthreads();
     // 2. stage the union windows: columns [bx0, bx0 + 8 cw), rows [by0, by0 + rows)
     int bx0[2], by0[2];
     bool staged[2];
 #pragma unroll
-    for (int l = 0; l < 2; l++) {
-      const int bxmin = s_box[l][0], bxmax = s_box[l][1], bymin = s_box[l][2], bymax = s_box[l][3];
-      bx0[l] = (bxmin - 3) & ~1;
-      by0[l] = bymin - 3;
-      const int cw = (bxmax + 9 - bx0[l] + 7) >> 3, rows = bymax - bymin + 11;  // 16-byte chunks per row, rows
-      staged[l] = bxmin <= bxmax && cw * 8 <= DMVR_WIN_W && rows <= DMVR_WIN_H;
-      if (staged[l]) {
-        const char* src = pool.base + off_y[l] + (long)(by0[l] * stride_y[l] + bx0[l]) * 2;
-        for (int k = tid; k < rows * cw; k += DMVR_SEARCH_WG) {
-          const int r = k / cw, c = k - r * cw;
+    for (int ll = 0; ll < 2; ll++) {
+      const int bxmin = __shfl(xmin, ll), bxmax = __shfl(xmax, ll), bymin = __shfl(ymin, ll), bymax = __shfl(ymax, ll);
+      bx0[ll] = (bxmin - 3) & ~1;
+      by0[ll] = bymin - 3;
+      const int cw = (bxmax + 9 - bx0[ll] + 7) >> 3, rows = bymax - bymin + 11;  // 16-byte chunks per row, rows
+      staged[ll] = bxmin <= bxmax && cw * 8 <= DMVR_WIN_W && rows <= DMVR_WIN_H;
+      if (staged[ll]) {
+        const char* src = pool.base + off_y[ll] + (long)(by0[ll] * stride_y[ll] + bx0[ll]) * 2;
+        for (int c4 = lane; c4 < rows * cw; c4 += 64) {
+          const int r = c4 / cw, c = c4 - r * cw;
           typedef uint32_t u4a4 __attribute__((ext_vector_type(4), aligned(4)));
-          const u4a4 q = *reinterpret_cast<const u4a4*>(src + ((long)r * stride_y[l] + 8 * c) * 2);
-          uint32_t* d = &s_win[l][r * DMVR_WIN_STRIDE + 4 * c];
-          lds_put(d[0], q.x, ~0u);
-          d[1] = q.y;
-          d[2] = q.z;
-          d[3] = q.w;
+          const u4a4 q = *reinterpret_cast<const u4a4*>(src + ((long)r * stride_y[ll] + 8 * c) * 2);
+          uint32_t* dp = &L.win[ll][r * DMVR_WIN_STRIDE + 4 * c];
+          lds_put(dp[0], q.x, ~0u);
+          dp[1] = q.y;
+          dp[2] = q.z;
+          dp[3] = q.w;
         }
       }
     }
-    __syncthreads();
-    // 3. rows 0 and 2 of both predictions per (offset, sub-block), SAD per offset
+    wave_lds_sync();
+    // 3. rows 0 and 2 of the lane's prediction per offset; SAD against the partner list's, per offset
+    const uint32_t* win = L.win[l];
+    const int wbx0 = l ? bx0[1] : bx0[0], wby0 = l ? by0[1] : by0[0];
+    const bool wstaged = l ? staged[1] : staged[0];
+    const uint32_t woff = l ? off_y[1] : off_y[0];
+    const int wstride = l ? stride_y[1] : stride_y[0];
 #pragma unroll 1
-    for (int base = 0; base < (N_OFF - 1) * 16; base += DMVR_SEARCH_WG) {  // uniform trip count (shuffles below)
-      const int oe = base + tid;
-      uint32_t v = 0;
-      if (oe < (N_OFF - 1) * n) {
-        int16_t p[2][8];
+    for (int j = 0; j < n_offs; j++) {
+      int32_t fx = pfx[0], fy = pfy[0];
 #pragma unroll
-        for (int l = 0; l < 2; l++) {
-          const mm_int2 q = s_pos[2 * oe + l];
-          const int xPos = q.x >> 4, yPos = q.y >> 4;
-          const uint32_t* ht = s_taps.lh[q.x & 15][(xPos - 3) & 1];
-          const uint32_t* vt = s_taps.lv[q.y & 15];
-          const int x0 = (xPos - 3) & ~1;
-          if (sb_out_of_range(xPos, yPos, geo.W, geo.H, geo.maxCUw, geo.maxCUh, 4, 4)) {
-#pragma unroll
-            for (int i = 0; i < 8; i++) p[l][i] = 0;
-          } else if (staged[l]) {
-            const LdsRows rows{&s_win[l][(yPos - 3 - by0[l]) * DMVR_WIN_STRIDE + ((x0 - bx0[l]) >> 1)], DMVR_WIN_STRIDE};
-            predict_rows02(rows, ht, vt, geo.bd, p[l]);
-          } else {
-            const PtrRows rows{pool.base + off_y[l] + (long)((yPos - 3) * stride_y[l] + x0) * 2, stride_y[l] * 2};
-            predict_rows02(rows, ht, vt, geo.bd, p[l]);
-          }
+      for (int q = 1; q < DMVR_LANE_OFFS; q++)
+        if (q == j) {
+          fx = pfx[q];
+          fy = pfy[q];
         }
-        v = dmvr_sad_rows02(p[0], p[1]);
+      const int xPos = fx >> 4, yPos = fy >> 4;
+      int16_t p[8];
+      if (sb_out_of_range(xPos, yPos, geo.W, geo.H, geo.maxCUw, geo.maxCUh, 4, 4)) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) p[i] = 0;
+      } else {
+        const uint32_t* ht = s_taps.lh[fx & 15][(xPos - 3) & 1];
+        const uint32_t* vt = s_taps.lv[fy & 15];
+        const int x0 = (xPos - 3) & ~1;
+        if (wstaged) {
+          const LdsRows rows{&win[(yPos - 3 - wby0) * DMVR_WIN_STRIDE + ((x0 - wbx0) >> 1)], DMVR_WIN_STRIDE};
+          predict_rows02(rows, ht, vt, geo.bd, p);
+        } else {
+          const PtrRows rows{pool.base + woff + (long)((yPos - 3) * wstride + x0) * 2, wstride * 2};
+          predict_rows02(rows, ht, vt, geo.bd, p);
+        }
       }
-      for (int d = 1; d < n; d <<= 1) v += __shfl_xor(v, d);  // n-lane segments (n divides 64)
-      if (oe < (N_OFF - 1) * n && (oe & (n - 1)) == 0) lds_put(s_cost[dmvr_outer_offset(oe >> log2n)], v, 0u);
+      uint32_t v = 0;
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const uint32_t mine = (uint32_t)(uint16_t)p[2 * i] | ((uint32_t)(uint16_t)p[2 * i + 1] << 16);
+        const uint32_t other = __shfl_xor(mine, 1);
+        v += (uint32_t)abs((int)(int16_t)(mine & 0xffffu) - (int)(int16_t)(other & 0xffffu)) +
+             (uint32_t)abs((int)(int16_t)(mine >> 16) - (int)(int16_t)(other >> 16));
+      }
+      for (int d = 2; d < 2 * n; d <<= 1) v += __shfl_xor(v, d);  // the part's n sub-blocks (same list)
+      if ((lane & (2 * n - 1)) == 0) lds_put(L.cost[dmvr_outer_offset(part * n_offs + j)], v, 0u);
     }
-    __syncthreads();
+    wave_lds_sync();
     // 4. the decision and the refined MVs
-    if (tid == 0) {
+    if (lane == 0) {
       int tdx, tdy;
-      dmvr_decide(u, s_cost, &tdx, &tdy);
+      dmvr_decide(u, L.cost, &tdx, &tdy);
       dmvr_apply(s, u, tdx, tdy, jobs, mvd);
     }
+    wave_lds_sync();  // the decision's reads before the next survivor's setups
   }
 #endif
 }
@@ -1082,6 +1113,12 @@ struct PlanSlot {
   DevBuf<mm_int2> mc_far[2][2];
   DevBuf<SubPuDev> dmvr_sub;  // MM-DMVR sub-PU records (k_plan_place) and their element offsets / chunks
   DevBuf<int> dmvr_off, dmvr_chunk;
+  // MM-DMVR work of the slot's picture: centre setups [2 s + l], refined deltas, survivor list
+  DevBuf<BlockSetup> dmvr_setup;
+  DevBuf<CentreTerms> dmvr_cterms;
+  DevBuf<int> dmvr_mvd, dmvr_surv_s;
+  DevBuf<unsigned long long> dmvr_count;
+  DevBuf<uint32_t> dmvr_ccost;
   int n_ensured = 0;  // largest stripe size the buffers were sized for (they only grow)
   int pics_ensured = 1;  // pictures per call the sub-block capacity covers (mm_pred_device_multi)
   bool dmvr_ensured = false;
@@ -1090,6 +1127,12 @@ struct PlanSlot {
     dmvr_sub.release();
     dmvr_off.release();
     dmvr_chunk.release();
+    dmvr_setup.release();
+    dmvr_cterms.release();
+    dmvr_mvd.release();
+    dmvr_surv_s.release();
+    dmvr_count.release();
+    dmvr_ccost.release();
     job_off.release();
     job_chunk.release();
     jobs.release();
@@ -1173,15 +1216,9 @@ struct mm_ctx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::map<int, RefHost> orgs;  // original luma pictures for mm_sad_window
   DevBuf<MeBlockDev> d_me_blocks;
-  // MM-DMVR of the device-planned picture (mm_set_dmvr / mm_pred_dmvr): the per-(sub-PU, offset,
-  // list) setups, the 25 costs and the refined deltas of every sub-PU; used on the context stream only
+  // MM-DMVR of the device-planned picture (mm_set_dmvr / mm_pred_dmvr): its buffers are the plan
+  // slot's (PlanSlot::dmvr_*); the search runs on the context stream
   bool dmvr = false;
-  DevBuf<int> d_dmvr_mvd;
-  DevBuf<BlockSetup> d_dmvr_setup;
-  DevBuf<mm_int2> d_dmvr_pos;  // both lists' reprojected positions per (survivor, offset, sub-block)
-  DevBuf<unsigned long long> d_dmvr_count;  // DmvrWork (k_dmvr_centre_dev's survivor list)
-  DevBuf<uint32_t> d_dmvr_ccost;
-  DevBuf<int> d_dmvr_surv_s, d_dmvr_surv_base, d_dmvr_surv_tbase, d_dmvr_surv_tchunk;
   // MM-MVP: the device copy of the epipole list (refreshed when its version moves, staged through a
   // pinned buffer on the context stream), the host-buffer API's query / result buffers and the
   // deferred status word (sticky until mm_mvp_status reads it)
@@ -1475,15 +1512,6 @@ int mm_destroy(mm_ctx* c) {
   c->d_ged.release();
   for (auto& kv : c->orgs) (void)hipFree(kv.second.y);
   c->d_me_blocks.release();
-  c->d_dmvr_mvd.release();
-  c->d_dmvr_setup.release();
-  c->d_dmvr_pos.release();
-  c->d_dmvr_count.release();
-  c->d_dmvr_ccost.release();
-  c->d_dmvr_surv_s.release();
-  c->d_dmvr_surv_base.release();
-  c->d_dmvr_surv_tbase.release();
-  c->d_dmvr_surv_tchunk.release();
   c->d_mvp_q.release();
   c->d_mvp_out.release();
   c->d_mvp_status.release();
@@ -1804,15 +1832,15 @@ static int ensure_slot_buffers(mm_ctx* c, PlanSlot& S, int n, bool dmvr, int pic
     HIPCHK(c, S.dmvr_sub.ensure(c, k.subs));
     HIPCHK(c, S.dmvr_off.ensure(c, k.subs));
     HIPCHK(c, S.dmvr_chunk.ensure(c, (size_t)k.dmvr_elems / 64 + 1));
-    HIPCHK(c, c->d_dmvr_setup.ensure(c, (size_t)k.subs * N_OFF * 2));
-    HIPCHK(c, c->d_dmvr_mvd.ensure(c, 2 * (size_t)k.subs));
-    HIPCHK(c, c->d_dmvr_pos.ensure(c, 2 * (size_t)k.dmvr_elems));
-    HIPCHK(c, c->d_dmvr_count.ensure(c, 1));
-    HIPCHK(c, c->d_dmvr_ccost.ensure(c, k.subs));
-    HIPCHK(c, c->d_dmvr_surv_s.ensure(c, k.subs));
-    HIPCHK(c, c->d_dmvr_surv_base.ensure(c, k.subs));
-    HIPCHK(c, c->d_dmvr_surv_tbase.ensure(c, k.subs));
-    HIPCHK(c, c->d_dmvr_surv_tchunk.ensure(c, 2 * (size_t)k.dmvr_elems / 8 / 64 + 1));
+    // per slot, sized by the sub-PUs: centre setups and centre terms (2 x (56 + 44) B), delta, centre
+    // cost, survivor index -- about 220 B per sub-PU (32 MB at 6144x3072; the other offsets' setups,
+    // positions and costs of the survivors live in the search kernel's registers and LDS)
+    HIPCHK(c, S.dmvr_setup.ensure(c, (size_t)k.subs * 2));
+    HIPCHK(c, S.dmvr_cterms.ensure(c, (size_t)k.subs * 2));
+    HIPCHK(c, S.dmvr_mvd.ensure(c, 2 * (size_t)k.subs));
+    HIPCHK(c, S.dmvr_count.ensure(c, 1));
+    HIPCHK(c, S.dmvr_ccost.ensure(c, k.subs));
+    HIPCHK(c, S.dmvr_surv_s.ensure(c, k.subs));
     S.dmvr_ensured = true;
   }
   bool fresh_jobs = false;
@@ -1881,20 +1909,16 @@ static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables
       st = st_back;
       back = false;
     }
-    const int gd = (int)std::min<long>(DMVR_GRID, ((long)k.subs * N_OFF * 2 + 255) / 256 + 1);
-    const DmvrWork dw{c->d_dmvr_count.p, c->d_dmvr_ccost.p, c->d_dmvr_surv_s.p, c->d_dmvr_surv_base.p,
-                      c->d_dmvr_surv_tbase.p, c->d_dmvr_surv_tchunk.p};
-    int32_t* mvd = want_mvd ? c->d_dmvr_mvd.p : nullptr;
-    hipLaunchKernelGGL(k_dmvr_setup_dev, dim3(gd), dim3(256), 0, st, c->sc, S.meta.p, S.dmvr_sub.p, t, c->d_dmvr_setup.p,
-                       dw.count);
+    const int gd = (int)std::min<long>(DMVR_GRID, ((long)k.subs * 2 + 255) / 256 + 1);
+    const DmvrWork dw{S.dmvr_count.p, S.dmvr_ccost.p, S.dmvr_surv_s.p, S.dmvr_cterms.p};
+    int32_t* mvd = want_mvd ? S.dmvr_mvd.p : nullptr;
+    hipLaunchKernelGGL(k_dmvr_setup_dev, dim3(gd), dim3(256), 0, st, c->sc, S.meta.p, S.dmvr_sub.p, t, S.dmvr_setup.p,
+                       S.dmvr_cterms.p, dw.count);
     const int gcen = (int)std::min<long>(DMVR_GRID, ((long)k.subs * 32 + 255) / 256);
     hipLaunchKernelGGL(k_dmvr_centre_dev, dim3(std::max(1, gcen)), dim3(256), 0, st, c->sc, geo, S.meta.p, S.dmvr_sub.p,
-                       c->d_dmvr_setup.p, make_cache(c), t, dw, S.jobs.p, mvd);
-    const int gc = (int)std::min<long>(DMVR_GRID, ((long)k.dmvr_elems * 2 / 8 + 255) / 256 + 1);
-    hipLaunchKernelGGL(k_dmvr_reproj_dev, dim3(gc), dim3(256), 0, st, c->sc, S.dmvr_sub.p, c->d_dmvr_setup.p,
-                       make_cache(c), dw, c->d_dmvr_pos.p);
-    hipLaunchKernelGGL(k_dmvr_search_dev, dim3(std::max(1, std::min(DMVR_SEARCH_GRID, k.subs))), dim3(DMVR_SEARCH_WG),
-                       0, st, geo, S.dmvr_sub.p, c->d_dmvr_pos.p, t, dw, S.jobs.p, mvd);
+                       S.dmvr_setup.p, make_cache(c), t, dw, S.jobs.p, mvd);
+    hipLaunchKernelGGL(k_dmvr_search_dev, dim3(std::max(1, std::min(DMVR_SEARCH_GRID, (k.subs + DMVR_WAVES - 1) / DMVR_WAVES))), dim3(DMVR_SEARCH_WG),
+                       0, st, c->sc, geo, S.dmvr_sub.p, make_cache(c), t, dw, S.jobs.p, mvd);
   }
   McRec mc;
   mc.meta = S.mc_meta.p;
@@ -1925,11 +1949,13 @@ static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables
     if (back) HIPCHK(c, hipEventRecord(c->ev_plan, st));
   }
   if (back) {  // plan-ahead: (reprojection and) interpolation on the context stream
-    // The host waits for this picture's planning (bound to k_setup_dev / k_reproj_dev) before it issues
-    // the context stream's wait: the event is then complete, so the runtime issues no cross-queue
-    // barrier packet between the previous picture's k_mc_dev and this picture's next kernel (C3
-    // 0.178-0.180 -> 0.173-0.175 ms per picture, profiles/r03_ab_hostsync.txt).  The planning waits
-    // only for the k_mc_dev of two calls back, so the host still runs about one picture ahead.
+    // Round 3 had the host wait for this picture's planning before it issued the context stream's
+    // wait, so that the runtime put no cross-queue barrier packet between two pictures' kernels (C3
+    // 0.178-0.180 -> 0.173-0.175 ms, profiles/r03_ab_hostsync.txt, when ev_plan completed with the
+    // short k_setup_dev).  With the reprojection ahead, ev_plan completes with k_reproj_dev, which runs
+    // as long as the previous picture's k_mc_dev: the wait put the host's wake-up (~20 us in the
+    // kernel trace) between k_reproj_dev and k_mc_dev and kept the next call's planning from being
+    // issued.  Without it: 0.1712-0.1727 vs 0.1724-0.1750 ms per picture (profiles/r05_ab_overlap.txt).
     if (PLAN_AHEAD_HOST_WAIT) HIPCHK(c, hipEventSynchronize(c->ev_plan));
     HIPCHK(c, hipStreamWaitEvent(st_back, c->ev_plan, 0));
     st = st_back;
@@ -1958,7 +1984,7 @@ static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables
 // go to the picture's status word and are reported by mm_pred_status.
 // only_list / hp / store: mm_pred_list (-1 / 0 / 3 for the normal prediction).
 // dmvr: MM_PUF_DMVR PUs allowed (the context's mm_set_dmvr, or mm_pred_dmvr); want_mvd: keep the
-// refined delta of every DMVR sub-PU, in placement order, in d_dmvr_mvd.
+// refined delta of every DMVR sub-PU, in placement order, in the slot's dmvr_mvd.
 static int launch_pictures(mm_ctx* c, const mm_pic_job* pics, int n_pics, int only_list = -1, int hp = 0,
                            int store = 3, bool may_plan_ahead = false, bool dmvr = false, bool want_mvd = false) {
   std::vector<std::pair<int, RefDev>> refs;
@@ -2296,7 +2322,7 @@ int mm_pred_dmvr(mm_ctx* c, int cur_poc, const mm_pu_desc* pus, int n, int16_t* 
   // the deltas of the sub-PUs in placement order: PUs in list order (DMVR bucket placement keeps
   // input order), sub-PUs in raster order
   if (mvd_out && n_sub)
-    HIPCHK(c, hipMemcpy(mvd_out, c->d_dmvr_mvd.p, 2 * (size_t)n_sub * sizeof(int32_t), hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(mvd_out, c->slot[0].dmvr_mvd.p, 2 * (size_t)n_sub * sizeof(int32_t), hipMemcpyDeviceToHost));
   return MM_OK;
 }
 

@@ -273,75 +273,132 @@ MM_HD void block_setup(BlockSetup* b, const SeqConst& s, int model, bool luma, i
                        int size_w, int size_h, int32_t mv_hor, int32_t mv_ver, const M3* ged_rot) {
   block_setup_f(b, s, model, luma, pos_x, pos_y, size_w, size_h, mv_to_float(mv_hor), mv_to_float(mv_ver), ged_rot);
 }
-MM_HD void block_setup_f(BlockSetup* b, const SeqConst& s, int model, bool luma, int pos_x, int pos_y, int size_w,
-                         int size_h, float mvx, float mvy, const M3* ged_rot) {
+// The MV-independent part of a block setup: what the model derives from the block centre alone
+// (TAN: sin / cos of the centre's elevation complement and its azimuth; 3DT: the centre's sphere
+// point; ROT: the un-rotation about the centre; GED MODULATED: the polar angle of the rotated centre).
+// block_setup_f is centre_terms + setup_from_centre; MM-DMVR, whose 25 offsets share one centre,
+// computes the centre terms once per (sub-PU, list) and only the MV part per offset.
+struct CentreTerms {
+  float t[9];
+  float cx, cy;  // the block centre in component units (MVReprojection.cpp:133)
+};
+MM_HD void centre_terms(CentreTerms* ct, const SeqConst& s, int model, float cx, float cy, const M3* ged_rot) {
+  for (int i = 0; i < 9; i++) ct->t[i] = 0.0f;
+  ct->cx = cx;
+  ct->cy = cy;
+  const Math sc{false};
+  switch (model) {
+    case TANGENTIAL: {  // TangentialMotionModel.cpp:8-48
+      V3 c3 = erp_to_sphere(cx, cy, s, sc);
+      V3 sp = cart_to_sph(c3, sc, false);
+      float epsC = (float)(PI_2_D - (double)sp.y);
+      ct->t[2] = sp.z;  // alphaC
+#if MM_TAN_CENTRE_MODE
+      ct->t[0] = g_sinf(epsC);  // sE
+      ct->t[1] = g_cosf(epsC);  // cE
+#else
+      ct->t[0] = sinf_via_double(epsC);  // sE: unqualified sin(float) -> double ::sin
+      ct->t[1] = cosf_via_double(epsC);  // cE
+#endif
+    } break;
+    case THREE_D_TRANSLATIONAL: {  // ThreeDTranslationalMotionModel.cpp:7-24
+      V3 c = erp_to_sphere(cx, cy, s, sc);
+      ct->t[0] = c.x;
+      ct->t[1] = c.y;
+      ct->t[2] = c.z;
+    } break;
+    case ROTATIONAL: {  // RotationalMotionModel.cpp:8-78
+      V3 sp = cart_to_sph(erp_to_sphere(cx, cy, s, sc), sc, false);
+      M3 unrotPhi = angle_axis(-sp.z, 0.0f, 0.0f, 1.0f);
+      M3 unrotTheta = angle_axis((float)(PI_2_D - (double)sp.y), 0.0f, 1.0f, 0.0f);
+      M3 unrot = mat_mul(unrotTheta, unrotPhi);
+      for (int i = 0; i < 9; i++) ct->t[i] = unrot.m[i];
+    } break;
+    case GEODESIC_X:
+    case GEODESIC_Y:
+    case GEODESIC_Z:
+    case GEODESIC_CAMPOSE:  // GeodesicMotionModel.cpp:101-176
+      if (s.ged_flavor == 1) {
+        V3 c3 = erp_to_sphere(cx, cy, s, sc);
+        V3 cr = mat_vec(*ged_rot, c3);
+        V3 sp = cart_to_sph(cr, sc, false);
+        ct->t[0] = sp.y;
+      }
+      break;
+    default:
+      break;
+  }
+}
+// The zero-MV shortcut of the models that have one (chroma only for GED: only modelMotion shortcuts)
+MM_HD bool setup_is_identity(int model, bool luma, float mvx, float mvy) {
+  const bool zero = (mvx == 0.0f && mvy == 0.0f);
+  if (model == TANGENTIAL || model == THREE_D_TRANSLATIONAL || model == ROTATIONAL) return zero;
+  if (model >= GEODESIC_X && model <= GEODESIC_CAMPOSE) return !luma && zero;
+  return false;
+}
+// The setup at MV (mvx, mvy) from the block's centre terms
+MM_HD void setup_from_centre(BlockSetup* b, const SeqConst& s, int model, bool luma, float mvx, float mvy,
+                             const CentreTerms& ct, const M3* ged_rot) {
   b->model = (int16_t)model;
   b->mvx = mvx;
   b->mvy = mvy;
-  // block centre in component units (MVReprojection.cpp:133)
-  const float cx = (float)pos_x + ((float)size_w - 1.0f) / 2.0f;
-  const float cy = (float)pos_y + ((float)size_h - 1.0f) / 2.0f;
   b->identity = 0;
   b->k = 0.0f;
   b->pad_ = 0.0f;
   for (int i = 0; i < 9; i++) b->M.m[i] = 0.0f;
-  const bool zero = (b->mvx == 0.0f && b->mvy == 0.0f);
+  if (model >= GEODESIC_X && model <= GEODESIC_CAMPOSE) b->M = *ged_rot;
+  if (setup_is_identity(model, luma, mvx, mvy)) {
+    b->identity = 1;
+    return;
+  }
   const Math sc{false};
   switch (model) {
-    case MPA_FRONT_BACK:
-    case MPA_LEFT_RIGHT:
-    case MPA_TOP_BOTTOM:
-      break;  // no shortcut, no per-block constants
-    case TANGENTIAL: {  // TangentialMotionModel.cpp:8-48
-      if (zero) { b->identity = 1; break; }
-      V3 c3 = erp_to_sphere(cx, cy, s, sc);
-      V3 sp = cart_to_sph(c3, sc, false);
-      float epsC = (float)(PI_2_D - (double)sp.y);
-      b->M.m[2] = sp.z;  // alphaC
-#if MM_TAN_CENTRE_MODE
-      b->M.m[0] = g_sinf(epsC);  // sE
-      b->M.m[1] = g_cosf(epsC);  // cE
-#else
-      b->M.m[0] = sinf_via_double(epsC);  // sE: unqualified sin(float) -> double ::sin
-      b->M.m[1] = cosf_via_double(epsC);  // cE
-#endif
+    case TANGENTIAL:
+      b->M.m[2] = ct.t[2];
+      b->M.m[0] = ct.t[0];
+      b->M.m[1] = ct.t[1];
+      break;
+    case THREE_D_TRANSLATIONAL: {
+      V3 cm = erp_to_sphere(ct.cx + b->mvx, ct.cy + b->mvy, s, sc);
+      b->M.m[0] = cm.x - ct.t[0];
+      b->M.m[1] = cm.y - ct.t[1];
+      b->M.m[2] = cm.z - ct.t[2];
     } break;
-    case THREE_D_TRANSLATIONAL: {  // ThreeDTranslationalMotionModel.cpp:7-24
-      if (zero) { b->identity = 1; break; }
-      V3 c = erp_to_sphere(cx, cy, s, sc);
-      V3 cm = erp_to_sphere(cx + b->mvx, cy + b->mvy, s, sc);
-      b->M.m[0] = cm.x - c.x;
-      b->M.m[1] = cm.y - c.y;
-      b->M.m[2] = cm.z - c.z;
-    } break;
-    case ROTATIONAL: {  // RotationalMotionModel.cpp:8-78
-      if (zero) { b->identity = 1; break; }
-      V3 sp = cart_to_sph(erp_to_sphere(cx, cy, s, sc), sc, false);
+    case ROTATIONAL: {
       M3 rot = mat_mul(angle_axis(-b->mvx * s.res, 0.0f, 0.0f, 1.0f),
                        angle_axis(b->mvy * s.res, 0.0f, 1.0f, 0.0f));
-      M3 unrotPhi = angle_axis(-sp.z, 0.0f, 0.0f, 1.0f);
-      M3 unrotTheta = angle_axis((float)(PI_2_D - (double)sp.y), 0.0f, 1.0f, 0.0f);
-      M3 unrot = mat_mul(unrotTheta, unrotPhi);
+      M3 unrot;
+      for (int i = 0; i < 9; i++) unrot.m[i] = ct.t[i];
       M3 unrotT = mat_transpose(unrot);
       b->M = mat_mul(unrotT, mat_mul(rot, unrot));
     } break;
     case GEODESIC_X:
     case GEODESIC_Y:
     case GEODESIC_Z:
-    case GEODESIC_CAMPOSE: {  // GeodesicMotionModel.cpp:101-176
-      b->M = *ged_rot;
-      if (!luma && zero) { b->identity = 1; break; }  // only modelMotion shortcuts (:130-132)
+    case GEODESIC_CAMPOSE:
       if (s.ged_flavor == 1) {
-        V3 c3 = erp_to_sphere(cx, cy, s, sc);
-        V3 cr = mat_vec(b->M, c3);
-        V3 sp = cart_to_sph(cr, sc, false);
         float rm = s.res * b->mvx;
-        b->k = g_sinf(sp.y + rm) / g_sinf(rm);
+        b->k = g_sinf(ct.t[0] + rm) / g_sinf(rm);
       }
-    } break;
-    default:
       break;
+    default:
+      break;  // MPA: no shortcut, no per-block constants
   }
+}
+MM_HD void block_setup_f(BlockSetup* b, const SeqConst& s, int model, bool luma, int pos_x, int pos_y, int size_w,
+                         int size_h, float mvx, float mvy, const M3* ged_rot) {
+  // block centre in component units (MVReprojection.cpp:133)
+  const float cx = (float)pos_x + ((float)size_w - 1.0f) / 2.0f;
+  const float cy = (float)pos_y + ((float)size_h - 1.0f) / 2.0f;
+  CentreTerms ct;
+  if (setup_is_identity(model, luma, mvx, mvy)) {  // the centre is not needed
+    for (int i = 0; i < 9; i++) ct.t[i] = 0.0f;
+    ct.cx = cx;
+    ct.cy = cy;
+  } else {
+    centre_terms(&ct, s, model, cx, cy, ged_rot);
+  }
+  setup_from_centre(b, s, model, luma, mvx, mvy, ct, ged_rot);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -46,7 +46,6 @@ int main() {
       mv_sum += mv.first + mv.second;
     }
     const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() / n_calls;
-    std::printf("MVP host per-call latency %.3f us (%d calls, checksum %ld)\n", us, n_calls, mv_sum);
 
     mm360::InterPredictionMM pred(&ctx);
     for (int by = 0; by < H; by += 16)
@@ -85,6 +84,8 @@ int main() {
       sum += a[k];
     }
     std::printf("OK reproject(0,0)=(%d,%d) luma-sum=%ld\n", f.X(0, 0), f.Y(0, 0), sum);
+    std::printf("MVP host per-call latency %.3f us (%d calls of motionVectorInDesiredMotionModel, MPA models, "
+                "checksum %ld)\n", us, n_calls, mv_sum);
     for (int k = 0; k < 2; k++) {
       (void)hipFree(dy[k]);
       (void)hipFree(dc[k][0]);
