@@ -190,9 +190,10 @@ static int twin_pred_segs(const Twin& t, const mmdev::PicTables& tab, const mm_p
     }
   }
 #pragma omp parallel for schedule(static, 256)
-  for (int g = 0; g < m.n_elems; g++)
-    reproj_thread_mc(g, find_item(job_off.data(), job_chunk.data(), g, m.n_jobs), t.sc, jobs.data(), job_off.data(),
-                     setups.data(), c, mc);
+  for (int g = 0; g < m.n_elems; g++) {
+    const int ji = find_item(job_off.data(), job_chunk.data(), g, m.n_jobs);
+    reproj_thread_mc(g, ji, t.sc, jobs.data(), job_off.data(), setups[ji], c, mc);
+  }
   Geometry geo = t.geo;
   geo.hp = hp;
   geo.store = store;

@@ -64,6 +64,9 @@ for step in "$@"; do
     pmcd=*)  # pmcd=<tag>=<counter,...>: one rocprofv3 --pmc pass over a short C3 run with a 30 % MM-DMVR share
       tag=$(echo "$step" | cut -d= -f2); ctrs=$(echo "$step" | cut -d= -f3 | tr ',' ' ')
       run "pmcd_$tag" 600 rocprofv3 --pmc $ctrs -d "gpurun_out/pmcd_$tag" -o run --output-format csv -- python3 bench.py --dmvr-share 0.3 --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 --no-mvp --no-c5 ;;
+    pmc5=*)  # pmc5=<tag>=<counter,...>: one rocprofv3 --pmc pass over a short C5 run
+      tag=$(echo "$step" | cut -d= -f2); ctrs=$(echo "$step" | cut -d= -f3 | tr ',' ' ')
+      run "pmc5_$tag" 600 rocprofv3 --pmc $ctrs -d "gpurun_out/pmc5_$tag" -o run --output-format csv -- python3 bench.py --config C5 --steps 1 --warmup 1 --no-cpu-baseline ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

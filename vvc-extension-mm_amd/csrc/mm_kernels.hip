@@ -394,7 +394,7 @@ __global__ void __launch_bounds__(256) k_reproj_dev(SeqConst sc, const PlanMeta*
   if (g - (int)__lane_id() >= n_elems) return;  // whole wave past the end
   const int ji = wave_find_item(job_offsets, chunk_start, g, meta->n_jobs);
   if (g >= n_elems) return;
-  reproj_thread_mc(g, ji, sc, jobs, job_offsets, setups, cache, mc);
+  reproj_thread_mc(g, ji, sc, jobs, job_offsets, setups[ji], cache, mc);
 }
 
 // The tap-pair tables (4 KB) are copied into LDS once per workgroup: every lane indexes them by
@@ -1932,23 +1932,29 @@ static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables
   // bound interpolation.  Its McRec writes go to this call's plan slot, whose previous reader (the
   // k_mc_dev of two calls back) the slot gate already orders before the planning.
   const bool reproj_ahead = back && MM_REPROJ_AHEAD;
-  if (back && KERNEL_EVENTS) {  // plan-ahead: ev_plan completes with k_setup_dev (or k_reproj_dev)
+  // the setups and the reprojection; `stop`: an event bound to the kernel's completion
+  // (hipExtLaunchKernelGGL), or null.  (Building the setups inside the reprojection kernel -- each
+  // workgroup its run of jobs into LDS -- measured 0.191 vs 0.172-0.174 ms per picture:
+  // profiles/r05_ab_overlap.txt.)
+  auto setup = [&](hipStream_t s_, hipEvent_t stop) {
+    hipExtLaunchKernelGGL(k_setup_dev, dim3(gs), dim3(256), 0, s_, nullptr, stop, 0, c->sc, S.meta.p, S.jobs.p, t,
+                          S.setup.p);
+  };
+  auto reproj = [&](hipStream_t s_, hipEvent_t stop) {
+    hipExtLaunchKernelGGL(k_reproj_dev, dim3(gr), dim3(256), 0, s_, nullptr, stop, 0, c->sc, S.meta.p, S.jobs.p,
+                          S.job_off.p, S.job_chunk.p, S.setup.p, make_cache(c), mc);
+  };
+  if (back) {
+    // plan-ahead: ev_plan completes with the last kernel of this picture on `aux` (the reprojection
+    // ahead, or the setups), bound to its dispatch when KERNEL_EVENTS
+    hipEvent_t stop = KERNEL_EVENTS ? c->ev_plan : nullptr;
     if (reproj_ahead) {
-      hipLaunchKernelGGL(k_setup_dev, dim3(gs), dim3(256), 0, st, c->sc, S.meta.p, S.jobs.p, t, S.setup.p);
-      hipExtLaunchKernelGGL(k_reproj_dev, dim3(gr), dim3(256), 0, st, nullptr, c->ev_plan, 0, c->sc, S.meta.p, S.jobs.p,
-                            S.job_off.p, S.job_chunk.p, S.setup.p, make_cache(c), mc);
+      setup(st, nullptr);
+      reproj(st, stop);
     } else {
-      hipExtLaunchKernelGGL(k_setup_dev, dim3(gs), dim3(256), 0, st, nullptr, c->ev_plan, 0, c->sc, S.meta.p, S.jobs.p,
-                            t, S.setup.p);
+      setup(st, stop);
     }
-  } else {
-    hipLaunchKernelGGL(k_setup_dev, dim3(gs), dim3(256), 0, st, c->sc, S.meta.p, S.jobs.p, t, S.setup.p);
-    if (reproj_ahead)
-      hipLaunchKernelGGL(k_reproj_dev, dim3(gr), dim3(256), 0, st, c->sc, S.meta.p, S.jobs.p, S.job_off.p, S.job_chunk.p,
-                         S.setup.p, make_cache(c), mc);
-    if (back) HIPCHK(c, hipEventRecord(c->ev_plan, st));
-  }
-  if (back) {  // plan-ahead: (reprojection and) interpolation on the context stream
+    if (!stop) HIPCHK(c, hipEventRecord(c->ev_plan, st));
     // Round 3 had the host wait for this picture's planning before it issued the context stream's
     // wait, so that the runtime put no cross-queue barrier packet between two pictures' kernels (C3
     // 0.178-0.180 -> 0.173-0.175 ms, profiles/r03_ab_hostsync.txt, when ev_plan completed with the
@@ -1959,11 +1965,11 @@ static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables
     if (PLAN_AHEAD_HOST_WAIT) HIPCHK(c, hipEventSynchronize(c->ev_plan));
     HIPCHK(c, hipStreamWaitEvent(st_back, c->ev_plan, 0));
     st = st_back;
+  } else {
+    setup(st, nullptr);
   }
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[1], st));
-  if (!reproj_ahead)
-    hipLaunchKernelGGL(k_reproj_dev, dim3(gr), dim3(256), 0, st, c->sc, S.meta.p, S.jobs.p, S.job_off.p, S.job_chunk.p,
-                       S.setup.p, make_cache(c), mc);
+  if (!reproj_ahead) reproj(st, nullptr);
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[2], st));
   // mc_done (plan-ahead): the slot's gate, complete when this k_mc is
   hipEvent_t stop = KERNEL_EVENTS ? mc_done : nullptr;

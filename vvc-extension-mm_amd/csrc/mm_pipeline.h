@@ -296,7 +296,7 @@ MM_HD void mpa_cache_thread(int t, const SeqConst& sc, int plane, int cols, int 
 
 // The reprojection of one element of a device-planned job, stored in k_mc's record layout.
 MM_HD void reproj_thread_mc(int g, int ji, const SeqConst& sc, const JobDev* jobs, const int* job_offsets,
-                            const BlockSetup* setups, const MpaCache& cache, const McRec& mc) {
+                            const BlockSetup& setup, const MpaCache& cache, const McRec& mc) {
   const JobDev& j = jobs[ji];
   // Elements are enumerated row-major over the block (the records k_mc reads and the frame-cache
   // entries are then contiguous across lanes); Eigen's column-major index still decides packet
@@ -322,7 +322,7 @@ MM_HD void reproj_thread_mc(int g, int ji, const SeqConst& sc, const JobDev* job
   const bool packet = packet_lane(eig, j.n);
   const GridSphere pg = grid_point(cache, j.model, (j.x >> 2) + col, (j.y >> 2) + row, packet);
   int32_t fx, fy;
-  reproject_element(sc, setups[ji], gx, gy, packet, mpa_cached, px, py, vip, j.comp ? 1 : 0, &fx, &fy, pg);
+  reproject_element(sc, setup, gx, gy, packet, mpa_cached, px, py, vip, j.comp ? 1 : 0, &fx, &fy, pg);
   // chroma 2x2 sub-block (row, col) belongs to luma 4x4 sub-block (row, col) of the same PU
   const int sb = j.sb_base + row * j.pu_cols + col;
   const int ox = j.x + 4 * col, oy = j.y + 4 * row;  // luma sub-block origin; 32 (ox / 2) == 16 ox
