@@ -38,3 +38,19 @@ def describe_mismatch(blocks, a, b, limit=3):
     for i in bad[:limit]:
         lines.append(f"block {blocks[i]} first: {a[off[i]:off[i+1]][:2].tolist()} vs {b[off[i]:off[i+1]][:2].tolist()}")
     return "\n".join(lines)
+
+
+def dmvr_zero_mv_pus(cfg, models, frame=3):
+    """DMVR PUs (workload.dmvr_pu_list) re-aimed so that search offsets land on a zero MV -- merge
+    (16, 0): offset (-1, 0) of L0 / (+1, 0) of L1; merge (-32, 16): offset (+2, -1) -- or the merge
+    MVs are zero themselves (an identity centre setup), every model in turn; every fourth PU keeps
+    its random MVs."""
+    pus = W.dmvr_pu_list(cfg, frame=frame)
+    aims = ([16, 0], [-32, 16], [0, 0])
+    for i in range(len(pus)):
+        if i % 4 == 3:
+            continue
+        mv0 = aims[i % 4]
+        pus[i]["mv"] = np.array([mv0, [-mv0[0], -mv0[1]]], dtype=np.int32)
+        pus[i]["model"] = (int(models[i % len(models)]),) * 2
+    return pus

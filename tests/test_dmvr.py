@@ -7,7 +7,7 @@ import pytest
 
 import mm360
 import twin
-from helpers import EPI, describe_mismatch
+from helpers import EPI, describe_mismatch, dmvr_zero_mv_pus
 from mm360 import workload as W
 from oracle.oracle import Oracle
 
@@ -31,6 +31,21 @@ def test_twin_dmvr_matches_oracle(w, h, models):
     assert (want_mvd != 0).any(axis=1).mean() > 0.3 and ((want_mvd % 16) != 0).any()
     for name, a, b in zip(("y", "cb", "cr"), got, want):
         assert np.array_equal(a, b), describe_mismatch(name, a, b)
+
+
+def test_twin_dmvr_zero_mv_offsets_matches_oracle():
+    """Offsets on the zero MV and zero merge MVs (identity setups; the device search derives the
+    offsets' setups from centre terms, test_gpu.py test_pred_dmvr_zero_mv_offsets_vs_oracle)."""
+    cfg = _cfg(512, 256, ALL)
+    params = mm360.seq_params(512, 256, ALL)
+    pus = dmvr_zero_mv_pus(cfg, ALL)
+    assert len(pus) >= 4 * len(ALL)  # every (aim, model) pair
+    refs = {poc: W.ref_planes(512, 256, poc) for poc in W.REF_POCS}
+    want, want_mvd = Oracle(params, EPI).predict_dmvr(W.CUR_POC, pus, refs, 512, 256)
+    got, got_mvd = twin.predict_dmvr(params, W.CUR_POC, pus, refs, 512, 256, EPI)
+    assert np.array_equal(got_mvd, want_mvd), np.argwhere(got_mvd != want_mvd)[:5]
+    for g, x in zip(got, want):
+        assert np.array_equal(g, x)
 
 
 def test_dmvr_rejects_ineligible_pus():

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 import mm360
-from helpers import EPI, GOLDEN, describe_mismatch, load_blocks, load_pus
+from helpers import EPI, GOLDEN, describe_mismatch, dmvr_zero_mv_pus, load_blocks, load_pus
 from mm360 import workload as W
 from oracle.oracle import Oracle
 
@@ -771,6 +771,31 @@ def test_pred_dmvr_vs_oracle(w, h):
     cfg = W.Config("T", w, h, tuple(models), 1, "test")
     params = mm360.seq_params(w, h, models)
     pus = W.dmvr_pu_list(cfg, frame=2)
+    refs = {poc: W.ref_planes(w, h, poc) for poc in W.REF_POCS}
+    want, want_mvd = Oracle(params, EPI).predict_dmvr(W.CUR_POC, pus, refs, w, h)
+    with _ctx(params) as ctx:
+        for poc, (y, cb, cr) in refs.items():
+            ctx.upload_ref(poc, y, cb, cr)
+        dst = _planes(cfg)
+        mvd = ctx.predict_dmvr(W.CUR_POC, pus, *dst)
+    assert np.array_equal(mvd, want_mvd), np.argwhere(mvd != want_mvd)[:5]
+    for name, t, x in zip(("y", "cb", "cr"), dst, want):
+        got = t.cpu().numpy()
+        assert np.array_equal(got, x), plane_mismatch(name, got, x)
+
+
+def test_pred_dmvr_zero_mv_offsets_vs_oracle():
+    """MM-DMVR where search offsets land on a zero MV (the models' identity setups, block_setup's
+    zero-MV shortcut) and where the merge MV itself is zero (the centre setup is the identity, the
+    offsets' setups still need the centre terms): the search derives each offset's setup from the
+    sub-PU's centre terms (mm_models.h setup_from_centre); deltas and planes == the oracle's full
+    block setups, every model, 16x16 and 16x8 / 8x16 sub-PUs."""
+    w, h = 512, 256
+    models = ME_ALL
+    cfg = W.Config("T", w, h, tuple(models), 1, "test")
+    params = mm360.seq_params(w, h, models)
+    pus = dmvr_zero_mv_pus(cfg, models)
+    assert len(pus) >= 4 * len(models)  # every (aim, model) pair
     refs = {poc: W.ref_planes(w, h, poc) for poc in W.REF_POCS}
     want, want_mvd = Oracle(params, EPI).predict_dmvr(W.CUR_POC, pus, refs, w, h)
     with _ctx(params) as ctx:
