@@ -704,6 +704,7 @@ def c5_record(args, steps=3, warmup=1):
     bit_exact of the device SADs against the oracle on a seeded sample of blocks, and the bound of
     k_me_sad from the committed PMC profile of this very library (VALU, not HBM: every candidate
     reprojects its block), when one exists."""
+    import glob
     import hashlib
     cfg = W.CONFIGS["C5"]
     params = mm360.seq_params(cfg.width, cfg.height, cfg.models)
@@ -735,12 +736,14 @@ def c5_record(args, steps=3, warmup=1):
         want = Oracle(params, [(W.CUR_POC, -1, W.GED_EPIPOLE_Q24)]).sad_window(
             W.CUR_POC, blocks[pick], W.ME_RANGE, 16, {poc: r[0] for poc, r in refs.items()}, org)
         bit_exact = bool(np.array_equal(got[pick], want))
-    bound = None
-    path = os.path.join(ROOT, "profiles", "r04_c5_pmc.json")
-    if os.path.exists(path):
+    bound = None  # the committed PMC profile of this very library, if any (tools/c5_pmc_json.py)
+    lib_sha = hashlib.sha256(open(mm360.LIB_PATH, "rb").read()).hexdigest()
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_c5_pmc.json")), reverse=True):
         d = json.load(open(path))
-        if d.get("lib_sha256") == hashlib.sha256(open(mm360.LIB_PATH, "rb").read()).hexdigest():
-            bound = {k: d[k] for k in ("kernel", "valu_busy", "valu_utilization", "note") if k in d}
+        if d.get("lib_sha256") == lib_sha:
+            bound = {k: d[k] for k in ("kernel", "valu_insts_per_wave", "valu_active_share", "valu_busy_2cyc",
+                                       "note") if k in d}
+            break
     n_cand = len(blocks) * C
     return {"workload": f"C5: {cfg.description}", "blocks": int(len(blocks)), "candidates": int(n_cand),
             "value": round(n_cand * steps / elapsed / 1e6, 2), "unit": "Mcandidates/s",

@@ -3,10 +3,12 @@ bench (tools/gpu_run.sh pmc_c5) -> profiles/r04_c5_pmc.json, keyed by the sha256
 that was profiled; bench.py's C3 line reports it as c5.bound when its own library has that hash.
 
 SQ_ACTIVE_INST_VALU counts, per wave, the quad-cycles in which the wave issued a VALU instruction
-(MI355X_MICROARCH.md: SQ_WAVE_CYCLES / SQ_ACTIVE_INST_* are quad-cycle counts); one SIMD issues at
-most one wave64 VALU instruction per 2 cycles (SIMD-32).  valu_busy = the SIMD-cycles VALU issue
-took over the SIMD-cycles the kernel ran: SQ_INSTS_VALU x 2 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8
-per XCD-summed cycle count) -- the share of the chip's VALU issue slots the kernel used."""
+(MI355X_MICROARCH.md: SQ_WAVE_CYCLES / SQ_ACTIVE_INST_* are quad-cycle counts).  Two figures:
+valu_active_share = SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x kernel cycles), the share of the SIMDs'
+time with a VALU quad-cycle in progress (one per instruction on this kernel); valu_busy_2cyc = the
+same with 2 cycles per instruction, the guide's SIMD-32 throughput of v_fma_f32 when waves
+interleave -- the share of issue slots used lies between the two.  Kernel cycles =
+GRBM_GUI_ACTIVE / 8 (summed over the XCDs)."""
 import csv
 import glob
 import hashlib
@@ -14,7 +16,7 @@ import json
 import sys
 
 ROOT = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
-OUT = sys.argv[2] if len(sys.argv) > 2 else "profiles/r04_c5_pmc.json"
+OUT = sys.argv[2] if len(sys.argv) > 2 else "profiles/r05_c5_pmc.json"
 KERNEL = "k_me_sad"
 
 
@@ -39,10 +41,10 @@ d = {"kernel": KERNEL, "lib_sha256": sha, "dispatches": n,
      "sq_insts_valu": insts, "sq_active_inst_valu": active, "sq_waves": waves, "sq_wave_cycles": wave_cycles,
      "grbm_gui_active": grbm,
      "valu_insts_per_wave": round(insts / waves, 1) if insts and waves else None,
-     "valu_busy": round(insts * 2 / (1024 * cycles), 3) if insts and cycles else None,
-     "valu_utilization": round(active * 4 / wave_cycles / 4, 3) if active and wave_cycles else None,
-     "note": "valu_busy = SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x kernel cycles): the share of the chip's VALU "
-             "issue slots k_me_sad used; valu_utilization = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES: the share of a "
-             "resident wave's cycles in which it issued VALU"}
+     "valu_active_share": round(active * 4 / (1024 * cycles), 3) if active and cycles else None,
+     "valu_busy_2cyc": round(insts * 2 / (1024 * cycles), 3) if insts and cycles else None,
+     "note": "valu_active_share = SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x kernel cycles); valu_busy_2cyc = "
+             "SQ_INSTS_VALU x 2 / (1024 SIMDs x kernel cycles) (the guide's SIMD-32 rate): the share of VALU "
+             "issue slots k_me_sad used lies between the two"}
 json.dump(d, open(OUT, "w"), indent=1)
 print(json.dumps(d))
