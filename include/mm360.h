@@ -250,7 +250,8 @@ int mm_pred_device(mm_ctx* ctx, int cur_poc, const mm_pu_desc* d_pus, int n, int
  * interpolation of all pictures share their launches, so small pictures or stripes no longer pay
  * the per-call launch chain each.  Same semantics as mm_pred_device per picture (plan-ahead,
  * deferred status; the status's PU index counts through the pictures' lists in call order).
- * 1 <= n_pics <= MM_MAX_PICS; MM_PUF_DMVR PUs only with n_pics == 1. */
+ * MM_PUF_DMVR PUs (mm_set_dmvr) are searched per picture inside the same chain -- the leaves of an
+ * RA temporal layer are DMVR's usual bi PUs.  1 <= n_pics <= MM_MAX_PICS. */
 #define MM_MAX_PICS 4
 typedef struct mm_pic_job {
   int32_t cur_poc;

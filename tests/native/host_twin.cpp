@@ -265,12 +265,13 @@ extern "C" int twin_pred(const mm_seq_params* p, int n_epi, const int32_t* epi, 
 }
 
 // mm_pred_device_multi twin: n_pics pictures (cur_pocs[q], PUs [pic_base[q], pic_base[q + 1]) of
-// `pus`) planned and predicted as ONE list, each into its own planes (dys[q], dcbs[q], dcrs[q]).
+// `pus`) planned and predicted as ONE list, each into its own planes (dys[q], dcbs[q], dcrs[q]);
+// dmvr: mm_set_dmvr's state.
 extern "C" int twin_pred_multi(const mm_seq_params* p, int n_epi, const int32_t* epi, int n_pics,
                                const int32_t* cur_pocs, const mm_pu_desc* pus, const int32_t* pic_base, int n_refs,
                                const int32_t* pocs, const int16_t* const* ys, const int16_t* const* cbs,
                                const int16_t* const* crs, int stride_y, int stride_c, int16_t* const* dys, int sdy,
-                               int16_t* const* dcbs, int16_t* const* dcrs, int sdc) {
+                               int16_t* const* dcbs, int16_t* const* dcrs, int sdc, int dmvr) {
   using namespace mmdev;
   Twin t;
   make_twin(p, &t);
@@ -283,6 +284,7 @@ extern "C" int twin_pred_multi(const mm_seq_params* p, int n_epi, const int32_t*
   std::string err;
   int rc = build_pic_tables(seq_info(*p), em, cur_pocs, n_pics, refs, &tab, &err);
   if (rc) return rc;
+  tab.dmvr = dmvr ? 1 : 0;  // mm_set_dmvr: MM_PUF_DMVR PUs of every picture run the search
   DstPlanes d{};
   for (int q = 0; q < MM_MAX_PICS; q++) {
     const int k = q < n_pics ? q : 0;

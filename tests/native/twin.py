@@ -39,7 +39,7 @@ def load():
                                     c_void_p, c_int, c_void_p, c_int, c_void_p]
     lib.twin_pred_multi.argtypes = [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p,
-                                    c_int]
+                                    c_int, c_int]
     lib.twin_mc_subblock.argtypes = [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                                      c_int, c_void_p, c_void_p, c_void_p]
     return lib
@@ -86,8 +86,9 @@ def predict(params, cur_poc, pus, refs, W, H, epipoles=(), dmvr=False):
     return dy, dcb, dcr
 
 
-def predict_multi(params, pictures, refs, W, H, epipoles=()):
-    """mm_pred_device_multi twin: pictures = [(cur_poc, pus)], predicted as one list; planes per picture."""
+def predict_multi(params, pictures, refs, W, H, epipoles=(), dmvr=False):
+    """mm_pred_device_multi twin: pictures = [(cur_poc, pus)], predicted as one list; planes per picture;
+    dmvr: mm_set_dmvr (MM_PUF_DMVR PUs run the search)."""
     lib = load()
     allp = np.ascontiguousarray(np.concatenate([p for _, p in pictures]))
     base = np.cumsum([0] + [len(p) for _, p in pictures]).astype(np.int32)
@@ -103,7 +104,7 @@ def predict_multi(params, pictures, refs, W, H, epipoles=()):
     rc = lib.twin_pred_multi(ctypes.addressof(params), n_epi, c_void_p(ea.ctypes.data), len(pictures),
                              c_void_p(cur.ctypes.data), c_void_p(allp.ctypes.data), c_void_p(base.ctypes.data),
                              len(pocs), c_void_p(pa.ctypes.data), ptrs[0], ptrs[1], ptrs[2], arrs[0][0].shape[1],
-                             arrs[1][0].shape[1], dp[0], W, dp[1], dp[2], W // 2)
+                             arrs[1][0].shape[1], dp[0], W, dp[1], dp[2], W // 2, int(dmvr))
     if rc:
         raise RuntimeError(f"twin predict_multi failed: {rc}")
     return outs

@@ -1051,6 +1051,40 @@ def test_pred_device_mixed_dmvr_picture_vs_oracle(plan_ahead):
             assert np.array_equal(a, b), plane_mismatch(name, a, b)
 
 
+@pytest.mark.parametrize("plan_ahead", [False, True])
+def test_pred_device_multi_with_dmvr_vs_oracle(plan_ahead):
+    """mm_pred_device_multi with mm_set_dmvr on: three C2 pictures, each with its own current POC,
+    references and camera-pose epipole, mixing MM_PUF_DMVR PUs (30 % of the DMVR-eligible bi leaves)
+    with ordinary PUs in ONE launch chain -- every picture's sub-PUs searched, decided and predicted
+    into its own planes -- == the oracle's predict_mixed picture by picture; twice, so the plan slots
+    and DMVR buffers are reused."""
+    from test_multi_picture import _pictures
+    cfg = W.CONFIGS["C2"]
+    models = tuple(cfg.models) + (mm360.GEODESIC_CAMPOSE,)
+    params = mm360.seq_params(cfg.width, cfg.height, models)
+    pics, refs, epis = _pictures(cfg, 3, dmvr_share=0.3)
+    for _, pus in pics:
+        pus["model"][::7] = mm360.GEODESIC_CAMPOSE
+        assert W.dmvr_flagged(pus).sum() > 100
+    orc = Oracle(params, epis)
+    want = [orc.predict_mixed(cur, pus, refs, cfg.width, cfg.height) for cur, pus in pics]
+    with _ctx(params, epis) as ctx:
+        ctx.set_dmvr(True)
+        ctx.set_plan_ahead(plan_ahead)
+        for poc, (y, cb, cr) in refs.items():
+            ctx.upload_ref(poc, torch.from_numpy(y).cuda(), torch.from_numpy(cb).cuda(), torch.from_numpy(cr).cuda())
+        d_lists = [mm360.pus_to_device(p) for _, p in pics]
+        torch.cuda.synchronize()  # plan-ahead contract: the lists are complete before the calls
+        for rnd in range(2):
+            outs = [_planes(cfg, fill=-1) for _ in pics]
+            ctx.predict_device_multi([(cur, d, *o) for (cur, _), d, o in zip(pics, d_lists, outs)])
+            assert ctx.status() == (mm360.MM_OK, -1)
+            for q, (o, w) in enumerate(zip(outs, want)):
+                for name, t, x in zip(("y", "cb", "cr"), o, w):
+                    got = t.cpu().numpy()
+                    assert np.array_equal(got, x), (rnd, q, plane_mismatch(name, got, x))
+
+
 def test_effective_blocks_end_to_end_vs_oracle():
     """a2 wired end to end: decoded PUs of a C2 picture (merge / mvRefine DMVR PUs, SbTMVP PUs with
     8x8 motion fields, BDOF-split bi PUs) -> the product's mm_derive_effective_blocks -> one

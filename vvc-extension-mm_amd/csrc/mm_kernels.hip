@@ -1820,7 +1820,7 @@ static int ensure_slot_buffers(mm_ctx* c, PlanSlot& S, int n, bool dmvr, int pic
   PlanCaps k;
   pics = std::max(pics, S.pics_ensured);  // (buffers only grow)
   const long area_sb = (long)(c->geo.W / 4) * (c->geo.H / 4) * pics;  // each picture predicts each sample once
-  const int subs = dmvr ? (int)std::min<long>((long)n * 64, (long)c->geo.W * c->geo.H / 128) : 0;
+  const int subs = dmvr ? (int)std::min<long>((long)n * 64, (long)c->geo.W * c->geo.H / 128 * pics) : 0;
   k.pus = n + subs;
   k.jobs = 4 * k.pus;
   k.sb = (int)std::min<long>((long)n * 1024, area_sb);
@@ -2181,9 +2181,7 @@ int mm_pred_device_multi(mm_ctx* c, const mm_pic_job* pics, int n_pics) {
   if (n > INT32_MAX / 2) return MM_ERR_ARG;
   if (n == 0) return MM_OK;
   HIPCHK(c, hipSetDevice(c->device));
-  if (n_pics == 1)
-    return launch_pictures(c, pics, 1, -1, 0, 3, true, c->dmvr);
-  return launch_pictures(c, pics, n_pics, -1, 0, 3, true, false);  // MM-DMVR: one picture per call
+  return launch_pictures(c, pics, n_pics, -1, 0, 3, true, c->dmvr);
 }
 
 int mm_set_dmvr(mm_ctx* c, int on) {
