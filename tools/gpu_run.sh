@@ -48,6 +48,7 @@ for step in "$@"; do
     c4_emulate) run c4_emulate 600 python bench.py --config C4 --c4-emulate ;;
     c4_gloo2) run c4_gloo2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --dist-backend gloo --steps 6 --warmup 2 ;;
     per_model) run per_model 900 bash tools/per_model.sh ;;
+    coherent) run coherent 600 python bench.py --coherent-mv --steps 20 --warmup 3 --no-cpu-baseline --no-mvp --no-c5 --no-dmvr ;;
     ubench) run ubench 300 bash -c "tools/ubench/load_check && tools/ubench/valu_rate2" ;;
     prof_r5) run prof_r5 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r5 -o run --output-format csv -- python3 bench.py --steps 12 --warmup 4 --no-cpu-baseline --no-mvp --no-c5 --no-dmvr ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 12 --warmup 4 --no-cpu-baseline --no-mvp --no-c5 --no-dmvr ;;
