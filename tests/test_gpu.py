@@ -362,8 +362,7 @@ def test_pred_contexts_in_flight_together():
     each context on its own stream with plan-ahead off, calls interleaved without synchronisation,
     every output == the oracle (the contexts share no mutable device state).  Context 0 starts with
     a third of its list, so its buffers grow mid-sequence while context 1's pictures are in flight:
-    growth retires the old buffers behind events on the growing context's own streams (no device-wide
-    synchronisation, DevBuf::ensure)."""
+    growth frees the old buffers in the growing context's own stream order (DevBuf::ensure)."""
     cfg = W.CONFIGS["C2"]
     params = mm360.seq_params(cfg.width, cfg.height, cfg.models)
     full = [W.pu_list(cfg, frame=f) for f in (7, 8)]
@@ -393,6 +392,65 @@ def test_pred_contexts_in_flight_together():
                 for x, t, name in zip(want[id(lists[k][r])], outs[k][r], ("y", "cb", "cr")):
                     got = t.cpu().numpy()
                     assert np.array_equal(got, x), (k, r, plane_mismatch(name, got, x))
+
+
+def test_growth_and_destroy_do_not_wait_for_other_streams():
+    """A context that grows its buffers, synchronises and is destroyed while unrelated work runs on
+    another stream (here ~0.3 s of matrix products on a torch stream) never waits for that work:
+    its buffers come from the stream-ordered pool and are freed in its own stream's order
+    (dev_alloc / dev_free; hipFree would wait for every queue of the device,
+    tools/ubench/free_sync.hip).  The picture it predicts == the oracle."""
+    import time
+    cfg = W.CONFIGS["C2"]
+    params = mm360.seq_params(cfg.width, cfg.height, cfg.models)
+    full = W.pu_list(cfg, frame=7)
+    short = full[: len(full) // 4]
+    refs = {poc: W.ref_planes(cfg.width, cfg.height, poc) for poc in W.REF_POCS}
+    want = Oracle(params, EPI).predict(W.CUR_POC, full, refs, cfg.width, cfg.height)
+    a = torch.randn(4096, 4096, device="cuda", dtype=torch.float32)
+    busy = torch.cuda.Stream()
+
+    def run_busy(n):
+        with torch.cuda.stream(busy):
+            x = a
+            for _ in range(n):
+                x = torch.mm(x, a) * 1e-3
+        return x
+
+    # calibrate the unrelated work (after a warm-up call, which selects the GEMM kernel): ~0.3 s
+    run_busy(2)
+    busy.synchronize()
+    t0 = time.perf_counter()
+    run_busy(20)
+    busy.synchronize()
+    per = (time.perf_counter() - t0) / 20
+    n_busy = min(20000, max(20, int(0.3 / max(per, 1e-5))))
+    ctx = _ctx(params)
+    try:
+        for poc, (y, cb, cr) in refs.items():
+            ctx.upload_ref(poc, torch.from_numpy(y).cuda(), torch.from_numpy(cb).cuda(), torch.from_numpy(cr).cuda())
+        d_short, d_full = mm360.pus_to_device(short), mm360.pus_to_device(full)
+        out = _planes(cfg, 0)
+        ctx.predict_device(W.CUR_POC, d_short, *out)
+        ctx.synchronize()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run_busy(n_busy)  # queued, ~0.3 s
+        ctx.predict_device(W.CUR_POC, d_full, *out)  # grows every plan buffer
+        ctx.synchronize()
+        t_ctx = time.perf_counter() - t0
+        got = [t.cpu().numpy() for t in out]
+    finally:
+        t1 = time.perf_counter()
+        ctx.close()
+        t_destroy = time.perf_counter() - t1
+    busy.synchronize()
+    t_busy = time.perf_counter() - t0
+    assert t_busy > 0.2, t_busy
+    assert t_ctx < 0.5 * t_busy, (t_ctx, t_busy)
+    assert t_destroy < 0.5 * t_busy, (t_destroy, t_busy)
+    for name, g, x in zip(("y", "cb", "cr"), got, want):
+        assert np.array_equal(g, x), plane_mismatch(name, g, x)
 
 
 @pytest.mark.parametrize("plan_ahead", [False, True])

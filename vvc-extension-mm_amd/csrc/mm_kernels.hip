@@ -1067,8 +1067,15 @@ struct RefHost {
 };
 
 struct mm_ctx;
-static void retire_buffer(mm_ctx* c, void* p);
+static hipError_t dev_alloc(mm_ctx* c, void** p, size_t bytes);
+static void dev_free(mm_ctx* c, void* p);
 
+// The buffers that grow with the pictures come from the device's stream-ordered pool
+// (hipMallocAsync / hipFreeAsync on the context stream, dev_alloc / dev_free): hipFree -- and
+// hipFreeAsync of memory hipMalloc returned -- waits for every queue of the device (a busy kernel on
+// another stream held it for the kernel's whole 266 ms, tools/ubench/free_sync.hip), so a context that
+// grew or was destroyed would stall every other context in flight; a pool free is ordered on the
+// context stream only (0.02 ms, its stream done in 0.1 ms beside the same kernel).
 template <typename T>
 struct DevBuf {
   T* p = nullptr;
@@ -1078,23 +1085,22 @@ struct DevBuf {
     if (fresh) *fresh = false;
     if (n <= cap && p) return hipSuccess;
     // Growing replaces a buffer that work still queued on the context's streams may use (the host
-    // runs pictures ahead of the GPU).  Nothing waits here: the old allocation is retired behind
-    // events on the context's streams and freed once they have passed (retire_buffer / reap), so
-    // other contexts and streams of the process never stall on one context's growth.  Buffers only
-    // grow, so this happens a few times per context.
-    if (p) retire_buffer(c, p);
-    p = nullptr;
-    cap = 0;
+    // runs pictures ahead of the GPU): the old allocation is freed in stream order behind that work
+    // (dev_free), nothing waits on the host.  Growth is geometric (x1.5), so a list that creeps up
+    // picture by picture reallocates a few times, not every picture.
     size_t want = std::max<size_t>(n, 1);
-    hipError_t e = hipMalloc(&p, want * sizeof(T));
-    if (e == hipSuccess) {
-      cap = want;
-      if (fresh) *fresh = true;
-    }
-    return e;
+    if (p) want = std::max(want, cap + cap / 2);
+    void* q = nullptr;
+    const hipError_t e = dev_alloc(c, &q, want * sizeof(T));
+    if (e != hipSuccess) return e;
+    if (p) dev_free(c, p);
+    p = static_cast<T*>(q);
+    cap = want;
+    if (fresh) *fresh = true;
+    return hipSuccess;
   }
-  void release() {
-    if (p) (void)hipFree(p);
+  void release(mm_ctx* c) {
+    if (p) dev_free(c, p);
     p = nullptr;
     cap = 0;
   }
@@ -1123,28 +1129,28 @@ struct PlanSlot {
   int pics_ensured = 1;  // pictures per call the sub-block capacity covers (mm_pred_device_multi)
   bool dmvr_ensured = false;
   PlanCaps caps{};
-  void release() {
-    dmvr_sub.release();
-    dmvr_off.release();
-    dmvr_chunk.release();
-    dmvr_setup.release();
-    dmvr_cterms.release();
-    dmvr_mvd.release();
-    dmvr_surv_s.release();
-    dmvr_count.release();
-    dmvr_ccost.release();
-    job_off.release();
-    job_chunk.release();
-    jobs.release();
-    setup.release();
-    blk.release();
-    blkq.release();
-    meta.release();
-    mc_meta.release();
+  void release(mm_ctx* c) {
+    dmvr_sub.release(c);
+    dmvr_off.release(c);
+    dmvr_chunk.release(c);
+    dmvr_setup.release(c);
+    dmvr_cterms.release(c);
+    dmvr_mvd.release(c);
+    dmvr_surv_s.release(c);
+    dmvr_count.release(c);
+    dmvr_ccost.release(c);
+    job_off.release(c);
+    job_chunk.release(c);
+    jobs.release(c);
+    setup.release(c);
+    blk.release(c);
+    blkq.release(c);
+    meta.release(c);
+    mc_meta.release(c);
     for (int l = 0; l < 2; l++) {
-      mc_lpos[l].release();
-      mc_cpos[l].release();
-      for (int k = 0; k < 2; k++) mc_far[l][k].release();
+      mc_lpos[l].release(c);
+      mc_cpos[l].release(c);
+      for (int k = 0; k < 2; k++) mc_far[l][k].release(c);
     }
   }
 };
@@ -1251,52 +1257,39 @@ struct mm_ctx {
   bool call_timing = true;
   bool timed = false;
   hipEvent_t ev_stage[3] = {nullptr, nullptr, nullptr};  // after planning, setup, reprojection
-  // buffers replaced by DevBuf growth, freed once the events recorded on the context's streams at
-  // retirement have completed (reap: mm_synchronize, mm_destroy)
-  struct Retired {
-    void* p;
-    hipEvent_t ev[3];
-  };
-  std::vector<Retired> grave;
+  hipEvent_t ev_mem = nullptr;  // dev_alloc / dev_free fences between the context's streams
 };
 
 static hipStream_t mvp_stream_of(const mm_ctx* c) { return c->mvp_on_own ? c->mvp_stream : c->stream; }
 
-static void retire_buffer(mm_ctx* c, void* p) {
-  mm_ctx::Retired r{p, {nullptr, nullptr, nullptr}};
-  const hipStream_t ss[3] = {c->stream, c->aux, c->mvp_on_own ? c->mvp_stream : nullptr};
-  for (int k = 0; k < 3; k++) {
-    if (k > 0 && !ss[k]) continue;
-    if (hipEventCreateWithFlags(&r.ev[k], hipEventDisableTiming) != hipSuccess ||
-        hipEventRecord(r.ev[k], ss[k]) != hipSuccess) {
-      // cannot fence the old buffer: fall back to draining this context's streams
-      for (int j = 0; j < 3; j++)
-        if (j == 0 || ss[j]) (void)hipStreamSynchronize(ss[j]);
-      break;
-    }
+// `to` waits for the work queued so far on `from` (GPU-side; a null handle is the null stream, which
+// the context stream may be)
+static void order_after(mm_ctx* c, hipStream_t to, hipStream_t from) {
+  if (from == to) return;
+  if (!c->ev_mem && hipEventCreateWithFlags(&c->ev_mem, hipEventDisableTiming) != hipSuccess) {
+    (void)hipStreamSynchronize(from);  // no event: drain `from` instead (this context's stream only)
+    return;
   }
-  c->grave.push_back(r);
+  if (hipEventRecord(c->ev_mem, from) != hipSuccess || hipStreamWaitEvent(to, c->ev_mem, 0) != hipSuccess)
+    (void)hipStreamSynchronize(from);
 }
 
-// Frees the retired buffers whose fences have passed (all of them when `wait`).
-static void reap(mm_ctx* c, bool wait) {
-  std::vector<mm_ctx::Retired> keep;
-  for (auto& r : c->grave) {
-    bool done = true;
-    for (auto e : r.ev)
-      if (e && !wait && hipEventQuery(e) != hipSuccess) done = false;
-    if (!done) {
-      keep.push_back(r);
-      continue;
-    }
-    for (auto e : r.ev)
-      if (e) {
-        (void)hipEventSynchronize(e);
-        (void)hipEventDestroy(e);
-      }
-    (void)hipFree(r.p);
-  }
-  c->grave.swap(keep);
+// A buffer from the stream-ordered pool, usable by work queued after this call on every stream of
+// the context (the auxiliary and MVP streams wait for the allocation's point on the context stream).
+static hipError_t dev_alloc(mm_ctx* c, void** p, size_t bytes) {
+  const hipError_t e = hipMallocAsync(p, bytes, c->stream);
+  if (e != hipSuccess) return e;
+  order_after(c, c->aux, c->stream);
+  if (c->mvp_on_own) order_after(c, c->mvp_stream, c->stream);
+  return hipSuccess;
+}
+
+// Frees a pool buffer once every piece of work queued so far on the context's streams has run: the
+// context stream waits for the auxiliary and MVP streams, then frees in its own order.
+static void dev_free(mm_ctx* c, void* p) {
+  order_after(c, c->stream, c->aux);
+  if (c->mvp_on_own) order_after(c, c->stream, c->mvp_stream);
+  (void)hipFreeAsync(p, c->stream);
 }
 
 static int read_status(mm_ctx* c, int* first_bad);
@@ -1445,9 +1438,9 @@ int mm_create(const mm_seq_params* p, int device, mm_ctx** out_ctx) {
   // MPA frame caches (MVReprojection::init -> MotionPlaneAdaptiveMotionModel::fillCache)
   const int cols = p->width / 4, rows = p->height / 4, n = cols * rows;
   const unsigned mpa_bits = p->active_models & (7u << MPA_FRONT_BACK);
-  if (mpa_bits && (hipMalloc(&c->mpa_px, 3 * (size_t)n * sizeof(float)) != hipSuccess ||
-                   hipMalloc(&c->mpa_py, 3 * (size_t)n * sizeof(float)) != hipSuccess ||
-                   hipMalloc(&c->mpa_vip, 3 * (size_t)n) != hipSuccess)) {
+  if (mpa_bits && (dev_alloc(c, reinterpret_cast<void**>(&c->mpa_px), 3 * (size_t)n * sizeof(float)) != hipSuccess ||
+                   dev_alloc(c, reinterpret_cast<void**>(&c->mpa_py), 3 * (size_t)n * sizeof(float)) != hipSuccess ||
+                   dev_alloc(c, reinterpret_cast<void**>(&c->mpa_vip), 3 * (size_t)n) != hipSuccess)) {
     mm_destroy(c);
     return MM_ERR_HIP;
   }
@@ -1457,7 +1450,7 @@ int mm_create(const mm_seq_params* p, int device, mm_ctx** out_ctx) {
                        rows, c->mpa_px + (size_t)pl * n, c->mpa_py + (size_t)pl * n, c->mpa_vip + (size_t)pl * n);
   }
   // separable toSphere table (MpaCache::trig_col / trig_row): 2 flavours x (cols + rows) pairs
-  if (hipMalloc(&c->trig, (size_t)4 * (cols + rows) * sizeof(float)) != hipSuccess) {
+  if (dev_alloc(c, reinterpret_cast<void**>(&c->trig), (size_t)4 * (cols + rows) * sizeof(float)) != hipSuccess) {
     mm_destroy(c);
     return MM_ERR_HIP;
   }
@@ -1468,7 +1461,7 @@ int mm_create(const mm_seq_params* p, int device, mm_ctx** out_ctx) {
   // atan2f + a sin/cos pair each (profiles/r03_ab_tan_grid.txt)
   if (p->active_models & (1u << TANGENTIAL)) {
     const long nt = 2L * cols * rows;
-    if (hipMalloc(&c->tan_grid, (size_t)nt * sizeof(TanEntry)) != hipSuccess) {
+    if (dev_alloc(c, reinterpret_cast<void**>(&c->tan_grid), (size_t)nt * sizeof(TanEntry)) != hipSuccess) {
       mm_destroy(c);
       return MM_ERR_HIP;
     }
@@ -1493,44 +1486,43 @@ int mm_destroy(mm_ctx* c) {
   if (!c) return MM_ERR_ARG;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
-  if (c->pool) (void)hipFree(c->pool);
-  if (c->trig) (void)hipFree(c->trig);
-  if (c->tan_grid) (void)hipFree(c->tan_grid);
-  if (c->mpa_px) (void)hipFree(c->mpa_px);
-  if (c->mpa_py) (void)hipFree(c->mpa_py);
-  if (c->mpa_vip) (void)hipFree(c->mpa_vip);
-  c->d_jobs.release();
-  c->d_job_off.release();
-  c->d_job_chunk.release();
-  c->d_pu_off.release();
-  c->d_pu_chunk.release();
-  c->d_setup.release();
-  c->d_reproj.release();
-  c->d_pu_in.release();
-  c->d_status.release();
-  for (int k = 0; k < 2; k++) c->slot[k].release();
-  c->d_ged.release();
-  for (auto& kv : c->orgs) (void)hipFree(kv.second.y);
-  c->d_me_blocks.release();
-  c->d_mvp_q.release();
-  c->d_mvp_out.release();
-  c->d_mvp_status.release();
-  c->d_mvp_bins.release();
-  c->d_mvp_local.release();
-  c->d_mvp_perm.release();
+  if (c->aux) (void)hipStreamSynchronize(c->aux);
+  if (c->mvp_on_own) (void)hipStreamSynchronize(c->mvp_stream);
+  for (void* q : {(void*)c->pool, (void*)c->trig, (void*)c->tan_grid, (void*)c->mpa_px, (void*)c->mpa_py,
+                  (void*)c->mpa_vip})
+    if (q) dev_free(c, q);
+  c->d_jobs.release(c);
+  c->d_job_off.release(c);
+  c->d_job_chunk.release(c);
+  c->d_pu_off.release(c);
+  c->d_pu_chunk.release(c);
+  c->d_setup.release(c);
+  c->d_reproj.release(c);
+  c->d_pu_in.release(c);
+  c->d_status.release(c);
+  for (int k = 0; k < 2; k++) c->slot[k].release(c);
+  c->d_ged.release(c);
+  for (auto& kv : c->orgs)
+    if (kv.second.y) dev_free(c, kv.second.y);
+  c->d_me_blocks.release(c);
+  c->d_mvp_q.release(c);
+  c->d_mvp_out.release(c);
+  c->d_mvp_status.release(c);
+  c->d_mvp_bins.release(c);
+  c->d_mvp_local.release(c);
+  c->d_mvp_perm.release(c);
   for (int b = 0; b < 2; b++) {
-    c->d_epi[b].release();
+    c->d_epi[b].release(c);
     if (c->ev_epi_done[b]) (void)hipEventDestroy(c->ev_epi_done[b]);
   }
   if (c->h_epi) (void)hipHostFree(c->h_epi);
   if (c->ev_epi) (void)hipEventDestroy(c->ev_epi);
-  c->d_me_off.release();
-  c->d_me_chunk.release();
+  c->d_me_off.release(c);
+  c->d_me_chunk.release(c);
   for (auto& e : c->ev_stage)
     if (e) (void)hipEventDestroy(e);
-  if (c->aux) (void)hipStreamSynchronize(c->aux);
-  if (c->mvp_on_own) (void)hipStreamSynchronize(c->mvp_stream);
-  reap(c, true);
+  (void)hipStreamSynchronize(c->stream);  // the pool frees above
+  if (c->ev_mem) (void)hipEventDestroy(c->ev_mem);
   if (c->aux) (void)hipStreamDestroy(c->aux);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
@@ -1545,6 +1537,9 @@ int mm_destroy(mm_ctx* c) {
 
 int mm_set_stream(mm_ctx* c, void* s) {
   if (!c) return MM_ERR_ARG;
+  // work queued on the old stream may still use the context's buffers, which are freed and fenced in
+  // the context stream's order from now on
+  (void)hipStreamSynchronize(c->stream);
   c->stream = (hipStream_t)s;
   return MM_OK;
 }
@@ -1554,7 +1549,6 @@ int mm_synchronize(mm_ctx* c) {
   if (!c) return MM_ERR_ARG;
   const int rc = read_status(c, nullptr);
   const int rm = read_mvp_status(c, nullptr);
-  reap(c, false);
   return rc ? rc : rm;
 }
 
@@ -1682,7 +1676,9 @@ static int pad_plane(mm_ctx* c, int16_t* origin, const PlaneLayout& l, int w, in
 }
 
 // A free picture slot of the reference pool; grows the pool (copying the resident pictures) when
-// full.  Growth waits for the context's work so no launch still reads the old allocation.
+// full.  The copy and the old allocation's release are ordered behind the context's queued work on
+// its own streams (dev_free), so no launch still reads the old allocation and nothing waits on the
+// host.
 static int take_pool_slot(mm_ctx* c, int* slot) {
   if (!c->pic_bytes) c->pic_bytes = luma_layout(c).bytes + (c->geo.chroma ? 2 * chroma_layout(c).bytes : 0);
   if (c->pool_free.empty()) {
@@ -1692,12 +1688,11 @@ static int take_pool_slot(mm_ctx* c, int* slot) {
       return fail(c, MM_ERR_ARG, "reference pool full (" + std::to_string(c->pool_cap) + " pictures, < 2 GiB)");
     const int cap = std::min(max_cap, std::max(4, 2 * c->pool_cap));
     char* np = nullptr;
-    HIPCHK(c, hipMalloc(&np, (size_t)cap * c->pic_bytes));
+    HIPCHK(c, dev_alloc(c, reinterpret_cast<void**>(&np), (size_t)cap * c->pic_bytes));
     if (c->pool) {
-      HIPCHK(c, hipStreamSynchronize(c->stream));
-      HIPCHK(c, hipStreamSynchronize(c->aux));
-      HIPCHK(c, hipMemcpy(np, c->pool, (size_t)c->pool_cap * c->pic_bytes, hipMemcpyDeviceToDevice));
-      (void)hipFree(c->pool);
+      order_after(c, c->stream, c->aux);
+      HIPCHK(c, hipMemcpyAsync(np, c->pool, (size_t)c->pool_cap * c->pic_bytes, hipMemcpyDeviceToDevice, c->stream));
+      dev_free(c, c->pool);
     }
     c->pool = np;
     for (int k = cap - 1; k >= c->pool_cap; k--) c->pool_free.push_back(k);
@@ -2249,7 +2244,7 @@ int mm_upload_org(mm_ctx* c, int poc, const int16_t* y, ptrdiff_t sy, int src_de
   RefHost& r = c->orgs[poc];
   if (!r.y) {
     r.stride_y = (c->geo.W + 63) & ~63;
-    HIPCHK(c, hipMalloc(&r.y, (size_t)r.stride_y * c->geo.H * sizeof(int16_t)));
+    HIPCHK(c, dev_alloc(c, reinterpret_cast<void**>(&r.y), (size_t)r.stride_y * c->geo.H * sizeof(int16_t)));
   }
   HIPCHK(c, hipMemcpy2DAsync(r.y, r.stride_y * 2, y, sy * 2, c->geo.W * 2, c->geo.H,
                              src_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->stream));
@@ -2511,19 +2506,20 @@ int mm_filter(mm_ctx* c, int comp, int vertical, const int16_t* src, ptrdiff_t s
   for (int r = 0; r < hh; r++)
     for (int q = 0; q < ww; q++) win[(size_t)r * ww + q] = src[(long)(r - my0) * src_stride + (q - mx0)];
   int16_t *dsrc = nullptr, *ddst = nullptr;
-  HIPCHK(c, hipMalloc(&dsrc, win.size() * 2));
-  hipError_t e = hipMalloc(&ddst, (size_t)w * h * 2);
-  if (e == hipSuccess) e = hipMemcpy(dsrc, win.data(), win.size() * 2, hipMemcpyHostToDevice);
+  HIPCHK(c, dev_alloc(c, reinterpret_cast<void**>(&dsrc), win.size() * 2));
+  hipError_t e = dev_alloc(c, reinterpret_cast<void**>(&ddst), (size_t)w * h * 2);
+  if (e == hipSuccess) e = hipMemcpyAsync(dsrc, win.data(), win.size() * 2, hipMemcpyHostToDevice, c->stream);
   if (e == hipSuccess) {
     hipLaunchKernelGGL(k_filter, dim3((w * h + 255) / 256), dim3(256), 0, c->stream, comp, vertical,
                        dsrc + (size_t)my0 * ww + mx0, ww, ddst, w, w, h, frac, is_first, is_last, c->geo.bd);
     e = hipGetLastError();
   }
   std::vector<int16_t> out((size_t)w * h);
-  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-  if (e == hipSuccess) e = hipMemcpy(out.data(), ddst, out.size() * 2, hipMemcpyDeviceToHost);
-  (void)hipFree(dsrc);
-  if (ddst) (void)hipFree(ddst);
+  if (e == hipSuccess) e = hipMemcpyAsync(out.data(), ddst, out.size() * 2, hipMemcpyDeviceToHost, c->stream);
+  dev_free(c, dsrc);
+  if (ddst) dev_free(c, ddst);
+  const hipError_t es = hipStreamSynchronize(c->stream);  // the copies (pageable host memory) and the frees
+  if (e == hipSuccess) e = es;
   if (e != hipSuccess) return fail(c, MM_ERR_HIP, hipGetErrorString(e));
   for (int r = 0; r < h; r++)
     for (int q = 0; q < w; q++) dst[(long)r * dst_stride + q] = out[(size_t)r * w + q];
