@@ -179,7 +179,10 @@ typedef struct mm_mvp_query {
 
 typedef struct mm_ctx mm_ctx;
 
-/* Lifecycle */
+/* Lifecycle.  A context's device buffers come from the device's stream-ordered memory pool and are
+ * freed in its own streams' order: growing them, mm_synchronize and mm_destroy never wait for other
+ * contexts' or the application's queues.  mm_set_stream first waits for the work queued on the
+ * context's previous stream. */
 int mm_create(const mm_seq_params* params, int device, mm_ctx** out_ctx);
 int mm_destroy(mm_ctx* ctx);
 int mm_set_stream(mm_ctx* ctx, void* hip_stream);     /* hipStream_t; NULL = default stream */
