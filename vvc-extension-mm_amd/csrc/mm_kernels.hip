@@ -413,8 +413,11 @@ __global__ void __launch_bounds__(256) k_reproj_dev(SeqConst sc, const PlanMeta*
 // neighbouring PUs share in its own L2.  Every workgroup stages the tap tables and the reference
 // table in LDS once for all its blocks.
 static_assert(N_BANDS == 8, "one band per XCD");
+#ifndef MM_MC_WAVES
+#define MM_MC_WAVES 3
+#endif
 template <bool UNI_HP>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k_mc_dev(Geometry geo, const PlanMeta* __restrict__ meta, McRec mc,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MM_MC_WAVES))) k_mc_dev(Geometry geo, const PlanMeta* __restrict__ meta, McRec mc,
                                                 const PicTables t, const DstPlanes dst) {
   const int band = blockIdx.x & 7, stride = (int)(gridDim.x >> 3) * 256;
   const int n_sb = meta->n_sb;  // (second guard: a band never reaches past the plan's sub-blocks)
