@@ -468,6 +468,9 @@ constexpr bool PLAN_AHEAD_HOST_WAIT = MM_PLAN_HOST_WAIT;
 #ifndef MM_REPROJ_AHEAD
 #define MM_REPROJ_AHEAD 1  // see launch_stripe
 #endif
+#ifndef MM_REPROJ_LDS
+#define MM_REPROJ_LDS 0  // A/B knob: dynamic LDS per k_reproj_dev workgroup, to cap its workgroups per CU
+#endif
 
 // --------------------------------------------------------------------------------------------
 // Encoder candidate windows (mm_sad_window, mm_me.h)
@@ -1939,7 +1942,7 @@ static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables
                           S.setup.p);
   };
   auto reproj = [&](hipStream_t s_, hipEvent_t stop) {
-    hipExtLaunchKernelGGL(k_reproj_dev, dim3(gr), dim3(256), 0, s_, nullptr, stop, 0, c->sc, S.meta.p, S.jobs.p,
+    hipExtLaunchKernelGGL(k_reproj_dev, dim3(gr), dim3(256), MM_REPROJ_LDS, s_, nullptr, stop, 0, c->sc, S.meta.p, S.jobs.p,
                           S.job_off.p, S.job_chunk.p, S.setup.p, make_cache(c), mc);
   };
   if (back) {
