@@ -240,7 +240,8 @@ int mm_pred(mm_ctx* ctx, int cur_poc, const mm_pu_desc* pus, int n, int16_t* dst
  * reprojection, interpolation and averaging -- as one asynchronous launch sequence on the
  * context stream, with no host synchronisation.  Descriptor validation (the reference's CHECKs:
  * geometry, model, reference, epipole) happens on the device; failing PUs are skipped and the
- * lowest failing PU's code is reported by the next mm_pred_status / mm_synchronize. */
+ * lowest failing PU's code is reported by mm_pred_status / mm_synchronize -- for the LAST
+ * device-planned call: a decoder that wants every picture's status reads it before the next call. */
 int mm_pred_device(mm_ctx* ctx, int cur_poc, const mm_pu_desc* d_pus, int n, int16_t* dst_y,
                    ptrdiff_t dst_stride_y, int16_t* dst_cb, int16_t* dst_cr,
                    ptrdiff_t dst_stride_c);
@@ -414,21 +415,19 @@ int mm_set_stripes(mm_ctx* ctx, int stripes);
  * a surviving sub-PU never leave the wave that searches it (round 4: 0.9 GB per context). */
 int mm_set_dmvr(mm_ctx* ctx, int on);
 
-/* Plan-ahead for mm_pred_device (default off): a picture's planning and setup kernels run on the
- * internal auxiliary stream, gated only by the completion of the interpolation kernel of the call
- * TWO back (the last user of the plan buffers they overwrite), so they overlap the previous
- * picture's reprojection and interpolation; the reprojection and interpolation stay on the
- * context stream after them.  Contract while on: the device PU list of call N is complete before
- * call N is issued AND is not written by device work that could still run after call N-2's
- * interpolation -- i.e. it is written by the host, by device work the caller has synchronised, or
- * by work enqueued on the context stream before call N-2 was issued.  A list written on the
- * context stream between calls N-2 and N is NOT ordered before call N's planning (synchronise
- * first, or keep plan-ahead off).  mm_pred / mm_pred_prepare + mm_pred_run copy and synchronise, so
- * they always qualify.  Applies to one-stripe calls without stage timing; results do not depend
- * on the setting.  While on, each call returns only after its picture's planning has run on the
- * device (it waits for the interpolation of the call two back), so the host stays about one
- * picture ahead of the GPU.  (No reference counterpart: VTM decodes a picture's PUs inside its
- * own CTU loop.) */
+/* Plan-ahead for mm_pred_device (default off): a picture's planning, setup and reprojection
+ * kernels run on the internal auxiliary stream, gated only by the completion of the interpolation
+ * kernel of the call TWO back (the last user of the plan buffers they overwrite), so they overlap
+ * the previous picture's interpolation; the interpolation stays on the context stream, which waits
+ * for them on the device, and a call returns without waiting for the GPU.  Contract while on: the
+ * device PU list of call N is complete before call N is issued AND is not written by device work
+ * that could still run after call N-2's interpolation -- i.e. it is written by the host, by device
+ * work the caller has synchronised, or by work enqueued on the context stream before call N-2 was
+ * issued.  A list written on the context stream between calls N-2 and N is NOT ordered before call
+ * N's planning (synchronise first, or keep plan-ahead off).  mm_pred / mm_pred_prepare +
+ * mm_pred_run copy and synchronise, so they always qualify.  Applies to one-stripe calls without
+ * stage timing; results do not depend on the setting.  (No reference counterpart: VTM decodes a
+ * picture's PUs inside its own CTU loop.) */
 int mm_set_plan_ahead(mm_ctx* ctx, int on);
 
 #ifdef __cplusplus
