@@ -265,6 +265,10 @@ def bench_pictures(args, cfg, params, rank, world, local, dist):
                               [(cur, -1, W.GED_EPIPOLE_Q24) for cur, _, _ in pictures])
         mvp["in_loop"] = mvp_in_loop(args, ctx, cfg, pictures, d_pus, outs, area)
 
+    multi = None
+    if args.config == "C3" and world == 1 and args.dmvr_share == 0 and args.uniform_model is None and P_ >= 2:
+        multi = multi_picture_record(args, ctx, pictures, d_pus, area, got)
+
     cpu, bit_exact, mism = None, None, None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # pictures the timed steps predicted (all of them unless --steps < --pictures)
@@ -297,10 +301,43 @@ def bench_pictures(args, cfg, params, rank, world, local, dist):
         }
         if mvp is not None:
             line["mvp"] = mvp
+        if multi is not None:
+            line["multi_picture"] = multi
         ctx.close()
         return line
     ctx.close()
     return None
+
+
+def multi_picture_record(args, ctx, pictures, d_pus, area, verified):
+    """Beside the headline (not `value`): the same rotating C3 pictures, k = 2 and 4 at a time in
+    ONE launch chain (mm_pred_device_multi) -- what a decoder gets for pictures that do not reference
+    each other (the leaves of an RA temporal layer, cfg/encoder_randomaccess_vtm.cfg:20-51).  Every
+    output equals the headline's own timed output of the same picture (which the bench checks
+    against the oracle)."""
+    P_ = len(pictures)
+    out = {}
+    for k in (2, 4):
+        if k > P_:
+            continue
+        outs = [planes(W.CONFIGS[args.config]) for _ in range(P_)]
+
+        def step(s, k=k, outs=outs):
+            f0 = (s * k) % P_
+            ctx.predict_device_multi([(pictures[(f0 + q) % P_][0], d_pus[(f0 + q) % P_], *outs[(f0 + q) % P_])
+                                      for q in range(k)])
+
+        steps = max(2, args.steps // k)
+        t = timed(steps, max(1, args.warmup // k), step, None)
+        ctx.synchronize()
+        same = all(np.array_equal(a.cpu().numpy(), b) for f in range(P_) for a, b in zip(outs[f], verified[f]))
+        n_pic = steps * k
+        px = sum(area[(s * k + q) % P_] for s in range(steps) for q in range(k))
+        out[str(k)] = {"ms_per_picture": round(t / n_pic * 1e3, 4), "value": round(px / t / 1e6, 2),
+                       "equals_headline_output": bool(same)}
+    out["note"] = ("k independent C3 pictures per mm_pred_device_multi call (one launch chain), plan-ahead as set; "
+                   "not part of value: the headline predicts one picture per call")
+    return out
 
 
 def dmvr_record(args, cfg, params, share=0.3, steps=12, warmup=3, correlated=False):
