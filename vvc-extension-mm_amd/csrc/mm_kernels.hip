@@ -718,7 +718,8 @@ __device__ __forceinline__ void wave_lds_sync() {
 #define MM_DMVR_SEARCH_WAVES 4  // waves per SIMD = workgroups per CU (LDS): 128 VGPRs, spill-free
 #endif
 constexpr int DMVR_SEARCH_GRID = 256 * MM_DMVR_SEARCH_WAVES;  // grid-stride over the survivors
-static_assert(MM_DMVR_SEARCH_WAVES * (sizeof(DmvrWaveLds) * DMVR_WAVES + sizeof(PackedTaps) + 64 * 36) <= 160 * 1024,
+static_assert(MM_DMVR_SEARCH_WAVES * (sizeof(DmvrWaveLds) * DMVR_WAVES + sizeof(PackedTaps) + (3 + MAX_SLOTS) * sizeof(M3)) <=
+                  160 * 1024,
               "the workgroups of one CU fit its LDS");
 __global__ void __launch_bounds__(DMVR_SEARCH_WG) __attribute__((amdgpu_waves_per_eu(MM_DMVR_SEARCH_WAVES))) k_dmvr_search_dev(
     SeqConst sc, Geometry geo, const SubPuDev* __restrict__ sp, MpaCache cache, const PicTables t, DmvrWork w,
