@@ -361,8 +361,8 @@ def dmvr_record(args, cfg, params, share=0.3, steps=12, warmup=3, correlated=Fal
             "bit_exact": line["bit_exact"], "mismatching_samples": line["mismatching_samples"],
             "bit_exact_sample": f"the {min(a.pictures, steps)} timed pictures vs the oracle",
             "cpu_all_cores_mpix_s": (cpu.get("all_cores") or {}).get("value"),
-            "note": "stages_ms.setup holds the DMVR kernels (setups, centre costs, survivors' positions and "
-                    "search) and k_setup_dev; not part of value"}
+            "note": "stages_ms.setup holds the DMVR kernels (centre terms and setups, centre costs, the "
+                    "survivors' search) and k_setup_dev; not part of value"}
 
 
 def mvp_per_picture(ctx, cfg, n_pus, params, epipoles, reps=10):

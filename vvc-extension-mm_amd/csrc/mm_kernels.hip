@@ -559,7 +559,7 @@ constexpr int DMVR_GRID = 2048;  // workgroups of 256 of the grid-stride setup k
 
 // The picture's DMVR survivors (sub-PUs whose centre cost does not end the search)
 struct DmvrWork {
-  unsigned long long* count;  // survivors << 32 (k_dmvr_centre_dev)
+  unsigned* count;            // survivors (k_dmvr_centre_dev)
   uint32_t* ccost;            // centre cost (xDMVRCost at the merge MVs) per sub-PU
   int* surv_s;                // sub-PU of survivor k
   const CentreTerms* cterms;  // centre terms [2 s + l] (k_dmvr_setup_dev)
@@ -571,11 +571,11 @@ struct DmvrWork {
 __global__ void __launch_bounds__(256) k_dmvr_setup_dev(SeqConst sc, const PlanMeta* __restrict__ meta,
                                                         const SubPuDev* __restrict__ sp, const PicTables t,
                                                         BlockSetup* __restrict__ out, CentreTerms* __restrict__ cterms,
-                                                        unsigned long long* __restrict__ count) {
+                                                        unsigned* __restrict__ count) {
   __shared__ M3 s_ged[3 + MAX_SLOTS];  // indexed per lane: staged by stage_arg_words
   stage_arg_words<sizeof(s_ged) / 4>(reinterpret_cast<const uint32_t*>(t.ged), reinterpret_cast<uint32_t*>(s_ged));
   __syncthreads();
-  if (blockIdx.x == 0 && threadIdx.x == 0) *count = 0ull;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *count = 0u;
   const int n_jobs = meta->n_sub * 2;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n_jobs; i += gridDim.x * blockDim.x)
     dmvr_centre_setup_thread(i, sc, sp, s_ged, out, cterms);
@@ -585,10 +585,10 @@ __global__ void __launch_bounds__(256) k_dmvr_setup_dev(SeqConst sc, const PlanM
 // 2 e + l list l of luma 4x4 sub-block e -- its position at the merge MV and rows 0 and 2 of its
 // 14-bit prediction; the L0 lane takes its partner's L1 rows by shuffle for the SAD, summed over
 // the 32 lanes.  minCost = cost - cost/4 < dx*dy ends the search: the sub-PU keeps its merge MVs
-// (dmvr_apply with a zero delta).  Otherwise it joins the survivor list with 2 x 24 x n position
-// items, allocated for the workgroup's survivors together by one atomic (a counter bumped per
-// sub-PU serialised ~14 K device-scope atomics, ~100 µs; a separate one-workgroup scan kernel took
-// 25 µs).  The list order varies from run to run; each survivor decides alone, so results do not.
+// (dmvr_apply with a zero delta).  Otherwise it joins the survivor list, whose entries the
+// workgroup's survivors take together with one atomic (a counter bumped per sub-PU serialised ~14 K
+// device-scope atomics, ~100 µs; a separate one-workgroup scan kernel took 25 µs).  The list order
+// varies from run to run; each survivor decides alone, so results do not.
 __global__ void __launch_bounds__(256) k_dmvr_centre_dev(SeqConst sc, Geometry geo, const PlanMeta* __restrict__ meta,
                                                          const SubPuDev* __restrict__ sp,
                                                          const BlockSetup* __restrict__ setups, MpaCache cache,
@@ -597,12 +597,12 @@ __global__ void __launch_bounds__(256) k_dmvr_centre_dev(SeqConst sc, Geometry g
 #if defined(__HIP_DEVICE_COMPILE__)  // device-only filter paths (mm_filter.h predict_rows02, PtrRows)
   __shared__ PackedTaps s_taps;
   __shared__ RefDev s_ref[MAX_SLOTS];  // indexed per lane: staged by stage_ref_table
-  __shared__ int s_items[8], s_pre[8], s_base[2];
+  __shared__ int s_surv[8], s_pre[8], s_base;
   const int tid = threadIdx.x;
   if (tid < sizeof(PackedTaps) / 16)
     lds_put(reinterpret_cast<uint4*>(&s_taps)[tid], reinterpret_cast<const uint4*>(&c_packed_taps)[tid], make_uint4(~0u, ~0u, ~0u, ~0u));
   stage_ref_table<MAX_SLOTS>(t.pool_slot4, t.pool, s_ref);
-  if (tid < 8) lds_put(s_items[tid], 0, 0);
+  if (tid < 8) lds_put(s_surv[tid], 0, 0);
   __syncthreads();
   const int n_sub = meta->n_sub;
   const RefPool pool = t.pool;
@@ -633,35 +633,28 @@ __global__ void __launch_bounds__(256) k_dmvr_centre_dev(SeqConst sc, Geometry g
     v = l ? 0u : v;  // each pair counted once
 #pragma unroll
     for (int d = 1; d < 32; d <<= 1) v += __shfl_xor(v, d);
-    // survivors of this workgroup's 8 sub-PUs: one 64-bit atomic per workgroup allocates their
-    // survivor indices and position items together (so item bases grow with the index)
+    // survivors of this workgroup's 8 sub-PUs: one atomic per workgroup allocates their list entries
     const int slot = tid >> 5;
-    int items = 0;
+    int survives = 0;
     if (s < n_sub && (g & 31) == 0) {
       w.ccost[s] = v;
-      const bool survives = v - (v >> 2) >= (uint32_t)(u.w * u.h);
-      items = survives ? 2 * (N_OFF - 1) * u.n : 0;
+      survives = v - (v >> 2) >= (uint32_t)(u.w * u.h) ? 1 : 0;
       if (!survives) dmvr_apply(s, u, 0, 0, jobs, mvd);  // notZeroCost = false: no refinement (:2520-2525)
-      lds_put(s_items[slot], items, 0);
+      lds_put(s_surv[slot], survives, 0);
     }
     __syncthreads();
     if (tid == 0) {
-      int ni = 0, ns = 0;
+      int ns = 0;
 #pragma unroll
       for (int k = 0; k < 8; k++) {
-        const int it = (base + 32 * k < n_sub * 32) ? s_items[k] : 0;
-        lds_put(s_pre[k], (ns << 20) | ni, 0);  // survivors before, items before (< 2^20 per workgroup)
-        ni += it;
-        ns += it ? 1 : 0;
+        lds_put(s_pre[k], ns, 0);  // survivors before sub-PU k of the workgroup
+        ns += (base + 32 * k < n_sub * 32) ? s_surv[k] : 0;
       }
-      unsigned long long old = 0;
-      if (ns) old = atomicAdd(w.count, ((unsigned long long)ns << 32) | (unsigned long long)ni);
-      lds_put(s_base[0], (int)(old >> 32), 0);
-      lds_put(s_base[1], (int)(old & 0xffffffffull), 0);
+      lds_put(s_base, ns ? (int)atomicAdd(w.count, (unsigned)ns) : 0, 0);
     }
     __syncthreads();
-    if (items) w.surv_s[s_base[0] + (s_pre[slot] >> 20)] = s;
-    __syncthreads();  // s_items / s_pre / s_base reused by the next iteration
+    if (survives) w.surv_s[s_base + s_pre[slot]] = s;
+    __syncthreads();  // s_surv / s_pre / s_base reused by the next iteration
   }
 #endif
 }
@@ -736,7 +729,7 @@ __global__ void __launch_bounds__(DMVR_SEARCH_WG) __attribute__((amdgpu_waves_pe
     lds_put(reinterpret_cast<uint4*>(&s_taps)[tid], reinterpret_cast<const uint4*>(&c_packed_taps)[tid], make_uint4(~0u, ~0u, ~0u, ~0u));
   stage_arg_words<sizeof(s_ged) / 4>(reinterpret_cast<const uint32_t*>(t.ged), reinterpret_cast<uint32_t*>(s_ged));
   __syncthreads();  // s_taps, s_ged: the only LDS the waves share
-  const int n_surv = (int)(*w.count >> 32);
+  const int n_surv = (int)*w.count;
   const RefPool pool = t.pool;
   for (int k = blockIdx.x * DMVR_WAVES + wv; k < n_surv; k += gridDim.x * DMVR_WAVES) {
     const int s = w.surv_s[k];
@@ -1130,7 +1123,7 @@ struct PlanSlot {
   DevBuf<BlockSetup> dmvr_setup;
   DevBuf<CentreTerms> dmvr_cterms;
   DevBuf<int> dmvr_mvd, dmvr_surv_s;
-  DevBuf<unsigned long long> dmvr_count;
+  DevBuf<unsigned> dmvr_count;
   DevBuf<uint32_t> dmvr_ccost;
   int n_ensured = 0;  // largest stripe size the buffers were sized for (they only grow)
   int pics_ensured = 1;  // pictures per call the sub-block capacity covers (mm_pred_device_multi)
