@@ -266,7 +266,8 @@ def bench_pictures(args, cfg, params, rank, world, local, dist):
         mvp["in_loop"] = mvp_in_loop(args, ctx, cfg, pictures, d_pus, outs, area)
 
     multi = None
-    if args.config == "C3" and world == 1 and args.dmvr_share == 0 and args.uniform_model is None and P_ >= 2:
+    if (args.config == "C3" and world == 1 and args.dmvr_share == 0 and args.uniform_model is None and P_ >= 2
+            and not args.no_multi):
         multi = multi_picture_record(args, ctx, pictures, d_pus, area, got)
 
     cpu, bit_exact, mism = None, None, None
@@ -875,6 +876,8 @@ def main():
     ap.add_argument("--no-mvp", action="store_true", help="C3: skip the MM-MVP figure beside the line")
     ap.add_argument("--no-c5", action="store_true", help="C3: skip the C5 (encoder ME) sub-record beside the line")
     ap.add_argument("--no-dmvr", action="store_true", help="C3: skip the MM-DMVR sub-record beside the line")
+    ap.add_argument("--no-multi", action="store_true",
+                    help="C3: skip the multi_picture sub-record (k pictures per launch) beside the line")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="length of the one-thread CPU baseline sample")
     ap.add_argument("--kernel-steps", type=int, default=8, help="extra steps timed per launch with HIP events")
     ap.add_argument("--lib", default=None, help="alternative build of libmm360.so (A/B experiments)")

@@ -48,20 +48,20 @@ for step in "$@"; do
     c4_emulate) run c4_emulate 600 python bench.py --config C4 --c4-emulate ;;
     c4_gloo2) run c4_gloo2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --dist-backend gloo --steps 6 --warmup 2 ;;
     per_model) run per_model 900 bash tools/per_model.sh ;;
-    coherent) run coherent 600 python bench.py --coherent-mv --steps 20 --warmup 3 --no-cpu-baseline --no-mvp --no-c5 --no-dmvr ;;
+    coherent) run coherent 600 python bench.py --coherent-mv --steps 20 --warmup 3 --no-cpu-baseline --no-mvp --no-c5 --no-dmvr --no-multi ;;
     ubench) run ubench 300 bash -c "tools/ubench/load_check && tools/ubench/valu_rate2" ;;
-    prof_r5) run prof_r5 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r5 -o run --output-format csv -- python3 bench.py --steps 12 --warmup 4 --no-cpu-baseline --no-mvp --no-c5 --no-dmvr ;;
-    prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 12 --warmup 4 --no-cpu-baseline --no-mvp --no-c5 --no-dmvr ;;
-    pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 --no-mvp --no-c5 --no-dmvr ;;
-    pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 --no-mvp --no-c5 --no-dmvr ;;
-    pmc_valu) run pmc_valu 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES -d gpurun_out/pmc_valu -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 --no-mvp --no-c5 --no-dmvr ;;
+    prof_r5) run prof_r5 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r5 -o run --output-format csv -- python3 bench.py --steps 12 --warmup 4 --no-cpu-baseline --no-mvp --no-c5 --no-dmvr --no-multi ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 12 --warmup 4 --no-cpu-baseline --no-mvp --no-c5 --no-dmvr --no-multi ;;
+    pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 --no-mvp --no-c5 --no-dmvr --no-multi ;;
+    pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 --no-mvp --no-c5 --no-dmvr --no-multi ;;
+    pmc_valu) run pmc_valu 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES -d gpurun_out/pmc_valu -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 --no-mvp --no-c5 --no-dmvr --no-multi ;;
     counters) run counters 300 rocprofv3 -L ;;
     pmc_c5) run pmc_c5 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES GRBM_GUI_ACTIVE -d gpurun_out/pmc_c5 -o run --output-format csv -- python3 bench.py --config C5 --steps 2 --warmup 1 --no-cpu-baseline ;;
-    pmc_mem) run pmc_mem 600 rocprofv3 --pmc TA_BUSY_avr TA_BUSY_max TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum -d gpurun_out/pmc_mem -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 --no-mvp --no-c5 --no-dmvr ;;
-    pmc_sq) run pmc_sq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU -d gpurun_out/pmc_sq -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 --no-mvp --no-c5 --no-dmvr ;;
+    pmc_mem) run pmc_mem 600 rocprofv3 --pmc TA_BUSY_avr TA_BUSY_max TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum -d gpurun_out/pmc_mem -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 --no-mvp --no-c5 --no-dmvr --no-multi ;;
+    pmc_sq) run pmc_sq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU -d gpurun_out/pmc_sq -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 --no-mvp --no-c5 --no-dmvr --no-multi ;;
     pmc=*)  # pmc=<tag>=<counter,counter,...>: one rocprofv3 --pmc pass over a short bench run
       tag=$(echo "$step" | cut -d= -f2); ctrs=$(echo "$step" | cut -d= -f3 | tr ',' ' ')
-      run "pmc_$tag" 600 rocprofv3 --pmc $ctrs -d "gpurun_out/pmc_$tag" -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 --no-mvp --no-c5 --no-dmvr ;;
+      run "pmc_$tag" 600 rocprofv3 --pmc $ctrs -d "gpurun_out/pmc_$tag" -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 --no-mvp --no-c5 --no-dmvr --no-multi ;;
     pmcd=*)  # pmcd=<tag>=<counter,...>: one rocprofv3 --pmc pass over a short C3 run with a 30 % MM-DMVR share
       tag=$(echo "$step" | cut -d= -f2); ctrs=$(echo "$step" | cut -d= -f3 | tr ',' ' ')
       run "pmcd_$tag" 600 rocprofv3 --pmc $ctrs -d "gpurun_out/pmcd_$tag" -o run --output-format csv -- python3 bench.py --dmvr-share 0.3 --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 --no-mvp --no-c5 ;;
