@@ -730,6 +730,16 @@ def bench_c4_emulate(args, cfg, params):
             cm.synchronize()
             multi[n][k] = round(t / args.steps / k * 1e3, 4)
     cm.close()
+    # the RA loop with the leaves predicted two at a time (bench_c4's line at N > 1), modelled: each
+    # rank's batch costs its single-stripe time x rank 0's measured ratio of two-in-one-chain to one
+    for n in (4, 8):
+        ratio = multi[n][2] / multi[n][1]
+        e = out["n"][n]
+        mc = e["mc_ms"]
+        for k, a in (("ring", e["allgather_ms"]["ring"]), ("mesh", e["allgather_ms"]["mesh"])):
+            v = round(G.schedule(64, mc, a, "ra32", batch_ms={2: mc * ratio})["ms_per_picture"], 4)
+            e["pred_ms_per_picture"][f"ra32_batched_{k}"] = v
+            e["pred_mpix_s"][f"ra32_batched_{k}"] = round(area / (v * 1e-3) / 1e6, 1)
     out["multi_picture_stripes"] = {
         "ms_per_stripe": multi,
         "note": "rank 0's stripe of k independent pictures predicted by ONE context in ONE launch chain per "

@@ -225,6 +225,19 @@ def test_schedule_model():
         slow_all = G.schedule(64, 0.1, 1.0, g, gather_all=True)  # all-gather bound
         slow_ref = G.schedule(64, 0.1, 1.0, g)
         assert slow_all["ms_per_picture"] >= 1.0 and 0.5 <= slow_ref["ms_per_picture"] <= 0.61
+        # batched leaves (the same grouping as DependencyLoop.next_batch): with a batch of two at the
+        # single-picture cost per picture nothing changes; cheaper batches cut only the leaves' MC
+        same = G.schedule(64, 1.0, 0.0, g, batch_ms={2: 1.0})
+        assert abs(same["ms_per_picture"] - 1.0) < 1e-9
+        cheap = G.schedule(64, 1.0, 0.0, g, batch_ms={2: 0.5})["ms_per_picture"]
+        loop = G.DependencyLoop(g, 4, None, None, None)
+        n_batched = 0
+        while loop.k < 64:
+            b = loop.next_batch(2)
+            n_batched += len(b) if len(b) == 2 else 0
+            loop.k += len(b)
+        assert n_batched > 0
+        assert abs(cheap - (64 - 0.5 * n_batched) / 64) < 1e-9, (cheap, n_batched)
 
 
 @pytest.mark.parametrize("batch", [1, 2])

@@ -98,24 +98,36 @@ def is_referenced(poc: int, gop: str = "ra32") -> bool:
 
 
 def schedule(n_pictures: int, mc_ms: float, allgather_ms: float, gop: str = "ra32",
-             gather_all: bool = False) -> Dict[str, float]:
+             gather_all: bool = False, batch_ms: Dict[int, float] = None) -> Dict[str, float]:
     """Modelled per-picture time of the CTU-row-sharded C4 loop: picture k's MC starts when the
     GPUs are free (picture k-1's MC is done) and the all-gathers of all its references have
     landed; a referenced picture (every picture with gather_all) is all-gathered after its MC, one
-    all-gather at a time on the links (RCCL's stream serialises them).  n_pictures should be a
-    whole number of GOPs."""
+    all-gather at a time on the links (RCCL's stream serialises them).  batch_ms {k: ms per picture}
+    (k >= 2): consecutive decode-order pictures none of which references another (DependencyLoop.
+    next_batch, up to max(batch_ms) of them) are predicted together at that per-picture time, once
+    all their references have landed.  n_pictures should be a whole number of GOPs."""
     seq = decode_sequence(n_pictures, gop)
+    max_pics = max(batch_ms) if batch_ms else 1
     landed: Dict[int, float] = {}
     t_mc = 0.0
     link = 0.0
     stall = 0.0
-    for poc, _, refs in seq:
-        ready = max([t_mc] + [landed.get(r, 0.0) for r in refs])
+    i = 0
+    while i < len(seq):
+        batch = [seq[i]]
+        while (len(batch) < max_pics and i + len(batch) < len(seq)
+               and not any(r == p for r in seq[i + len(batch)][2] for p, _, _ in batch)):
+            batch.append(seq[i + len(batch)])
+        k = len(batch)
+        per = mc_ms if k == 1 else batch_ms[k]
+        ready = max([t_mc] + [landed.get(r, 0.0) for _, _, refs in batch for r in refs])
         stall += ready - t_mc
-        t_mc = ready + mc_ms
-        if gather_all or is_referenced(poc, gop):
-            link = max(t_mc, link) + allgather_ms
-            landed[poc] = link
+        t_mc = ready + k * per
+        for poc, _, _ in batch:
+            if gather_all or is_referenced(poc, gop):
+                link = max(t_mc, link) + allgather_ms
+                landed[poc] = link
+        i += k
     total = max(t_mc, link)
     return {"ms_per_picture": total / n_pictures, "stall_ms_per_picture": stall / n_pictures}
 
