@@ -4,8 +4,8 @@
 //
 // Builds a 256x128 ERP sequence context with the MPA models, uploads two synthetic reference
 // pictures, reprojects one block (MVReprojection call shape) and predicts a picture's PU list
-// twice -- host list (mm_pred) and device-resident list (mm_pred_device) -- and checks that both
-// predictions agree.  Exit 0 and "OK" on success; exit 2 when no HIP device is present.
+// four times -- host list (mm_pred), device-resident list (mm_pred_device) and two pictures in one
+// launch chain (mm_pred_device_multi) -- and checks that all predictions agree.  Exit 0 and "OK" on success; exit 2 when no HIP device is present.
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -55,8 +55,8 @@ int main() {
         const int model[2] = {MM_MPA_FRONT_BACK + (bx / 16) % 3, MM_MPA_TOP_BOTTOM};
         pred.addPU(bx, by, 16, 16, mv, ref, model);
       }
-    int16_t *dy[2], *dc[2][2];
-    for (int k = 0; k < 2; k++) {
+    int16_t *dy[4], *dc[4][2];
+    for (int k = 0; k < 4; k++) {
       if (hipMalloc(&dy[k], W * H * 2) != hipSuccess || hipMalloc(&dc[k][0], W * H / 2) != hipSuccess ||
           hipMalloc(&dc[k][1], W * H / 2) != hipSuccess)
         return 1;
@@ -72,21 +72,27 @@ int main() {
     pred.predictPictureDevice(8, d_pus, (int)n, dy[1], W, dc[1][0], dc[1][1], W / 2);
     ctx.synchronize();
 
+    // the same list twice in ONE launch chain (two independent pictures, mm_pred_device_multi)
+    pred.predictPicturesDevice({mm_pic_job{8, d_pus, (int32_t)n, dy[2], W, dc[2][0], dc[2][1], W / 2},
+                                mm_pic_job{8, d_pus, (int32_t)n, dy[3], W, dc[3][0], dc[3][1], W / 2}});
+    ctx.synchronize();
+
     std::vector<int16_t> a(W * H), b(W * H);
     if (hipMemcpy(a.data(), dy[0], W * H * 2, hipMemcpyDeviceToHost) != hipSuccess) return 1;
-    if (hipMemcpy(b.data(), dy[1], W * H * 2, hipMemcpyDeviceToHost) != hipSuccess) return 1;
     long sum = 0;
-    for (int k = 0; k < W * H; k++) {
-      if (a[k] != b[k]) {
-        std::printf("MISMATCH at %d\n", k);
-        return 1;
-      }
-      sum += a[k];
+    for (int q = 1; q < 4; q++) {
+      if (hipMemcpy(b.data(), dy[q], W * H * 2, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+      for (int k = 0; k < W * H; k++)
+        if (a[k] != b[k]) {
+          std::printf("MISMATCH picture %d at %d\n", q, k);
+          return 1;
+        }
     }
+    for (int k = 0; k < W * H; k++) sum += a[k];
     std::printf("OK reproject(0,0)=(%d,%d) luma-sum=%ld\n", f.X(0, 0), f.Y(0, 0), sum);
     std::printf("MVP host per-call latency %.3f us (%d calls of motionVectorInDesiredMotionModel, MPA models, "
                 "checksum %ld)\n", us, n_calls, mv_sum);
-    for (int k = 0; k < 2; k++) {
+    for (int k = 0; k < 4; k++) {
       (void)hipFree(dy[k]);
       (void)hipFree(dc[k][0]);
       (void)hipFree(dc[k][1]);

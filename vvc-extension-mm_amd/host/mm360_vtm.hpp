@@ -254,6 +254,13 @@ class InterPredictionMM {
     check(ctx_->get(), mm_pred_device(ctx_->get(), curPOC, devPUs, n, dstY, strideY, dstCb, dstCr, strideC),
           "mm_pred_device");
   }
+  // Several pictures that do not reference each other (the leaves of one RA temporal layer) in one
+  // launch chain, each with its own current POC, device PU list and destination planes; asynchronous
+  // like predictPictureDevice.  At most MM_MAX_PICS pictures.
+  void predictPicturesDevice(const std::vector<mm_pic_job>& pictures) {
+    check(ctx_->get(), mm_pred_device_multi(ctx_->get(), pictures.data(), (int)pictures.size()),
+          "mm_pred_device_multi");
+  }
 
  private:
   Context* ctx_;
