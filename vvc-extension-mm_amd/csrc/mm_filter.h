@@ -13,14 +13,14 @@
 
 namespace mmflt {
 
-// The pool holding every resident reference picture of a context (device address, size, and the
-// constant distance from a picture's Cb plane to its Cr plane).
+// The pool holding every resident reference picture of a context (device address and size).
 struct RefPool {
   const char* base;
   uint32_t bytes;
-  int cr_delta;
   // every pool slot has the same layout: slot k's luma plane origin is base + k * pic_bytes + y0,
-  // its Cb origin base + k * pic_bytes + cb0 (device kernels derive RefDev offsets from slot numbers)
+  // the origin of its interleaved chroma plane (one dword Cb | Cr << 16 per chroma position)
+  // base + k * pic_bytes + cb0 (device kernels derive RefDev offsets from slot numbers); stride_c
+  // counts chroma positions (dwords)
   uint32_t pic_bytes, y0, cb0;
   int stride_y, stride_c;
 };
@@ -421,7 +421,7 @@ struct LdsRows {
 };
 
 // Interior window of sub-block (xPos, yPos) of a pooled plane whose first sample is at byte
-// `plane_off` of the pool (soff: uniform extra offset, e.g. Cr = Cb + cr_delta).
+// `plane_off` of the pool (soff: uniform extra offset).
 template <int NT, int SBW, int SBH>
 __device__ __forceinline__ void predict_subblock_pool(const RefPool& pool, uint32_t plane_off, int soff,
                                                       int stride, int xPos, int yPos, const uint32_t* __restrict__ ht,
@@ -430,6 +430,65 @@ __device__ __forceinline__ void predict_subblock_pool(const RefPool& pool, uint3
   const int x0 = (xPos - H0) & ~1;  // even sample at or below the window start: 4-byte aligned rows
   const PtrRows rows{pool.base + plane_off + soff + (long)((yPos - H0) * stride + x0) * 2, stride * 2};
   predict_rows<NT, SBW, SBH>(rows, ht, vt, bi, bd, out);
+}
+
+// Both 4:2:0 chroma 2x2 sub-blocks at (xPos, yPos) from the pool's interleaved chroma plane (dword
+// Cb | Cr << 16 per position; `plane_off` = byte offset of position (0, 0), `stride` in positions).
+// One window of 5 x 5 positions serves Cb and Cr, so a sub-block touches about half the cache lines
+// two separate planes cost (one 20-byte row segment instead of two 12-byte ones per window row).
+// The integer sums are those of predict_rows<4, 2, 2> on each plane: per window row the sample
+// pairs (s0, s1), (s2, s3) of a plane are one v_perm each from the position dwords, the first output
+// is A0 . (s0, s1) + A1 . (s2, s3), the second B0 . (s0, s1) + B1 . (s2, s3) + B2 . (s4, *) with
+// s4 taken straight from position dword 4 (B2 = (f3, 0) for Cb; (0, f3) for Cr's high half).
+// ht: PackedTaps::ch[xFrac][0] (A0 A1 0 | B0 B1 B2), vt: PackedTaps::cv[yFrac].
+__device__ __forceinline__ void predict_chroma_pool_il(const RefPool& pool, uint32_t plane_off, int stride, int xPos,
+                                                       int yPos, const uint32_t* __restrict__ ht,
+                                                       const uint32_t* __restrict__ vt, bool bi, int bd,
+                                                       int16_t* ocb, int16_t* ocr) {
+  constexpr int R = 5;  // window rows (2 + 4 - 1)
+  typedef uint32_t u4 __attribute__((ext_vector_type(4), aligned(4)));
+  const int maxv = (1 << bd) - 1;
+  const FiltParam fh = filt_param(true, false, bd);
+  const FiltParam fv = filt_param(false, !bi, bd);
+  const uint32_t a0 = ht[0], a1 = ht[1], b0 = ht[3], b1 = ht[4], b2 = ht[5], b2r = ht[5] << 16;
+  const uint32_t ve0 = vt[0], ve1 = vt[1], vo0 = vt[2], vo1 = vt[3], vo2 = vt[4];
+  const char* base = pool.base + plane_off + (long)((yPos - 1) * stride + xPos - 1) * 4;
+  uint32_t tb[R + 1][2], tr[R + 1][2];  // H outputs (low 16 bits used); row R is the zero pad
+  tb[R][0] = tb[R][1] = tr[R][0] = tr[R][1] = 0u;
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const char* p = base + (long)r * stride * 4;
+    uint32_t d[5];
+#if defined(MM_PROBE_NOLOAD)
+    for (int k = 0; k < 5; k++) d[k] = (uint32_t)(size_t)p + 0x10001u * k;
+#else
+    const u4 q = *reinterpret_cast<const u4*>(p);
+    d[0] = q.x; d[1] = q.y; d[2] = q.z; d[3] = q.w;
+    d[4] = *reinterpret_cast<const uint32_t*>(p + 16);
+#endif
+    const uint32_t cb01 = __builtin_amdgcn_perm(d[1], d[0], 0x05040100u);
+    const uint32_t cb23 = __builtin_amdgcn_perm(d[3], d[2], 0x05040100u);
+    const uint32_t cr01 = __builtin_amdgcn_perm(d[1], d[0], 0x07060302u);
+    const uint32_t cr23 = __builtin_amdgcn_perm(d[3], d[2], 0x07060302u);
+    tb[r][0] = (uint32_t)(dot2_(cb23, a1, dot2_seed_(cb01, a0, fh.offset)) >> fh.shift);
+    tb[r][1] = (uint32_t)(dot2_(d[4], b2, dot2_(cb23, b1, dot2_seed_(cb01, b0, fh.offset))) >> fh.shift);
+    tr[r][0] = (uint32_t)(dot2_(cr23, a1, dot2_seed_(cr01, a0, fh.offset)) >> fh.shift);
+    tr[r][1] = (uint32_t)(dot2_(d[4], b2r, dot2_(cr23, b1, dot2_seed_(cr01, b0, fh.offset))) >> fh.shift);
+  }
+#pragma unroll
+  for (int pl = 0; pl < 2; pl++) {
+    uint32_t(*t)[2] = pl ? tr : tb;
+    int16_t* out = pl ? ocr : ocb;
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+      const uint32_t p0 = pack_lo16_(t[0][c], t[1][c]), p1 = pack_lo16_(t[2][c], t[3][c]),
+                     p2 = pack_lo16_(t[4][c], t[5][c]);
+      const int s0 = dot2_(p1, ve1, dot2_seed_(p0, ve0, fv.offset)) >> fv.shift;
+      const int s1 = dot2_(p2, vo2, dot2_(p1, vo1, dot2_seed_(p0, vo0, fv.offset))) >> fv.shift;
+      out[c] = fv.clip ? clip_pel(s0, maxv) : (int16_t)s0;
+      out[2 + c] = fv.clip ? clip_pel(s1, maxv) : (int16_t)s1;
+    }
+  }
 }
 #else
 // predict_subblock for an interior window (host): same arithmetic, window rows read with wide loads

@@ -1179,9 +1179,10 @@ struct mm_ctx {
   std::string err;
   std::map<int, RefHost> refs;
   // Reference pool: every resident reference picture in one allocation of pool_cap picture slots
-  // (Y | Cb | Cr, rows 128-byte aligned); kernels address planes by 32-bit byte offsets from the
-  // pool base (RefDev::off_y / off_cb, mm_filter.h RefPool), so the pool stays below 2 GiB.
+  // (Y | interleaved CbCr, rows 128-byte aligned); kernels address planes by 32-bit byte offsets from
+  // the pool base (RefDev::off_y / off_cb, mm_filter.h RefPool), so the pool stays below 2 GiB.
   char* pool = nullptr;
+  int16_t* chroma_stage = nullptr;  // host-sourced Cb | Cr planes on their way into the pool
   size_t pic_bytes = 0;
   int pool_cap = 0;
   std::vector<int> pool_free;
@@ -1488,8 +1489,8 @@ int mm_destroy(mm_ctx* c) {
   (void)hipStreamSynchronize(c->stream);
   if (c->aux) (void)hipStreamSynchronize(c->aux);
   if (c->mvp_on_own) (void)hipStreamSynchronize(c->mvp_stream);
-  for (void* q : {(void*)c->pool, (void*)c->trig, (void*)c->tan_grid, (void*)c->mpa_px, (void*)c->mpa_py,
-                  (void*)c->mpa_vip})
+  for (void* q : {(void*)c->pool, (void*)c->chroma_stage, (void*)c->trig, (void*)c->tan_grid, (void*)c->mpa_px,
+                  (void*)c->mpa_py, (void*)c->mpa_vip})
     if (q) dev_free(c, q);
   c->d_jobs.release(c);
   c->d_job_off.release(c);
@@ -1607,6 +1608,9 @@ int mm_epipole_count(mm_epipole_list* e) { return e ? e->l->count() : -1; }
 // in-range sub-block (sb_out_of_range admits positions up to maxCU outside the picture; the
 // 8-tap luma window reaches 4 samples beyond, the 4-tap chroma one 2), so k_mc never clamps.
 // Margins are 64 samples aligned so plane origins stay 128-byte aligned; +8 samples spare.
+// The chroma plane is interleaved: one dword Cb | Cr << 16 per position (chroma_layout's stride
+// counts positions, its bytes are those of the two planes), so one window row segment of k_mc's
+// chroma filter serves both components (mm_filter.h predict_chroma_pool_il).
 struct PlaneLayout {
   int mx, my, stride;  // margin columns / rows, row stride (samples)
   size_t bytes;        // whole padded plane
@@ -1623,7 +1627,9 @@ static PlaneLayout luma_layout(const mm_ctx* c) {
   return plane_layout(c->geo.W, c->geo.H, c->geo.maxCUw, c->geo.maxCUh, 4, 3);
 }
 static PlaneLayout chroma_layout(const mm_ctx* c) {
-  return plane_layout(c->geo.Wc, c->geo.Hc, c->geo.maxCUwc, c->geo.maxCUhc, 2, 1);
+  PlaneLayout l = plane_layout(c->geo.Wc, c->geo.Hc, c->geo.maxCUwc, c->geo.maxCUhc, 2, 1);
+  l.bytes *= 2;  // interleaved Cb | Cr dwords
+  return l;
 }
 
 static void place_ref(mm_ctx* c, RefHost& r) {
@@ -1632,8 +1638,9 @@ static void place_ref(mm_ctx* c, RefHost& r) {
   r.stride_c = lc.stride;
   char* base = c->pool + (size_t)r.slot * c->pic_bytes;
   r.y = reinterpret_cast<int16_t*>(base + 2 * ((size_t)ly.my * ly.stride + ly.mx));
-  r.cb = c->geo.chroma ? reinterpret_cast<int16_t*>(base + ly.bytes + 2 * ((size_t)lc.my * lc.stride + lc.mx)) : nullptr;
-  r.cr = c->geo.chroma ? reinterpret_cast<int16_t*>(reinterpret_cast<char*>(r.cb) + lc.bytes) : nullptr;
+  // cb: position (0, 0) of the interleaved chroma plane (Cb | Cr << 16 dwords); no separate Cr plane
+  r.cb = c->geo.chroma ? reinterpret_cast<int16_t*>(base + ly.bytes + 4 * ((size_t)lc.my * lc.stride + lc.mx)) : nullptr;
+  r.cr = nullptr;
 }
 
 // Fills a plane's margins from its nearest edge sample (corners from the corner sample), one
@@ -1667,6 +1674,38 @@ __global__ void __launch_bounds__(256) k_pad_plane(int16_t* __restrict__ o, int 
   *reinterpret_cast<u2*>(o + (long)y * stride + x) = v;
 }
 
+// The interleaved chroma plane with its margins from the two source planes, one 4-position (16-byte)
+// chunk per thread over the whole padded plane: position (x, y) holds Cb | Cr << 16 of the source
+// sample at (x, y) clamped to the picture -- what pad_plane's edge replication gives each plane.
+__global__ void __launch_bounds__(256) k_pad_chroma_il(uint32_t* __restrict__ o, int stride, int w, int h, int mx,
+                                                       int my, const int16_t* __restrict__ cb,
+                                                       const int16_t* __restrict__ cr, long src_stride) {
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  const int fq = (w + 2 * mx) >> 2;  // chunks per padded row
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long)fq * (h + 2 * my)) return;
+  const int r = (int)(t / fq);
+  const int x = 4 * (int)(t - (long)r * fq) - mx, y = r - my;
+  const long sy = (long)(y < 0 ? 0 : (y >= h ? h - 1 : y)) * src_stride;
+  uint32_t v[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int sx = x + k < 0 ? 0 : (x + k >= w ? w - 1 : x + k);
+    v[k] = (uint32_t)(uint16_t)cb[sy + sx] | ((uint32_t)(uint16_t)cr[sy + sx] << 16);
+  }
+  *reinterpret_cast<u4*>(o + (long)y * stride + x) = u4{v[0], v[1], v[2], v[3]};
+}
+
+static int pad_chroma_il(mm_ctx* c, int16_t* origin, const int16_t* cb, const int16_t* cr, long src_stride) {
+  const PlaneLayout l = chroma_layout(c);
+  const int w = c->geo.Wc, h = c->geo.Hc;
+  const long n = (long)((w + 2 * l.mx) >> 2) * (h + 2 * l.my);
+  hipLaunchKernelGGL(k_pad_chroma_il, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream,
+                     reinterpret_cast<uint32_t*>(origin), l.stride, w, h, l.mx, l.my, cb, cr, src_stride);
+  HIPCHK(c, hipGetLastError());
+  return MM_OK;
+}
+
 static int pad_plane(mm_ctx* c, int16_t* origin, const PlaneLayout& l, int w, int h) {
   const long n = (long)2 * l.my * ((w + 2 * l.mx) >> 2) + (long)h * ((2 * l.mx) >> 2);
   hipLaunchKernelGGL(k_pad_plane, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c->stream, origin, l.stride, w, h,
@@ -1680,7 +1719,7 @@ static int pad_plane(mm_ctx* c, int16_t* origin, const PlaneLayout& l, int w, in
 // its own streams (dev_free), so no launch still reads the old allocation and nothing waits on the
 // host.
 static int take_pool_slot(mm_ctx* c, int* slot) {
-  if (!c->pic_bytes) c->pic_bytes = luma_layout(c).bytes + (c->geo.chroma ? 2 * chroma_layout(c).bytes : 0);
+  if (!c->pic_bytes) c->pic_bytes = luma_layout(c).bytes + (c->geo.chroma ? chroma_layout(c).bytes : 0);
   if (c->pool_free.empty()) {
     const size_t limit = ((size_t)1 << 31) - 1;
     const int max_cap = (int)std::min<size_t>(limit / c->pic_bytes, 64);
@@ -1709,10 +1748,9 @@ static RefPool pool_of(const mm_ctx* c) {
   RefPool p{};
   p.base = c->pool;
   p.bytes = (uint32_t)((size_t)c->pool_cap * c->pic_bytes);
-  p.cr_delta = c->geo.chroma ? (int)lc.bytes : 0;
   p.pic_bytes = (uint32_t)c->pic_bytes;
   p.y0 = (uint32_t)(2 * ((size_t)ly.my * ly.stride + ly.mx));
-  p.cb0 = c->geo.chroma ? (uint32_t)(ly.bytes + 2 * ((size_t)lc.my * lc.stride + lc.mx)) : 0u;
+  p.cb0 = c->geo.chroma ? (uint32_t)(ly.bytes + 4 * ((size_t)lc.my * lc.stride + lc.mx)) : 0u;
   p.stride_y = ly.stride;
   p.stride_c = lc.stride;
   return p;
@@ -1763,14 +1801,21 @@ int mm_upload_ref(mm_ctx* c, int poc, const int16_t* y, ptrdiff_t sy, const int1
   const int W = c->geo.W, H = c->geo.H, Wc = c->geo.Wc, Hc = c->geo.Hc;
   hipMemcpyKind k = src_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
   HIPCHK(c, hipMemcpy2DAsync(r.y, r.stride_y * 2, y, sy * 2, W * 2, H, k, c->stream));
-  if (c->geo.chroma) {
-    HIPCHK(c, hipMemcpy2DAsync(r.cb, r.stride_c * 2, cb, sc_ * 2, Wc * 2, Hc, k, c->stream));
-    HIPCHK(c, hipMemcpy2DAsync(r.cr, r.stride_c * 2, cr, sc_ * 2, Wc * 2, Hc, k, c->stream));
-  }
   RCCHK(pad_plane(c, r.y, luma_layout(c), W, H));
   if (c->geo.chroma) {
-    RCCHK(pad_plane(c, r.cb, chroma_layout(c), Wc, Hc));
-    RCCHK(pad_plane(c, r.cr, chroma_layout(c), Wc, Hc));
+    // device sources are interleaved straight from their planes; host ones through a device copy
+    const int16_t *scb = cb, *scr = cr;
+    long ss = (long)sc_;
+    if (!src_dev) {
+      if (!c->chroma_stage) HIPCHK(c, dev_alloc(c, reinterpret_cast<void**>(&c->chroma_stage), (size_t)4 * Wc * Hc));
+      int16_t* st = c->chroma_stage;
+      HIPCHK(c, hipMemcpy2DAsync(st, Wc * 2, cb, sc_ * 2, Wc * 2, Hc, k, c->stream));
+      HIPCHK(c, hipMemcpy2DAsync(st + (size_t)Wc * Hc, Wc * 2, cr, sc_ * 2, Wc * 2, Hc, k, c->stream));
+      scb = st;
+      scr = st + (size_t)Wc * Hc;
+      ss = Wc;
+    }
+    RCCHK(pad_chroma_il(c, r.cb, scb, scr, ss));
   }
   if (!src_dev) HIPCHK(c, hipStreamSynchronize(c->stream));  // host source buffers may be reused at once
   return MM_OK;

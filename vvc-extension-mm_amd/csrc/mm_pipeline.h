@@ -18,7 +18,7 @@ struct RefDev {
   const int16_t* cb;
   const int16_t* cr;
   int stride_y, stride_c;
-  uint32_t off_y, off_cb;  // byte offsets of the Y and Cb planes in the context's RefPool
+  uint32_t off_y, off_cb;  // byte offsets of the Y and interleaved chroma planes in the context's RefPool
 };
 
 // One reprojection job == one reprojectMotionVectorSubblocks call
@@ -539,25 +539,23 @@ MM_HD void mc_rec_impl(int g, const McIn& in, const Geometry& geo, const Taps& t
     if (sb_out_of_range(xPos, yPos, geo.Wc, geo.Hc, geo.maxCUwc, geo.maxCUhc, 2, 2)) {
       for (int i = 0; i < 4; i++) pcb[l][i] = pcr[l][i] = oor;
 #if defined(__HIP_DEVICE_COMPILE__)
-    } else if (geo.padded || window_interior<4, 2, 2>(xPos, yPos, geo.Wc, geo.Hc)) {
-      const uint32_t* ht = taps.packed->ch[xFrac][(xPos - 1) & 1];
-      const uint32_t* vt = taps.packed->cv[yFrac];
-      predict_subblock_pool<4, 2, 2>(taps.pool, r.off_cb, 0, r.stride_c, xPos, yPos, ht, vt, true, geo.bd, pcb[l]);
-      predict_subblock_pool<4, 2, 2>(taps.pool, r.off_cb, taps.pool.cr_delta, r.stride_c, xPos, yPos, ht, vt, true,
-                                     geo.bd, pcr[l]);
+    } else {  // device contexts always hold padded pool planes (geo.padded), chroma interleaved
+      predict_chroma_pool_il(taps.pool, r.off_cb, r.stride_c, xPos, yPos, taps.packed->ch[xFrac][0],
+                             taps.packed->cv[yFrac], true, geo.bd, pcb[l], pcr[l]);
+    }
 #else
     } else if (window_interior<4, 2, 2>(xPos, yPos, geo.Wc, geo.Hc)) {
       predict_subblock_interior<4, 2, 2>(r.cb, r.stride_c, xPos, yPos, taps.chroma[xFrac], taps.chroma[yFrac], true,
                                          geo.bd, pcb[l]);
       predict_subblock_interior<4, 2, 2>(r.cr, r.stride_c, xPos, yPos, taps.chroma[xFrac], taps.chroma[yFrac], true,
                                          geo.bd, pcr[l]);
-#endif
     } else {
       predict_subblock<4, 2, 2>(r.cb, r.stride_c, geo.Wc, geo.Hc, xPos, yPos, taps.chroma[xFrac], taps.chroma[yFrac],
                                 true, geo.bd, pcb[l]);
       predict_subblock<4, 2, 2>(r.cr, r.stride_c, geo.Wc, geo.Hc, xPos, yPos, taps.chroma[xFrac], taps.chroma[yFrac],
                                 true, geo.bd, pcr[l]);
     }
+#endif
   }
   const int pa = used[0] ? 0 : 1;
   const int cx = ox >> 1, cy = oy >> 1;
