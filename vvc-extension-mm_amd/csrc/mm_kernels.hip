@@ -508,9 +508,31 @@ __global__ void __launch_bounds__(256) k_me_chunks(const int* __restrict__ off, 
   chunk[c] = lo;
 }
 
+// Orders one wave's LDS accesses (its lanes run in lockstep; LDS serves a wave's accesses in order)
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 #ifndef MM_ME_WAVES
 #define MM_ME_WAVES 4  // waves per SIMD of k_me_sad (its body alone would take 162 VGPRs: 3 waves)
 #endif
+// Window staging (MM_ME_LDS): a wave's lanes are consecutive window rows j of one block (16 lanes per
+// row for a 16x16 block), so the 8-tap windows of all their candidates -- each candidate one sample
+// step from the last -- fall in one box of about (block + 2 range + 8) x (block + 4 + 8) samples.  The
+// wave loads that box into its LDS once and every candidate's window rows are then LDS reads
+// instead of texture-path loads.  The box comes from each lane's first and last candidate plus
+// ME_WIN_SLACK samples; a candidate whose window is not inside it (curved motion) and lanes of
+// another block read the pool as before, so results never depend on the box.
+#ifndef MM_ME_LDS
+#define MM_ME_LDS 1
+#endif
+constexpr int ME_WIN_W = 88, ME_WIN_H = 48;           // staged box per wave: samples x rows
+constexpr int ME_WIN_STRIDE = ME_WIN_W / 2 + 1;       // dwords per LDS row (odd: rows start on different banks)
+[[maybe_unused]] constexpr int ME_WIN_SLACK = 2;
+static_assert(MM_ME_WAVES * (4 * ME_WIN_H * ME_WIN_STRIDE * 4 + MAX_SLOTS * (int)sizeof(RefDev)) <= 160 * 1024,
+              "the workgroups of one CU fit its LDS");
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MM_ME_WAVES))) k_me_sad(SeqConst sc, Geometry geo, MeWindow w,
                                                 const MeBlockDev* __restrict__ blocks, int n_blocks,
                                                 const int* __restrict__ blk_off, const int* __restrict__ chunk,
@@ -518,6 +540,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MM_ME_
                                                 const PicTables t, const int16_t* __restrict__ org, int org_stride,
                                                 uint32_t* __restrict__ sads) {
   __shared__ RefDev s_ref[MAX_SLOTS];  // indexed per lane: staged by stage_ref_table
+#if MM_ME_LDS && defined(__HIP_DEVICE_COMPILE__)
+  __shared__ uint32_t s_win[4][ME_WIN_H * ME_WIN_STRIDE];  // per wave
+#endif
   stage_ref_table<MAX_SLOTS>(t.pool_slot4, t.pool, s_ref);
   __syncthreads();
   const int g = xcd_block() * blockDim.x + threadIdx.x;
@@ -532,10 +557,67 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MM_ME_
     me_elem_init(g, bi, sc, w, blocks, setups, cache, org, org_stride, &el, &j);
     key = blocks[bi].sad_off + j * w.side;
   }
+#if MM_ME_LDS && defined(__HIP_DEVICE_COMPILE__)
+  // the box of the wave's last active lane's block, from its lanes' first and last candidates
+  const uint64_t act = __ballot(active);
+  const int bref = __shfl(bi, 63 - __clzll(act));
+  const bool mine = active && bi == bref;
+  int xmin = INT_MAX, xmax = INT_MIN, ymin = INT_MAX, ymax = INT_MIN;
+  if (mine) {
+#pragma unroll 1
+    for (int q = 0; q < 2; q++) {
+      int32_t fx, fy;
+      me_cand_pos(el, q ? w.side - 1 : 0, j, bi, sc, w, setups, &fx, &fy);
+      const int xPos = fx >> 4, yPos = fy >> 4;
+      if (!me_out_of_range(xPos, yPos, geo)) {
+        xmin = min(xmin, xPos);
+        xmax = max(xmax, xPos);
+        ymin = min(ymin, yPos);
+        ymax = max(ymax, yPos);
+      }
+    }
+  }
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    xmin = min(xmin, __shfl_xor(xmin, d));
+    xmax = max(xmax, __shfl_xor(xmax, d));
+    ymin = min(ymin, __shfl_xor(ymin, d));
+    ymax = max(ymax, __shfl_xor(ymax, d));
+  }
+  const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const bool any = xmin <= xmax;  // some lane of the block has an in-range extreme candidate
+  if (!any) xmin = xmax = ymin = ymax = 0;
+  // columns [bx0, bx0 + 8 cw) hold every window (12 samples from its even start) of a position in
+  // [xmin - SLACK, xmax + SLACK]; rows [by0, by0 + rows) every window's rows yPos - 3 .. yPos + 7
+  const int bx0 = (xmin - ME_WIN_SLACK - 3) & ~1, by0 = ymin - ME_WIN_SLACK - 3;
+  const int cw = (xmax + ME_WIN_SLACK + 9 - bx0 + 7) >> 3, rows = ymax + ME_WIN_SLACK + 8 - by0;
+  const bool staged = any && cw * 8 <= ME_WIN_W && rows <= ME_WIN_H;
+  if (staged) {  // wave-uniform
+    const RefDev r = s_ref[__builtin_amdgcn_readfirstlane(blocks[bref].slot)];
+    const char* src = t.pool.base + r.off_y + (long)(by0 * r.stride_y + bx0) * 2;
+    for (int c4 = lane; c4 < rows * cw; c4 += 64) {
+      const int rr = c4 / cw, c = c4 - rr * cw;
+      typedef uint32_t u4a4 __attribute__((ext_vector_type(4), aligned(4)));
+      const u4a4 q = *reinterpret_cast<const u4a4*>(src + ((long)rr * r.stride_y + 8 * c) * 2);
+      uint32_t* dp = &s_win[wv][rr * ME_WIN_STRIDE + 4 * c];
+      dp[0] = q.x;
+      dp[1] = q.y;
+      dp[2] = q.z;
+      dp[3] = q.w;
+    }
+  }
+  wave_lds_sync();
+  const MeWin win{s_win[wv], ME_WIN_STRIDE, bx0, by0, bx0 + 8 * cw, by0 + rows};
+  const bool use_win = staged && mine;
+#endif
 #pragma unroll 1
   for (int i = 0; i < w.side; i++) {  // uniform trip count (shuffles below)
     uint32_t v = 0;
+#if MM_ME_LDS && defined(__HIP_DEVICE_COMPILE__)
+    if (active) v = me_cand_sad_win(el, i, j, bi, sc, geo, taps, w, blocks, setups, s_ref, win, use_win);
+#else
     if (active) v = me_cand_sad(el, i, j, bi, sc, geo, taps, w, blocks, setups, s_ref);
+#endif
     const int idx = active ? key + i : key;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -700,12 +782,6 @@ struct DmvrWaveLds {
 static_assert(2 * (N_OFF - 1) <= 64, "one lane per (offset, list) setup");
 static_assert((N_OFF - 1) % 4 == 0 && (N_OFF - 1) / 2 == DMVR_LANE_OFFS, "24 offsets split over 2 or 4 parts");
 
-// Orders one wave's LDS accesses (its lanes run in lockstep; LDS serves a wave's accesses in order)
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 #ifndef MM_DMVR_SEARCH_WAVES
 #define MM_DMVR_SEARCH_WAVES 4  // waves per SIMD = workgroups per CU (LDS): 128 VGPRs, spill-free

@@ -99,19 +99,54 @@ MM_HD void me_elem_init(int g, int bi, const SeqConst& sc, const MeWindow& w, co
     for (int k = 0; k < 4; k++) el->org[r * 4 + k] = o[(long)r * org_stride + k];
 }
 
+// The element's reprojected position (1/16 luma) for candidate i of its row j.
+MM_HD void me_cand_pos(const MeElem& el, int i, int j, int bi, const SeqConst& sc, const MeWindow& w,
+                       const BlockSetup* setups, int32_t* fx, int32_t* fy) {
+  const BlockSetup& s = setups[(long)bi * w.C + (long)j * w.side + i];
+  float mx, my;
+#if defined(MM_PROBE_ME_NOTAIL)  // timing probe (wrong results): a candidate-dependent position without the model tail
+  mx = el.gx + 0.37f * (float)i + s.mvx * 1e-9f;
+  my = el.gy + 0.21f * (float)j;
+#else
+  motion_tail(sc, s, el.head, el.gx, el.gy, Math{el.packet != 0}, el.mpa != 0, el.px, el.py, el.vip != 0, &mx, &my);
+#endif
+  reproject_finish(sc, el.gx, el.gy, mx, my, el.packet != 0, 0, fx, fy);
+}
+
+// RdCost::xGetSAD over this sub-block's rows of the block (rows 4*row + r; subShift 1 keeps the even
+// block rows, which are the even rows of every sub-block), scaled by subShift
+MM_HD uint32_t me_sad_of(const MeElem& el, int sub_shift, const int16_t* p) {
+  const int rstep = 1 << sub_shift;
+  uint32_t sum = 0;
+  for (int r = 0; r < 4; r += rstep)
+    for (int k = 0; k < 4; k++) {
+      const int d = (int)el.org[r * 4 + k] - (int)p[r * 4 + k];
+      sum += (uint32_t)(d < 0 ? -d : d);
+    }
+  return sum << sub_shift;
+}
+
+// ME zero rule: a sub-block predicts zeros when its position is out of range (maxCUWidth = 0,
+// InterSearch.cpp:6329-6335)
+MM_HD bool me_out_of_range(int xPos, int yPos, const Geometry& geo) {
+  return xPos < 0 || yPos < 0 || xPos >= geo.W - 4 || yPos >= geo.H - 4;
+}
+
 // The (subShift-scaled) SAD of the element's sub-block for candidate i of its row j.
 MM_HD uint32_t me_cand_sad(const MeElem& el, int i, int j, int bi, const SeqConst& sc, const Geometry& geo,
                            const Taps& taps, const MeWindow& w, const MeBlockDev* blocks, const BlockSetup* setups,
                            const RefDev* refs) {
   const MeBlockDev& b = blocks[bi];
-  const BlockSetup& s = setups[(long)bi * w.C + (long)j * w.side + i];
-  float mx, my;
-  motion_tail(sc, s, el.head, el.gx, el.gy, Math{el.packet != 0}, el.mpa != 0, el.px, el.py, el.vip != 0, &mx, &my);
   int32_t fx, fy;
-  reproject_finish(sc, el.gx, el.gy, mx, my, el.packet != 0, 0, &fx, &fy);
+  me_cand_pos(el, i, j, bi, sc, w, setups, &fx, &fy);
   const int xPos = fx >> 4, yPos = fy >> 4, xFrac = fx & 15, yFrac = fy & 15;
   int16_t p[16];
-  if (xPos < 0 || yPos < 0 || xPos >= geo.W - 4 || yPos >= geo.H - 4) {  // maxCUWidth = 0
+#if defined(MM_PROBE_ME_NOFILTER)  // timing probe (wrong results): the position without the prediction
+  for (int k = 0; k < 16; k++) p[k] = (int16_t)(xPos + k * yPos + xFrac * yFrac);
+  if (false) {
+#else
+  if (me_out_of_range(xPos, yPos, geo)) {
+#endif
     for (int k = 0; k < 16; k++) p[k] = 0;
   } else {
     const RefDev r = refs[b.slot];
@@ -130,16 +165,43 @@ MM_HD uint32_t me_cand_sad(const MeElem& el, int i, int j, int bi, const SeqCons
                                 geo.bd, p);
     }
   }
-  // RdCost::xGetSAD over this sub-block's rows of the block (rows 4*row + r; subShift 1 keeps
-  // the even block rows, which are the even rows of every sub-block)
-  const int rstep = 1 << b.sub_shift;
-  uint32_t sum = 0;
-  for (int r = 0; r < 4; r += rstep)
-    for (int k = 0; k < 4; k++) {
-      const int d = (int)el.org[r * 4 + k] - (int)p[r * 4 + k];
-      sum += (uint32_t)(d < 0 ? -d : d);
-    }
-  return sum << b.sub_shift;
+  return me_sad_of(el, b.sub_shift, p);
 }
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// A reference window staged in a wave's LDS (k_me_sad): luma samples [x0, x1) x rows [y0, y1) of the
+// wave's reference, x0 even, row r at lds + (r - y0) * stride dwords.
+struct MeWin {
+  const uint32_t* lds;
+  int stride, x0, y0, x1, y1;
+};
+// me_cand_sad with the window rows read from the staged window when `use` and the candidate's window
+// lies inside it; otherwise from the pool as me_cand_sad does (same integer sums either way).
+__device__ __forceinline__ uint32_t me_cand_sad_win(const MeElem& el, int i, int j, int bi, const SeqConst& sc,
+                                                    const Geometry& geo, const Taps& taps, const MeWindow& w,
+                                                    const MeBlockDev* blocks, const BlockSetup* setups,
+                                                    const RefDev* refs, const MeWin& win, bool use) {
+  const MeBlockDev& b = blocks[bi];
+  int32_t fx, fy;
+  me_cand_pos(el, i, j, bi, sc, w, setups, &fx, &fy);
+  const int xPos = fx >> 4, yPos = fy >> 4, xFrac = fx & 15, yFrac = fy & 15;
+  int16_t p[16];
+  if (me_out_of_range(xPos, yPos, geo)) {
+    for (int k = 0; k < 16; k++) p[k] = 0;
+  } else {
+    const uint32_t* ht = taps.packed->lh[xFrac][(xPos - 3) & 1];
+    const uint32_t* vt = taps.packed->lv[yFrac];
+    const int xw = (xPos - 3) & ~1;  // the window's dword-aligned rows: 12 samples from xw, rows yPos - 3 .. yPos + 7
+    if (use && xw >= win.x0 && xw + 12 <= win.x1 && yPos - 3 >= win.y0 && yPos + 8 <= win.y1) {
+      const LdsRows rows{win.lds + (yPos - 3 - win.y0) * win.stride + ((xw - win.x0) >> 1), win.stride};
+      predict_rows<8, 4, 4>(rows, ht, vt, false, geo.bd, p);
+    } else {
+      const RefDev r = refs[b.slot];
+      predict_subblock_pool<8, 4, 4>(taps.pool, r.off_y, 0, r.stride_y, xPos, yPos, ht, vt, false, geo.bd, p);
+    }
+  }
+  return me_sad_of(el, b.sub_shift, p);
+}
+#endif
 
 }  // namespace mmme
