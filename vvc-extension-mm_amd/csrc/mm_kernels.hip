@@ -619,6 +619,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MM_ME_
     if (active) v = me_cand_sad(el, i, j, bi, sc, geo, taps, w, blocks, setups, s_ref);
 #endif
     const int idx = active ? key + i : key;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (w.seg16) {  // lanes 16 k .. 16 k + 15 hold one (block, row): four DPP sums, no LDS round trips
+      v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+      v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+      v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+      v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);  // row_mirror
+      if (active && (lane & 15) == 0) atomicAdd(&sads[idx], v);
+      continue;
+    }
+#endif
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
       const uint32_t vu = __shfl_up(v, d);
@@ -2408,7 +2418,9 @@ int mm_sad_window(mm_ctx* c, int cur_poc, const mm_me_block* blocks, int n, int 
     hipLaunchKernelGGL(k_me_setup, dim3((bt.n_jobs + 255) / 256), dim3(256), 0, c->stream, c->sc, w, c->d_me_blocks.p,
                        bt.n_jobs, t, c->d_setup.p);
     const int ne = (int)bt.n_elems;
-    hipLaunchKernelGGL(k_me_sad, dim3(round_grid((ne + 255) / 256)), dim3(256), 0, c->stream, c->sc, c->geo, w,
+    MeWindow wb = w;  // 16 sub-blocks per block: a block's window row is one aligned 16-lane group
+    wb.seg16 = std::all_of(bt.blocks.begin(), bt.blocks.end(), [](const MeBlockDev& b) { return b.n == 16; }) ? 1 : 0;
+    hipLaunchKernelGGL(k_me_sad, dim3(round_grid((ne + 255) / 256)), dim3(256), 0, c->stream, c->sc, c->geo, wb,
                        c->d_me_blocks.p, (int)bt.blocks.size(), c->d_me_off.p, c->d_me_chunk.p, ne, c->d_setup.p,
                        make_cache(c), t, oit->second.y, oit->second.stride_y, sads);
     HIPCHK(c, hipGetLastError());

@@ -33,6 +33,7 @@ struct MeBlockDev {
 
 struct MeWindow {
   int range, step, side, C;  // side = 2 * range + 1, C = side * side
+  int seg16 = 0;             // device: every block of the batch has 16 sub-blocks (k_me_sad's 16-lane sums)
 };
 
 // candidate c of the window -> MV offset (row-major over the vertical offset)
