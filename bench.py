@@ -52,17 +52,19 @@ RED_DEVICE = ["cuda"]  # where the timing reductions run: "cpu" under the gloo r
 def measured_traffic(args, config):
     """HBM bytes per k_mc_dev launch from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes
     (profiles/r0N_traffic.json, tools/traffic_json.py), only when that profile was taken with
-    this very library (sha256) and the same workload; else None."""
+    this very library (sha256) and the same workload: (bytes, source label), else (None, reason).
+    The PMC passes are not run inside the bench: the counters need their own rocprofv3 runs."""
     import glob
     import hashlib
     if config != "C3" or args.uniform_model is not None or args.coherent_mv or args.dmvr_share > 0:
-        return None
+        return None, "no committed profile for this workload"
     sha = hashlib.sha256(open(mm360.LIB_PATH, "rb").read()).hexdigest()
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")), reverse=True):
         d = json.load(open(path))
         if d.get("lib_sha256") == sha and d.get("pictures") == args.pictures:
-            return d["traffic_bytes_per_launch"]
-    return None
+            return d["traffic_bytes_per_launch"], (f"{os.path.relpath(path, ROOT)} (library sha256 match; "
+                                                   f"rocprofv3 FETCH_SIZE / WRITE_SIZE passes, not this run)")
+    return None, f"no committed PMC profile of this library (sha256 {sha[:16]})"
 
 
 def host_info(threads):
@@ -242,6 +244,15 @@ def bench_pictures(args, cfg, params, rank, world, local, dist):
     # bit-exact check below reads these (every sample of a C3 picture is predicted, so a sample the
     # timed steps left unwritten would read -1 and fail the check)
     got = [tuple(t.cpu().numpy() for t in o) for o in outs]
+    # k_mc_dev as it runs in the timed loop: the same steps replayed with every k_mc_dev launch
+    # bracketed by kernel-bound events (mm_set_kernel_timing: no marker packets; under plan-ahead
+    # the stop event is the slot's gate), so its duration includes the overlap with the next
+    # picture's planning and reprojection on the auxiliary queue
+    ctx.set_kernel_timing(True)
+    replay = timed(args.steps, args.warmup, step, None)
+    loop_k = ctx.kernel_times_ms()[-args.steps:]
+    ctx.set_kernel_timing(False)
+    loop_kernel_ms = float(np.mean(loop_k))
     steps_area = sum(area[s % P_] for s in range(args.steps))
     total_area = float(steps_area)
     if dist:
@@ -258,7 +269,10 @@ def bench_pictures(args, cfg, params, rank, world, local, dist):
     st = np.mean(np.array(stages), axis=0)
     kernel_ms = float(st[3])
     alg_step = float(np.mean([alg[s % P_] for s in range(args.kernel_steps)]))
-    achieved = alg_step / (kernel_ms * 1e-3) / 1e9
+    alg_loop = float(np.mean([alg[s % P_] for s in range(args.steps)]))
+    achieved_iso = alg_step / (kernel_ms * 1e-3) / 1e9
+    achieved = alg_loop / (loop_kernel_ms * 1e-3) / 1e9
+    traffic, traffic_src = measured_traffic(args, args.config)
     mvp = None
     if args.config == "C3" and not args.no_mvp:
         mvp = mvp_per_picture(ctx, cfg, int(np.mean([len(p) for _, p, _ in pictures])), params,
@@ -292,9 +306,19 @@ def bench_pictures(args, cfg, params, rank, world, local, dist):
                        "parallelism": "1 GPU" if world == 1 else f"replicas x{world} (own pictures per GPU)"},
             "bit_exact": bit_exact, "mismatching_samples": mism,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": measured_traffic(args, args.config),
-                         "kernel": "k_mc_dev", "kernel_ms": round(kernel_ms, 4),
-                         "algorithmic_bytes": int(alg_step)},
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel": "k_mc_dev", "kernel_ms": round(loop_kernel_ms, 4),
+                         "kernel_ms_source": (f"mean of the {len(loop_k)} k_mc_dev launches of a replay of the timed "
+                                              f"steps, kernel-bound HIP events on the launch stream "
+                                              f"(mm_set_kernel_timing); replay {replay / args.steps * 1e3:.4f} ms "
+                                              f"per step vs {elapsed / args.steps * 1e3:.4f} timed"),
+                         "algorithmic_bytes": int(alg_loop),
+                         "frac_isolated": round(achieved_iso / HBM_PEAK_GBS, 4),
+                         "kernel_ms_isolated": round(kernel_ms, 4),
+                         "frac_end_to_end": round(alg_loop / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4),
+                         "note": "frac: k_mc_dev in the timed plan-ahead loop (beside the next picture's "
+                                 "reprojection); frac_isolated: stage-timing pass, stages one after another; "
+                                 "frac_end_to_end: algorithmic bytes / ms_per_step"},
             "stages_ms": {"plan": round(float(st[0]), 4), "setup": round(float(st[1]), 4),
                           "reproj": round(float(st[2]), 4), "mc": round(float(st[3]), 4),
                           "pipeline": round(float(st.sum()), 4)},

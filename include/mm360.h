@@ -255,7 +255,10 @@ int mm_pred_device(mm_ctx* ctx, int cur_poc, const mm_pu_desc* d_pus, int n, int
  * the per-call launch chain each.  Same semantics as mm_pred_device per picture (plan-ahead,
  * deferred status; the status's PU index counts through the pictures' lists in call order).
  * MM_PUF_DMVR PUs (mm_set_dmvr) are searched per picture inside the same chain -- the leaves of an
- * RA temporal layer are DMVR's usual bi PUs.  1 <= n_pics <= MM_MAX_PICS. */
+ * RA temporal layer are DMVR's usual bi PUs.  1 <= n_pics <= MM_MAX_PICS.  One launch chain holds
+ * 16 distinct GEODESIC_CAMPOSE epipoles (over every (cur_poc, resident reference) pair of its
+ * pictures); pictures beyond that are cut into consecutive runs of their own chain, and every run
+ * but the last is then synchronised and its status read before the next is issued. */
 #define MM_MAX_PICS 4
 typedef struct mm_pic_job {
   int32_t cur_poc;
@@ -392,6 +395,16 @@ int mm_set_call_timing(mm_ctx* ctx, int on);
  * ms[1] k_setup, ms[2] k_reproj, ms[3] k_mc. */
 int mm_set_stage_timing(mm_ctx* ctx, int on);
 int mm_last_stage_timing(mm_ctx* ctx, float ms[4]);
+
+/* Kernel timing of the interpolation kernel (k_mc_dev) inside an ordinary call sequence: while on,
+ * every k_mc_dev launch is bracketed by a start / stop event pair bound to the dispatch itself
+ * (no marker packets; under plan-ahead the stop event is also the plan slot's gate), so the
+ * durations are those of the launches as they overlap the next picture's planning and
+ * reprojection.  mm_kernel_times synchronises the context stream and returns the durations (ms)
+ * of up to the last 256 launches since the timing was switched on or last read, oldest first, in
+ * ms[0 .. *n); the count restarts.  (No reference counterpart; the bench's roofline reads it.) */
+int mm_set_kernel_timing(mm_ctx* ctx, int on);
+int mm_kernel_times(mm_ctx* ctx, float* ms, int cap, int* n);
 
 /* Stripe pipelining of mm_pred_device / mm_pred_run (default 1, 1..64): the PU list is cut into
  * `stripes` contiguous ranges that are planned and predicted independently, alternating between

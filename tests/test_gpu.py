@@ -1143,6 +1143,87 @@ def test_pred_device_multi_with_dmvr_vs_oracle(plan_ahead):
                     assert np.array_equal(got, x), (rnd, q, plane_mismatch(name, got, x))
 
 
+def test_pred_plan_ahead_dmvr_on_off_growing_lists():
+    """Plan-ahead with MM-DMVR switched on and off between calls while the lists grow (round-5
+    advisor): a small DMVR list, a larger plain list, a medium DMVR list -- the third call's
+    DMVR-derived capacities (jobs, sub-PU records) exceed what the first sized, so its buffers must
+    grow through the synchronised branch, not under the auxiliary stream's planning.  Every output
+    == the oracle (predict_mixed), twice round."""
+    cfg = W.CONFIGS["C2"]
+    params = mm360.seq_params(cfg.width, cfg.height, cfg.models)
+    refs = {poc: W.ref_planes(cfg.width, cfg.height, poc) for poc in W.REF_POCS}
+    full_d = W.pu_list(cfg, frame=3, dmvr_share=0.5)
+    plain = W.pu_list(cfg, frame=4)
+    small_d = full_d[W.dmvr_flagged(full_d)][:40]
+    medium_d = full_d[: 2 * len(full_d) // 3]
+    calls = [(True, small_d), (False, plain), (True, medium_d)]
+    orc = Oracle(params, EPI)
+    want = [orc.predict_mixed(W.CUR_POC, p, refs, cfg.width, cfg.height) for _, p in calls]
+    with _ctx(params) as ctx:
+        ctx.set_plan_ahead(True)
+        for poc, (y, cb, cr) in refs.items():
+            ctx.upload_ref(poc, torch.from_numpy(y).cuda(), torch.from_numpy(cb).cuda(), torch.from_numpy(cr).cuda())
+        d_lists = [mm360.pus_to_device(p) for _, p in calls]
+        torch.cuda.synchronize()  # plan-ahead contract: the lists are complete before the calls
+        for rnd in range(2):
+            outs = [_planes(cfg, fill=0) for _ in calls]
+            for (dm, _), d, o in zip(calls, d_lists, outs):
+                ctx.set_dmvr(dm)
+                ctx.predict_device(W.CUR_POC, d, *o)
+            ctx.synchronize()
+            for k, (o, w) in enumerate(zip(outs, want)):
+                for name, t, x in zip(("y", "cb", "cr"), o, w):
+                    got = t.cpu().numpy()
+                    assert np.array_equal(got, x), (rnd, k, plane_mismatch(name, got, x))
+
+
+@pytest.mark.parametrize("plan_ahead", [False, True])
+def test_pred_device_multi_more_epipoles_than_one_chain_holds(plan_ahead):
+    """mm_pred_device_multi over four C1 pictures with six resident references and one distinct
+    camera-pose epipole per (cur, ref) pair: 24 epipoles, more than one launch chain's 16
+    (PicTables::ged), so the call is cut into runs (round-5 advisor) -- every picture == the oracle,
+    and a failing PU in the last picture is reported with its index counted through all four lists."""
+    cfg = W.CONFIGS["C1"]
+    params = mm360.seq_params(cfg.width, cfg.height, tuple(cfg.models) + (mm360.GEODESIC_CAMPOSE,))
+    ref_pocs = [0, 16, 32, 48, 64, 80]
+    refs = {p: W.ref_planes(cfg.width, cfg.height, p) for p in ref_pocs}
+    rng = np.random.default_rng(91)
+    pics, epis = [], []
+    for q in range(4):
+        cur = 8 + 16 * q
+        for r in ref_pocs:
+            v = rng.normal(size=3)
+            v = v / np.linalg.norm(v)
+            epis.append((cur, r, tuple(int(round(c * (1 << 24))) for c in v)))
+        pus = W.pu_list(cfg, frame=q)
+        pus["ref_poc"] = np.where(pus["ref_poc"] >= 0, np.array(ref_pocs)[rng.integers(0, 6, size=pus["ref_poc"].shape)], -1)
+        pus["model"][::3] = mm360.GEODESIC_CAMPOSE
+        pics.append((cur, pus))
+    orc = Oracle(params, epis)
+    want = [orc.predict(cur, pus, refs, cfg.width, cfg.height) for cur, pus in pics]
+    with _ctx(params, epis) as ctx:
+        ctx.set_plan_ahead(plan_ahead)
+        for poc, (y, cb, cr) in refs.items():
+            ctx.upload_ref(poc, torch.from_numpy(y).cuda(), torch.from_numpy(cb).cuda(), torch.from_numpy(cr).cuda())
+        d_lists = [mm360.pus_to_device(p) for _, p in pics]
+        torch.cuda.synchronize()
+        outs = [_planes(cfg, -3) for _ in pics]
+        ctx.predict_device_multi([(cur, d, *o) for (cur, _), d, o in zip(pics, d_lists, outs)])
+        assert ctx.status() == (mm360.MM_OK, -1)
+        for q, (o, w) in enumerate(zip(outs, want)):
+            for name, t, x in zip(("y", "cb", "cr"), o, w):
+                got = t.cpu().numpy()
+                assert np.array_equal(got, x), (q, plane_mismatch(name, got, x))
+        bad = pics[3][1].copy()
+        bad["x"][2] = 3  # not 4x4 aligned
+        d_bad = mm360.pus_to_device(bad)
+        torch.cuda.synchronize()
+        ctx.predict_device_multi([(pics[0][0], d_lists[0], *outs[0]), (pics[1][0], d_lists[1], *outs[1]),
+                                  (pics[2][0], d_lists[2], *outs[2]), (pics[3][0], d_bad, *outs[3])])
+        code, first = ctx.status()
+        assert code == mm360.MM_ERR_ARG and first == sum(len(p) for _, p in pics[:3]) + 2, (code, first)
+
+
 def test_effective_blocks_end_to_end_vs_oracle():
     """a2 wired end to end: decoded PUs of a C2 picture (merge / mvRefine DMVR PUs, SbTMVP PUs with
     8x8 motion fields, BDOF-split bi PUs) -> the product's mm_derive_effective_blocks -> one

@@ -4,7 +4,7 @@
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 for v in "$@"; do
-  L=tmp_variants/$v/libmm360.so; [ "$v" = default ] && L=vvc-extension-mm_amd/lib/libmm360.so
+  L=ab_variants/$v/libmm360.so; [ "$v" = default ] && L=vvc-extension-mm_amd/lib/libmm360.so
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "gpurun_out/abp_$v" -o run --output-format csv -- \
     python3 bench.py --steps 12 --warmup 4 --no-cpu-baseline --dmvr-share 0.3 --plan-ahead 0 --no-mvp --no-c5 --lib "$L" \
     > "gpurun_out/abp_$v.log" 2>&1 || exit 1

@@ -1,6 +1,6 @@
 """One mm_pred_dmvr call on the test suite's DMVR workload (tests/test_gpu.py
 test_pred_dmvr_vs_oracle) with a chosen library build: debugging aid for A/B builds.
-  python tools/dmvr_probe.py --lib tmp_variants/X/libmm360.so --size 1024x512 [--check]"""
+  python tools/dmvr_probe.py --lib ab_variants/X/libmm360.so --size 1024x512 [--check]"""
 import argparse
 import os
 import sys

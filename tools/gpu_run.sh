@@ -20,21 +20,21 @@ for step in "$@"; do
     tests) run gpu_tests 900 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread ;;
     tests_k=*)  # tests_k=<pytest -k expression>: a subset of the GPU suite
       run gpu_tests_k 600 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread -k "${step#tests_k=}" ;;
-    race_probe) run race_probe 900 env MM360_LIB=tmp_variants/probe/libmm360.so python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread ;;
+    race_probe) run race_probe 900 env MM360_LIB=ab_variants/probe/libmm360.so python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread ;;
     probe_ctl)  # positive control: the probe build with the s_ged barriers removed must FAIL (wrong pictures)
-      run probe_ctl 300 bash -c 'MM360_LIB=tmp_variants/probe_ctl/libmm360.so python -u -m pytest tests/test_gpu.py -q -k "pred_full_frame_vs_oracle or pred_uniform_per_model" --timeout 120 --timeout-method thread; rc=$?; echo "pytest rc=$rc (1 = tests failed as expected)"; test $rc -eq 1' ;;
+      run probe_ctl 300 bash -c 'MM360_LIB=ab_variants/probe_ctl/libmm360.so python -u -m pytest tests/test_gpu.py -q -k "pred_full_frame_vs_oracle or pred_uniform_per_model" --timeout 120 --timeout-method thread; rc=$?; echo "pytest rc=$rc (1 = tests failed as expected)"; test $rc -eq 1' ;;
     abb=*)  # abb=<rounds>=<v1,v2,...>: alternating headline runs of library variants (default = in-tree)
       rounds=$(echo "$step" | cut -d= -f2); vs=$(echo "$step" | cut -d= -f3 | tr ',' ' ')
       run "abb_$(echo "$vs" | tr ' ' '_')" 900 bash tools/ab_bench.sh "$rounds" $vs ;;
     example) run example 120 vvc-extension-mm_amd/lib/example_decode ;;
     dmvrab=*)  # dmvrab=<v1,v2,...>: C3 with a 30 % MM-DMVR share, per library variant (default = in-tree)
       for v in $(echo "$step" | cut -d= -f2 | tr ',' ' '); do
-        L=tmp_variants/$v/libmm360.so; [ "$v" = default ] && L=vvc-extension-mm_amd/lib/libmm360.so
+        L=ab_variants/$v/libmm360.so; [ "$v" = default ] && L=vvc-extension-mm_amd/lib/libmm360.so
         run "dmvr_$v" 600 python bench.py --dmvr-share 0.3 --steps 12 --warmup 3 --no-cpu-baseline --no-mvp --no-c5 --lib "$L"
       done ;;
     c5ab=*)  # c5ab=<v1,v2,...>: C5 (Mcandidates/s) of library variants (default = in-tree), one run each
       for v in $(echo "$step" | cut -d= -f2 | tr ',' ' '); do
-        L=tmp_variants/$v/libmm360.so; [ "$v" = default ] && L=vvc-extension-mm_amd/lib/libmm360.so
+        L=ab_variants/$v/libmm360.so; [ "$v" = default ] && L=vvc-extension-mm_amd/lib/libmm360.so
         run "c5_$v" 600 python bench.py --config C5 --steps 2 --warmup 1 --no-cpu-baseline --lib "$L"
       done ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;

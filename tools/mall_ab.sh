@@ -1,7 +1,7 @@
 #!/bin/bash
 # Is k_mc bound below L1?  The C3 bench with 1 picture (its 2 references, 132 MB padded, stay resident in
 # the 256 MB MALL) against 4 rotating pictures (529 MB of references), for the kept one-lane k_mc and
-# the paired-lane variant (tmp_variants/pair, tools/build_rev.sh exp/mc-pair-lanes pair).
+# the paired-lane variant (ab_variants/pair, tools/build_rev.sh exp/mc-pair-lanes pair).
 cd "$(dirname "$0")/.." && mkdir -p gpurun_out && export TMPDIR=/tmp
 run() {
   tag=$1; shift
@@ -11,7 +11,7 @@ run() {
 }
 for round in 1 2; do
   run old_p1_$round --pictures 1
-  run pair_p1_$round --pictures 1 --lib tmp_variants/pair/libmm360.so
+  run pair_p1_$round --pictures 1 --lib ab_variants/pair/libmm360.so
   run old_p4_$round --pictures 4
-  run pair_p4_$round --pictures 4 --lib tmp_variants/pair/libmm360.so
+  run pair_p4_$round --pictures 4 --lib ab_variants/pair/libmm360.so
 done

@@ -1,13 +1,13 @@
 """Debug aid: a copy of the library whose device-plan kernels record, from block 0, a start marker
 (sequence number << 8 | kernel code) into host-mapped memory, readable after a GPU fault through
-mm_debug_marks.  Writes tmp_variants/marks/csrc; build with tools/build_variant.sh conventions."""
+mm_debug_marks.  Writes ab_variants/marks/csrc; build with tools/build_variant.sh conventions."""
 import os
 import re
 import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-d = os.path.join(ROOT, "tmp_variants", "marks")
+d = os.path.join(ROOT, "ab_variants", "marks")
 shutil.rmtree(d, ignore_errors=True)
 os.makedirs(os.path.join(d, "csrc"))
 os.makedirs(os.path.join(d, "include"))

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Non-temporal k_mc output stores (nt) and record loads (ntr) vs the kept library (tmp_variants/nt, ntr).
+# Non-temporal k_mc output stores (nt) and record loads (ntr) vs the kept library (ab_variants/nt, ntr).
 cd "$(dirname "$0")/.." && mkdir -p gpurun_out && export TMPDIR=/tmp
 run() {
   tag=$1; shift
@@ -9,6 +9,6 @@ run() {
 }
 for round in 1 2; do
   run def_$round --pictures 4
-  run nt_$round --pictures 4 --lib tmp_variants/nt/libmm360.so
-  run ntr_$round --pictures 4 --lib tmp_variants/ntr/libmm360.so
+  run nt_$round --pictures 4 --lib ab_variants/nt/libmm360.so
+  run ntr_$round --pictures 4 --lib ab_variants/ntr/libmm360.so
 done

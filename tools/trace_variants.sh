@@ -4,7 +4,7 @@
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 for v in "$@"; do
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/tr_$v -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --kernel-steps 1 --lib tmp_variants/$v/libmm360.so > gpurun_out/tr_$v.log 2>&1 || exit 1
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/tr_$v -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --kernel-steps 1 --lib ab_variants/$v/libmm360.so > gpurun_out/tr_$v.log 2>&1 || exit 1
   python3 - "$v" <<'PY'
 import csv, sys
 v = sys.argv[1]

@@ -1296,7 +1296,16 @@ struct mm_ctx {
   // context stream waits for ev_plan before the reprojection
   bool plan_ahead = false;
   int ahead_par = 0;                               // slot of the next plan-ahead picture
+  int last_slot = 0;  // plan slot of the last call's (first) stripe: where its MM-DMVR deltas are
   hipEvent_t ev_gate[2] = {nullptr, nullptr};      // ev_gate[s]: the last k_mc_dev using slot s is done
+  // mm_set_kernel_timing: every k_mc_dev launch bracketed by a kernel-bound start / stop event pair
+  // from this ring (hipExtLaunchKernelGGL), read back by mm_kernel_times; under plan-ahead the stop
+  // event doubles as the slot's gate (gate[s] points at it), so the timed loop records no extra packet
+  static constexpr int KT_RING = 256;
+  bool kt_on = false;
+  int kt_n = 0;                                    // launches recorded since the last mm_kernel_times
+  hipEvent_t kt_ev[KT_RING][2] = {};
+  hipEvent_t gate[2] = {nullptr, nullptr};         // the event the next planning of slot s waits for
   hipEvent_t ev_plan = nullptr;
   // validation status words, one per picture, ping-pong: a picture reports into d_status[pic_par]
   // and its first stripe zeroes the other word for the next picture
@@ -1522,6 +1531,8 @@ int mm_create(const mm_seq_params* p, int device, mm_ctx** out_ctx) {
     mm_destroy(c);
     return MM_ERR_HIP;
   }
+  c->gate[0] = c->ev_gate[0];
+  c->gate[1] = c->ev_gate[1];
   // MPA frame caches (MVReprojection::init -> MotionPlaneAdaptiveMotionModel::fillCache)
   const int cols = p->width / 4, rows = p->height / 4, n = cols * rows;
   const unsigned mpa_bits = p->active_models & (7u << MPA_FRONT_BACK);
@@ -1615,6 +1626,9 @@ int mm_destroy(mm_ctx* c) {
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   for (auto& e : c->ev_gate)
     if (e) (void)hipEventDestroy(e);
+  for (auto& pr : c->kt_ev)
+    for (auto& e : pr)
+      if (e) (void)hipEventDestroy(e);
   if (c->ev_plan) (void)hipEventDestroy(c->ev_plan);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -1942,7 +1956,12 @@ static int round_grid(long v) { return (int)((v + 8 * XCD_RUN - 1) / (8 * XCD_RU
 // With MM-DMVR a PU is placed as up to 64 sub-PUs (128x128 / 16x16); a sub-PU covers at least 128
 // luma samples (PU::checkDMVRCondition), so the picture bounds them by W * H / 128, and their cost
 // elements (N_OFF per luma sub-block) by N_OFF times the picture's sub-blocks.
-static int ensure_slot_buffers(mm_ctx* c, PlanSlot& S, int n, bool dmvr, int pics = 1) {
+// fits (dry run): set to false when any buffer would have to grow; nothing is allocated or changed.
+// slot_fits is this dry run, so a call whose capacities (the DMVR-derived ones included) exceed any
+// buffer takes the synchronised growth branch of launch_pictures (round-5 advisor: a small DMVR call,
+// a larger plain one and a medium DMVR one used to pass the old n / pics / dmvr test and grow the
+// jobs and DMVR buffers unsynchronised).
+static int ensure_slot_buffers(mm_ctx* c, PlanSlot& S, int n, bool dmvr, int pics = 1, bool* fits = nullptr) {
   PlanCaps k;
   pics = std::max(pics, S.pics_ensured);  // (buffers only grow)
   const long area_sb = (long)(c->geo.W / 4) * (c->geo.H / 4) * pics;  // each picture predicts each sample once
@@ -1953,54 +1972,66 @@ static int ensure_slot_buffers(mm_ctx* c, PlanSlot& S, int n, bool dmvr, int pic
   k.elems = 4 * k.sb;
   k.subs = subs;
   k.dmvr_elems = dmvr ? (int)std::min<long>((long)N_OFF * area_sb, (long)subs * N_OFF * 16) : 0;
-  S.caps = k;
+  if (fits) *fits = true;
+  // grow (or, dry run, check) one buffer; fresh: it was (re)allocated
+  auto need = [&](auto& b, size_t want, bool* fresh = nullptr) -> hipError_t {
+    if (fresh) *fresh = false;
+    if (fits) {
+      if (!b.p || want > b.cap) *fits = false;
+      return hipSuccess;
+    }
+    return b.ensure(c, want, fresh);
+  };
   if (dmvr) {
-    HIPCHK(c, S.dmvr_sub.ensure(c, k.subs));
-    HIPCHK(c, S.dmvr_off.ensure(c, k.subs));
-    HIPCHK(c, S.dmvr_chunk.ensure(c, (size_t)k.dmvr_elems / 64 + 1));
+    HIPCHK(c, need(S.dmvr_sub, k.subs));
+    HIPCHK(c, need(S.dmvr_off, k.subs));
+    HIPCHK(c, need(S.dmvr_chunk, (size_t)k.dmvr_elems / 64 + 1));
     // per slot, sized by the sub-PUs: centre setups and centre terms (2 x (56 + 44) B), delta, centre
     // cost, survivor index -- about 220 B per sub-PU (32 MB at 6144x3072; the other offsets' setups,
     // positions and costs of the survivors live in the search kernel's registers and LDS)
-    HIPCHK(c, S.dmvr_setup.ensure(c, (size_t)k.subs * 2));
-    HIPCHK(c, S.dmvr_cterms.ensure(c, (size_t)k.subs * 2));
-    HIPCHK(c, S.dmvr_mvd.ensure(c, 2 * (size_t)k.subs));
-    HIPCHK(c, S.dmvr_count.ensure(c, 1));
-    HIPCHK(c, S.dmvr_ccost.ensure(c, k.subs));
-    HIPCHK(c, S.dmvr_surv_s.ensure(c, k.subs));
-    S.dmvr_ensured = true;
+    HIPCHK(c, need(S.dmvr_setup, (size_t)k.subs * 2));
+    HIPCHK(c, need(S.dmvr_cterms, (size_t)k.subs * 2));
+    HIPCHK(c, need(S.dmvr_mvd, 2 * (size_t)k.subs));
+    HIPCHK(c, need(S.dmvr_count, 1));
+    HIPCHK(c, need(S.dmvr_ccost, k.subs));
+    HIPCHK(c, need(S.dmvr_surv_s, k.subs));
   }
   bool fresh_jobs = false;
-  HIPCHK(c, S.jobs.ensure(c, k.jobs, &fresh_jobs));
+  HIPCHK(c, need(S.jobs, k.jobs, &fresh_jobs));
   if (fresh_jobs) HIPCHK(c, hipMemsetAsync(S.jobs.p, 0, S.jobs.cap * sizeof(JobDev), c->stream));
-  HIPCHK(c, S.job_off.ensure(c, k.jobs));
-  HIPCHK(c, S.job_chunk.ensure(c, k.elems / 64 + 1));
-  HIPCHK(c, S.setup.ensure(c, k.jobs));
-  HIPCHK(c, S.meta.ensure(c, 1));
-  HIPCHK(c, S.blk.ensure(c, (size_t)((n + PLAN_BLOCK - 1) / PLAN_BLOCK) * N_KEYS));
-  HIPCHK(c, S.blkq.ensure(c, (size_t)((n + PLACE_BLOCK - 1) / PLACE_BLOCK) * N_KEYS));
+  HIPCHK(c, need(S.job_off, k.jobs));
+  HIPCHK(c, need(S.job_chunk, k.elems / 64 + 1));
+  HIPCHK(c, need(S.setup, k.jobs));
+  HIPCHK(c, need(S.meta, 1));
+  HIPCHK(c, need(S.blk, (size_t)((n + PLAN_BLOCK - 1) / PLAN_BLOCK) * N_KEYS));
+  HIPCHK(c, need(S.blkq, (size_t)((n + PLACE_BLOCK - 1) / PLACE_BLOCK) * N_KEYS));
   // The records k_reproj/k_mc exchange are zeroed once when allocated: every record a plan
   // counts is written before it is read (classify_pu decides counts and emission alike), and a
   // record that never was written still holds in-picture values (position 0, slot 0), never
   // uninitialised memory that k_mc would use as a destination offset.
   bool fresh = false;
-  HIPCHK(c, S.mc_meta.ensure(c, k.sb, &fresh));
+  HIPCHK(c, need(S.mc_meta, k.sb, &fresh));
   if (fresh) HIPCHK(c, hipMemsetAsync(S.mc_meta.p, 0, S.mc_meta.cap * sizeof(mm_int2), c->stream));
   for (int l = 0; l < 2; l++) {
-    HIPCHK(c, S.mc_lpos[l].ensure(c, k.sb, &fresh));
+    HIPCHK(c, need(S.mc_lpos[l], k.sb, &fresh));
     if (fresh) HIPCHK(c, hipMemsetAsync(S.mc_lpos[l].p, 0, S.mc_lpos[l].cap * sizeof(uint32_t), c->stream));
-    HIPCHK(c, S.mc_cpos[l].ensure(c, k.sb, &fresh));
+    HIPCHK(c, need(S.mc_cpos[l], k.sb, &fresh));
     if (fresh) HIPCHK(c, hipMemsetAsync(S.mc_cpos[l].p, 0, S.mc_cpos[l].cap * sizeof(uint32_t), c->stream));
     for (int q = 0; q < 2; q++) {  // touched only by the sub-blocks whose positions are far
-      HIPCHK(c, S.mc_far[l][q].ensure(c, k.sb, &fresh));
+      HIPCHK(c, need(S.mc_far[l][q], k.sb, &fresh));
       if (fresh) HIPCHK(c, hipMemsetAsync(S.mc_far[l][q].p, 0, S.mc_far[l][q].cap * sizeof(mm_int2), c->stream));
     }
   }
+  if (fits) return MM_OK;
+  S.caps = k;
+  if (dmvr) S.dmvr_ensured = true;
   S.n_ensured = std::max(S.n_ensured, n);
   S.pics_ensured = pics;
   return MM_OK;
 }
-static bool slot_fits(const PlanSlot& S, int n, bool dmvr, int pics = 1) {
-  return n <= S.n_ensured && pics <= S.pics_ensured && (!dmvr || S.dmvr_ensured);
+static bool slot_fits(mm_ctx* c, PlanSlot& S, int n, bool dmvr, int pics = 1) {
+  bool fits = false;
+  return ensure_slot_buffers(c, S, n, dmvr, pics, &fits) == MM_OK && fits;
 }
 
 // One stripe (PUs [base, base + n) of the picture's list) through k_plan_count + k_plan_place +
@@ -2010,7 +2041,7 @@ static bool slot_fits(const PlanSlot& S, int n, bool dmvr, int pics = 1) {
 static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables& t, const Geometry& geo,
                          const PuSegs& d_in, int n, int base, unsigned long long* status,
                          unsigned long long* next_status, const DstPlanes& dst, bool plan_ahead = false,
-                         bool want_mvd = false, hipEvent_t mc_done = nullptr) {
+                         bool want_mvd = false, hipEvent_t mc_done = nullptr, hipEvent_t* gate_out = nullptr) {
   // plan-ahead: `st` is the auxiliary stream for the planning kernels; the rest runs on the
   // context stream (which may be the null stream, so a flag, not a null handle, says so)
   hipStream_t st_back = c->stream;
@@ -2097,13 +2128,27 @@ static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[1], st));
   if (!reproj_ahead) reproj(st, nullptr);
   if (c->stage_timing) HIPCHK(c, hipEventRecord(c->ev_stage[2], st));
-  // mc_done (plan-ahead): the slot's gate, complete when this k_mc is
-  hipEvent_t stop = KERNEL_EVENTS ? mc_done : nullptr;
+  // mc_done (plan-ahead): the slot's gate, complete when this k_mc is; *gate_out = the event the
+  // slot's next planning waits for (mc_done, or the kernel-timing stop event bound to this k_mc)
+  hipEvent_t start = nullptr, stop = KERNEL_EVENTS ? mc_done : nullptr;
+  if (c->kt_on) {
+    hipEvent_t* pr = c->kt_ev[c->kt_n % mm_ctx::KT_RING];
+    start = pr[0];
+    stop = pr[1];
+    c->kt_n++;
+  }
   if (geo.hp)
-    hipExtLaunchKernelGGL(k_mc_dev<true>, dim3(gm), dim3(256), 0, st, nullptr, stop, 0, geo, S.meta.p, mc, t, dst);
+    hipExtLaunchKernelGGL(k_mc_dev<true>, dim3(gm), dim3(256), 0, st, start, stop, 0, geo, S.meta.p, mc, t, dst);
   else
-    hipExtLaunchKernelGGL(k_mc_dev<false>, dim3(gm), dim3(256), 0, st, nullptr, stop, 0, geo, S.meta.p, mc, t, dst);
-  if (mc_done && !KERNEL_EVENTS) HIPCHK(c, hipEventRecord(mc_done, st));
+    hipExtLaunchKernelGGL(k_mc_dev<false>, dim3(gm), dim3(256), 0, st, start, stop, 0, geo, S.meta.p, mc, t, dst);
+  if (mc_done && (c->kt_on || !KERNEL_EVENTS)) {
+    if (c->kt_on && gate_out)
+      *gate_out = stop;  // bound to this k_mc_dev: no marker packet in the timed loop
+    else
+      HIPCHK(c, hipEventRecord(mc_done, st));
+  } else if (gate_out) {
+    *gate_out = mc_done;
+  }
   HIPCHK(c, hipGetLastError());
   return MM_OK;
 }
@@ -2117,8 +2162,10 @@ static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables
 // only_list / hp / store: mm_pred_list (-1 / 0 / 3 for the normal prediction).
 // dmvr: MM_PUF_DMVR PUs allowed (the context's mm_set_dmvr, or mm_pred_dmvr); want_mvd: keep the
 // refined delta of every DMVR sub-PU, in placement order, in the slot's dmvr_mvd.
+// status_base: added to the PU index a validation failure reports (a run of a split multi-picture call)
 static int launch_pictures(mm_ctx* c, const mm_pic_job* pics, int n_pics, int only_list = -1, int hp = 0,
-                           int store = 3, bool may_plan_ahead = false, bool dmvr = false, bool want_mvd = false) {
+                           int store = 3, bool may_plan_ahead = false, bool dmvr = false, bool want_mvd = false,
+                           int status_base = 0) {
   std::vector<std::pair<int, RefDev>> refs;
   refs = ref_slots(c);
   PicTables t;
@@ -2177,7 +2224,7 @@ static int launch_pictures(mm_ctx* c, const mm_pic_job* pics, int n_pics, int on
   if (may_plan_ahead && c->plan_ahead && K == 1 && !c->stage_timing) {
     // Plan-ahead: planning + setup of this picture on `aux`, gated only by the k_mc_dev of the
     // slot's previous user (two calls back), so they overlap the previous picture's kernels.
-    if (!slot_fits(c->slot[0], per, dmvr, n_pics) || !slot_fits(c->slot[1], per, dmvr, n_pics)) {
+    if (!slot_fits(c, c->slot[0], per, dmvr, n_pics) || !slot_fits(c, c->slot[1], per, dmvr, n_pics)) {
       // growing frees buffers the other stream may still use, and zeroes on the context stream
       HIPCHK(c, hipStreamSynchronize(c->aux));
       HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -2187,11 +2234,12 @@ static int launch_pictures(mm_ctx* c, const mm_pic_job* pics, int n_pics, int on
       for (int s = 0; s < 2; s++) RCCHK(ensure_slot_buffers(c, c->slot[s], per, dmvr, n_pics));  // caps only
     }
     // the slot's previous user (two calls back) has finished its k_mc_dev
-    HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_gate[c->ahead_par], 0));
+    HIPCHK(c, hipStreamWaitEvent(c->aux, c->gate[c->ahead_par], 0));
     c->timed = c->call_timing;
     if (c->timed) HIPCHK(c, hipEventRecord(c->ev0, c->stream));
-    RCCHK(launch_stripe(c, c->slot[c->ahead_par], c->aux, t, geo, segs_of(0, n), n, 0, status, next_status, dst, true,
-                        want_mvd, c->ev_gate[c->ahead_par]));
+    RCCHK(launch_stripe(c, c->slot[c->ahead_par], c->aux, t, geo, segs_of(0, n), n, status_base, status, next_status, dst, true,
+                        want_mvd, c->ev_gate[c->ahead_par], &c->gate[c->ahead_par]));
+    c->last_slot = c->ahead_par;
     c->ahead_par ^= 1;
     if (c->timed) HIPCHK(c, hipEventRecord(c->ev1, c->stream));
     c->last_status = status;
@@ -2201,12 +2249,13 @@ static int launch_pictures(mm_ctx* c, const mm_pic_job* pics, int n_pics, int on
   }
   for (int s = 0; s < std::min(K, 2); s++) {
     // growth of buffers a plan-ahead call on the auxiliary stream may still use
-    if (!slot_fits(c->slot[s], per, dmvr, n_pics)) HIPCHK(c, hipStreamSynchronize(c->aux));
+    if (!slot_fits(c, c->slot[s], per, dmvr, n_pics)) HIPCHK(c, hipStreamSynchronize(c->aux));
     RCCHK(ensure_slot_buffers(c, c->slot[s], per, dmvr, n_pics));
   }
   // each event a call records costs the context stream ~4 us (profiles/r03_ab_event_scope.txt)
   c->timed = c->call_timing || c->stage_timing;
   if (c->timed) HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+  c->last_slot = 0;
   if (K > 1) {
     HIPCHK(c, hipEventRecord(c->ev_fork, c->stream));
     HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_fork, 0));
@@ -2214,7 +2263,7 @@ static int launch_pictures(mm_ctx* c, const mm_pic_job* pics, int n_pics, int on
   for (int s = 0; s < K; s++) {
     const int base = s * per, m = std::min(per, n - base);
     if (m <= 0) break;
-    RCCHK(launch_stripe(c, c->slot[s & 1], (s & 1) ? c->aux : c->stream, t, geo, segs_of(base, m), m, base, status,
+    RCCHK(launch_stripe(c, c->slot[s & 1], (s & 1) ? c->aux : c->stream, t, geo, segs_of(base, m), m, status_base + base, status,
                         s == 0 ? next_status : nullptr, dst, false, want_mvd));
   }
   if (K > 1) {
@@ -2227,6 +2276,8 @@ static int launch_pictures(mm_ctx* c, const mm_pic_job* pics, int n_pics, int on
   if (c->plan_ahead) {  // both slots may have been used by this call's stripes
     HIPCHK(c, hipEventRecord(c->ev_gate[0], c->stream));
     HIPCHK(c, hipEventRecord(c->ev_gate[1], c->stream));
+    c->gate[0] = c->ev_gate[0];
+    c->gate[1] = c->ev_gate[1];
   }
   c->last_status = status;
   c->pic_par ^= 1;
@@ -2248,6 +2299,8 @@ int mm_set_plan_ahead(mm_ctx* c, int on) {
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipEventRecord(c->ev_gate[0], c->stream));
     HIPCHK(c, hipEventRecord(c->ev_gate[1], c->stream));
+    c->gate[0] = c->ev_gate[0];
+    c->gate[1] = c->ev_gate[1];
   }
   c->plan_ahead = on != 0;
   return MM_OK;
@@ -2307,7 +2360,24 @@ int mm_pred_device_multi(mm_ctx* c, const mm_pic_job* pics, int n_pics) {
   if (n > INT32_MAX / 2) return MM_ERR_ARG;
   if (n == 0) return MM_OK;
   HIPCHK(c, hipSetDevice(c->device));
-  return launch_pictures(c, pics, n_pics, -1, 0, 3, true, c->dmvr);
+  // One launch chain holds MAX_SLOTS distinct camera-pose epipoles (PicTables::ged): pictures whose
+  // (cur, ref) epipoles together exceed that are cut into consecutive runs, each its own chain
+  // (round-5 advisor: four RA leaves with five distinct references each used to fail the call).
+  const auto refs = ref_slots(c);
+  int cur[MAX_PICS];
+  for (int q = 0; q < n_pics; q++) cur[q] = pics[q].cur_poc;
+  // A run's deferred status word is overwritten by the next run's planning, so every run but the last
+  // is checked before the next one is issued (host synchronisation only on this rare path).
+  int pu_base = 0;
+  for (int q0 = 0; q0 < n_pics;) {
+    int q1 = q0 + 1;
+    while (q1 < n_pics && count_cam_epipoles(c->epipoles, cur + q0, q1 + 1 - q0, refs) <= MAX_SLOTS) q1++;
+    RCCHK(launch_pictures(c, pics + q0, q1 - q0, -1, 0, 3, true, c->dmvr, false, pu_base));
+    if (q1 < n_pics) RCCHK(read_status(c, nullptr));
+    for (int q = q0; q < q1; q++) pu_base += pics[q].n;
+    q0 = q1;
+  }
+  return MM_OK;
 }
 
 int mm_set_dmvr(mm_ctx* c, int on) {
@@ -2452,9 +2522,11 @@ int mm_pred_dmvr(mm_ctx* c, int cur_poc, const mm_pu_desc* pus, int n, int16_t* 
   const int rc = read_status(c, nullptr);
   if (rc) return rc;
   // the deltas of the sub-PUs in placement order: PUs in list order (DMVR bucket placement keeps
-  // input order), sub-PUs in raster order
+  // input order), sub-PUs in raster order -- in the plan slot the call used (slot 0 while this call
+  // runs without plan-ahead and DMVR keeps one stripe, but read from where it actually went)
   if (mvd_out && n_sub)
-    HIPCHK(c, hipMemcpy(mvd_out, c->slot[0].dmvr_mvd.p, 2 * (size_t)n_sub * sizeof(int32_t), hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(mvd_out, c->slot[c->last_slot].dmvr_mvd.p, 2 * (size_t)n_sub * sizeof(int32_t),
+                        hipMemcpyDeviceToHost));
   return MM_OK;
 }
 
@@ -2620,6 +2692,44 @@ int mm_last_stage_timing(mm_ctx* c, float ms[4]) {
   HIPCHK(c, hipEventSynchronize(c->ev1));
   hipEvent_t e[5] = {c->ev0, c->ev_stage[0], c->ev_stage[1], c->ev_stage[2], c->ev1};
   for (int i = 0; i < 4; i++) HIPCHK(c, hipEventElapsedTime(&ms[i], e[i], e[i + 1]));
+  return MM_OK;
+}
+
+int mm_set_kernel_timing(mm_ctx* c, int on) {
+  if (!c) return MM_ERR_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (on && !c->kt_ev[0][0]) {
+    // timing events without the system-scope release (they publish nothing, like the slot gates)
+    for (auto& pr : c->kt_ev)
+      for (auto& e : pr) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+  }
+  if (!on && c->kt_on && c->plan_ahead) {
+    // the gates may point into the ring: gate on the current position of the context stream again
+    HIPCHK(c, hipEventRecord(c->ev_gate[0], c->stream));
+    HIPCHK(c, hipEventRecord(c->ev_gate[1], c->stream));
+    c->gate[0] = c->ev_gate[0];
+    c->gate[1] = c->ev_gate[1];
+  }
+  c->kt_on = on != 0;
+  c->kt_n = 0;
+  return MM_OK;
+}
+
+int mm_kernel_times(mm_ctx* c, float* ms, int cap, int* n_out) {
+  if (!c || !n_out || cap < 0 || (cap > 0 && !ms)) return MM_ERR_ARG;
+  *n_out = 0;
+  if (!c->kt_ev[0][0]) return fail(c, MM_ERR_ARG, "kernel timing was never on (mm_set_kernel_timing)");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const int n = std::min(c->kt_n, mm_ctx::KT_RING);
+  const int first = c->kt_n - n;  // the last n launches, oldest first
+  int k = 0;
+  for (int i = 0; i < n && k < cap; i++, k++) {
+    hipEvent_t* pr = c->kt_ev[(first + i) % mm_ctx::KT_RING];
+    HIPCHK(c, hipEventElapsedTime(&ms[k], pr[0], pr[1]));
+  }
+  *n_out = k;
+  c->kt_n = 0;
   return MM_OK;
 }
 

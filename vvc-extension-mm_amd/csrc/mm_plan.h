@@ -254,6 +254,20 @@ inline int build_pic_tables(const SeqInfo& s, const EpipoleMap& epi, const int* 
   }
   return MM_OK;
 }
+// Distinct camera-pose epipoles the pictures cur_pocs[0..n) need against the resident references:
+// one call's rotation table holds MAX_SLOTS of them (a single picture never needs more, it has at
+// most MAX_SLOTS references), so mm_pred_device_multi cuts its pictures into runs that fit.
+inline int count_cam_epipoles(const EpipoleMap& epi, const int* cur_pocs, int n,
+                              const std::vector<std::pair<int, RefDev>>& refs) {
+  std::vector<std::array<int32_t, 3>> used;
+  for (const auto& r : refs)
+    for (int q = 0; q < n; q++) {
+      std::array<int32_t, 3> e;
+      if (find_epipole(epi, cur_pocs[q], r.first, &e) && std::find(used.begin(), used.end(), e) == used.end())
+        used.push_back(e);
+    }
+  return (int)used.size();
+}
 inline int build_pic_tables(const SeqInfo& s, const EpipoleMap& epi, int cur_poc,
                             const std::vector<std::pair<int, RefDev>>& refs, mmdev::PicTables* t,
                             std::string* err) {

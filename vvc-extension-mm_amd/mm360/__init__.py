@@ -58,7 +58,7 @@ EXPORTED_SYMBOLS = (
     "mm_set_stripes", "mm_set_plan_ahead", "mm_pred_list", "mm_derive_effective_blocks", "mm_epipole_list_create",
     "mm_epipole_list_destroy", "mm_get_epipole_list", "mm_epipole_add", "mm_epipole_make_available", "mm_epipole_has",
     "mm_epipole_find", "mm_epipole_derive_predictor", "mm_epipole_count", "mm_mvp_convert_device", "mm_mvp_status", "mm_set_dmvr",
-    "mm_set_mvp_stream", "mm_mvp_convert_host", "mm_pred_device_multi",
+    "mm_set_mvp_stream", "mm_mvp_convert_host", "mm_pred_device_multi", "mm_set_kernel_timing", "mm_kernel_times",
 )
 
 BCW_DEFAULT = 2  # CommonDef.h:348-349; g_BcwWeights = {-2, 3, 4, 5, 10} (Rom.cpp:203)
@@ -186,6 +186,8 @@ def load_library() -> ctypes.CDLL:
         "mm_pred_dmvr": (c_int, [vp, c_int, vp, c_int, vp, ctypes.c_ssize_t, vp, vp, ctypes.c_ssize_t, vp]),
         "mm_sad_window": (c_int, [vp, c_int, vp, c_int, c_int, c_int, vp]),
         "mm_last_stage_timing": (c_int, [vp, POINTER(c_float)]),
+        "mm_set_kernel_timing": (c_int, [vp, c_int]),
+        "mm_kernel_times": (c_int, [vp, POINTER(c_float), c_int, POINTER(c_int)]),
         "mm_set_stripes": (c_int, [vp, c_int]),
         "mm_set_plan_ahead": (c_int, [vp, c_int]),
         "mm_pred_list": (c_int, [vp, c_int, vp, c_int, c_int, c_int, vp, ctypes.c_ssize_t, vp, vp,
@@ -570,6 +572,17 @@ class MMContext:
         ms = (c_float * 4)()
         self._check(self.lib.mm_last_stage_timing(self.h, ms))
         return tuple(float(v) for v in ms)
+
+    def set_kernel_timing(self, on: bool):
+        """mm_set_kernel_timing: k_mc_dev launches bracketed by kernel-bound events while on."""
+        self._check(self.lib.mm_set_kernel_timing(self.h, int(on)))
+
+    def kernel_times_ms(self):
+        """mm_kernel_times: k_mc_dev durations (ms) of the launches since the last read, oldest first."""
+        ms = (c_float * 256)()
+        n = c_int(0)
+        self._check(self.lib.mm_kernel_times(self.h, ms, 256, ctypes.byref(n)))
+        return [float(ms[i]) for i in range(n.value)]
 
     # -- encoder motion search (InterSearch::xMVReprojectionInterpolation + RdCost::xGetSAD) -
     def upload_org(self, poc: int, y):
