@@ -275,9 +275,16 @@ def bench_pictures(args, cfg, params, rank, world, local, dist):
     traffic, traffic_src = measured_traffic(args, args.config)
     mvp = None
     if args.config == "C3" and not args.no_mvp:
-        mvp = mvp_per_picture(ctx, cfg, int(np.mean([len(p) for _, p, _ in pictures])), params,
+        mvp = mvp_per_picture(ctx, cfg, int(np.mean([list_uses(p) for _, p, _ in pictures])), params,
                               [(cur, -1, W.GED_EPIPOLE_Q24) for cur, _, _ in pictures])
         mvp["in_loop"] = mvp_in_loop(args, ctx, cfg, pictures, d_pus, outs, area)
+        sp = mvp["spatial_host"]
+        par = sp[f"ms_per_picture_{sp['threads']}_threads"]
+        mvp["decoder_bound_ms_per_picture"] = {
+            "value": round(max(mvp["in_loop"]["ms_per_picture"], par), 4),
+            "note": f"max of the GPU loop with the TMVP batches ({mvp['in_loop']['ms_per_picture']} ms) and the "
+                    f"host's spatial conversions on {sp['threads']} threads ({par} ms), which overlap the GPU work "
+                    f"of earlier pictures in a decoder"}
 
     multi = None
     if (args.config == "C3" and world == 1 and args.dmvr_share == 0 and args.uniform_model is None and P_ >= 2
@@ -390,14 +397,26 @@ def dmvr_record(args, cfg, params, share=0.3, steps=12, warmup=3, correlated=Fal
                     "survivors' search) and k_setup_dev; not part of value"}
 
 
-def mvp_per_picture(ctx, cfg, n_pus, params, epipoles, reps=10):
-    """MM-MVP (mm_mvp_convert_device) beside the C3 number, outside its timed
-    region: one conversion per PU and list (2 x PUs queries, the seeded query mix tiled), queries
-    and results resident in HBM, stream-ordered on the context stream; device time of each call
-    from HIP events around its launch (mm_last_timing), and wall time per call over `reps`
-    back-to-back calls.  The synchronous host-buffer call (PCIe copies in and out) is reported
-    beside it."""
-    q = np.resize(W.mvp_queries(cfg.width, cfg.height, cfg.models, 20000, seed=5), 2 * n_pus)
+def list_uses(pus):
+    """(PU, used list) pairs of a PU list."""
+    return int((pus["ref_poc"] >= 0).sum())
+
+
+def mvp_per_picture(ctx, cfg, n_uses, params, epipoles, reps=10):
+    """MM-MVP beside the C3 number, outside its timed region, split the way a
+    decoder binds it (MVP): per PU and used list, two spatial candidates (the left and
+    above neighbours of addMVPCandUnscaled / the merge list, UnitTools.cpp:2930-2992, 3134-3167) that
+    convert a neighbour's FINAL MV and so run one at a time in decoding order on the host
+    (mm_mvp_convert_host), and one collocated (TMVP) candidate (UnitTools.cpp:2267-2304) whose
+    picture's worth is converted as one device batch (mm_mvp_convert_device, queries and results
+    resident in HBM).  Host: one thread over the picture's spatial queries, and 16 threads (the
+    per-GPU share of the box's host) each converting a run of CTU rows with its own epipole list --
+    the WPP-style parallelism a decoder has -- wall time.  Device: kernel time (HIP events) and wall
+    time per call over `reps` back-to-back calls; the synchronous host-buffer call beside it."""
+    from concurrent.futures import ThreadPoolExecutor
+    n_sp, n_tm = 2 * n_uses, n_uses
+    q_sp = np.resize(W.mvp_queries(cfg.width, cfg.height, cfg.models, 20000, seed=3), n_sp)
+    q = np.resize(W.mvp_queries(cfg.width, cfg.height, cfg.models, 20000, seed=5), n_tm)
     d_q = mm360.queries_to_device(q)
     d_out = torch.zeros((len(q), 2), dtype=torch.int32, device="cuda")
     ctx.mvp_convert_device(d_q, d_out)  # warm-up (epipole table upload)
@@ -420,31 +439,53 @@ def mvp_per_picture(ctx, cfg, n_pus, params, epipoles, reps=10):
         t0 = time.perf_counter()
         ctx.mvp_convert(q)
         host = min(host, time.perf_counter() - t0)
-    # the host per-query form (mm_mvp_convert_host: the spatial merge / AMVP candidates, converted one at
-    # a time in decoding order, UnitTools.cpp:2930-2992, 3134-3167) on this thread: the picture's
-    # queries in one call, so the time per query is the conversion's own cost (a C++ decoder calls it
-    # per candidate; a ctypes call per query from Python would time the binding instead)
+    # spatial candidates on the host: the picture's queries in one call per thread, so the time per
+    # query is the conversion's own cost (a C++ decoder calls it per candidate; a ctypes call per query
+    # from Python would time the binding instead)
     epi = ctx.epipole_list()
-    mm360.mvp_convert_host(params, q[:1000], epi)
+    mm360.mvp_convert_host(params, q_sp[:1000], epi)
     t0 = time.perf_counter()
-    host_mv = mm360.mvp_convert_host(params, q, epi)
-    host_us = (time.perf_counter() - t0) / len(q) * 1e6
-    # check (after timing): the timed device conversions and the host form against the oracle
+    host_mv = mm360.mvp_convert_host(params, q_sp, epi)
+    host1 = time.perf_counter() - t0
+    threads = cpu_threads()
+    lists = []
+    for _ in range(threads):
+        e = mm360.EpipoleList()
+        for cur, ref, qq in epipoles:
+            e.add(cur, ref, qq, True)
+        lists.append(e)
+    chunks = np.array_split(np.arange(n_sp), threads)
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(lambda k: mm360.mvp_convert_host(params, q_sp[chunks[k][:100]], lists[k]), range(threads)))
+        t0 = time.perf_counter()
+        parts = list(ex.map(lambda k: mm360.mvp_convert_host(params, q_sp[chunks[k]], lists[k]), range(threads)))
+        host_n = time.perf_counter() - t0
+    host_par = np.concatenate(parts)
+    # check (after timing): the timed device conversions and both host forms against the oracle
     from oracle.oracle import Oracle
-    want = Oracle(params, epipoles).mvp(q)
+    orc = Oracle(params, epipoles)
+    want, want_sp = orc.mvp(q), orc.mvp(q_sp)
     bad = int((got != want).any(axis=1).sum())
-    bad_host = int((host_mv != want).any(axis=1).sum())
-    return {"queries_per_picture": int(len(q)), "ms_per_picture": round(wall * 1e3, 4),
-            "kernel_ms": round(float(np.mean(dev)), 4), "host_buffer_call_ms": round(host * 1e3, 4),
+    bad_host = int((host_mv != want_sp).any(axis=1).sum()) + int((host_par != want_sp).any(axis=1).sum())
+    return {"queries_per_picture": {"spatial": int(n_sp), "tmvp": int(n_tm)},
+            "query_model": "per PU and used list: 2 spatial candidates (left, above) converted on the host in "
+                           "decoding order + 1 collocated (TMVP) candidate converted in the picture's device batch",
+            "spatial_host": {"ms_per_picture_1_thread": round(host1 * 1e3, 3),
+                             "us_per_query": round(host1 / n_sp * 1e6, 3),
+                             f"ms_per_picture_{threads}_threads": round(host_n * 1e3, 3), "threads": threads,
+                             "note": "mm_mvp_convert_host (the product's model bodies compiled for the host, no "
+                                     "oracle); the threads split the picture's queries in CTU-row runs, each with "
+                                     "its own epipole list (WPP-style); wall time"},
+            "tmvp_device": {"ms_per_picture": round(wall * 1e3, 4), "kernel_ms": round(float(np.mean(dev)), 4),
+                            "host_buffer_call_ms": round(host * 1e3, 4)},
             "bit_exact": bad == 0 and bad_host == 0, "mismatching_queries": bad + bad_host,
-            "bit_exact_sample": "the last timed device call's MVs and the host per-query form's, vs the oracle",
-            "host_per_query_us": round(host_us, 3), "host_per_query_cores": 1,
-            "note": "device-resident queries (mm_mvp_convert_device), back-to-back calls; host_per_query_us: "
-                    "mm_mvp_convert_host on one host thread (spatial candidates); not part of value"}
+            "bit_exact_sample": "the last timed device batch and both host forms' MVs, vs the oracle",
+            "host_per_query_us": round(host1 / n_sp * 1e6, 3), "host_per_query_cores": 1,
+            "note": "not part of value; in_loop: C3 with the TMVP batches on their own stream"}
 
 
 def mvp_in_loop(args, ctx, cfg, pictures, d_pus, outs, area):
-    """C3 with MM-MVP in the decode loop: a picture's conversions (one per PU and list, one batch)
+    """C3 with MM-MVP in the decode loop: a picture's TMVP conversions (one per PU and used list, one batch)
     run on their own stream (mm_set_mvp_stream), two pictures ahead, while earlier pictures are
     predicted on the context stream; a picture's PU list depends on its conversions, so before its
     prediction call is issued the host waits for them (the plan-ahead contract: a call's list is
@@ -455,7 +496,7 @@ def mvp_in_loop(args, ctx, cfg, pictures, d_pus, outs, area):
     (merge lists that chain, UnitTools.cpp:2269-2302, convert in dependent batches): device time of
     the call and host wall time of the synchronous host-buffer call."""
     P_ = len(pictures)
-    qs = [np.resize(W.mvp_queries(cfg.width, cfg.height, cfg.models, 20000, seed=11 + f), 2 * len(p))
+    qs = [np.resize(W.mvp_queries(cfg.width, cfg.height, cfg.models, 20000, seed=11 + f), list_uses(p))
           for f, (_, p, _) in enumerate(pictures)]
     d_q = [mm360.queries_to_device(q) for q in qs]
     d_o = [torch.zeros((len(q), 2), dtype=torch.int32, device="cuda") for q in qs]
@@ -806,15 +847,24 @@ def c5_record(args, steps=3, warmup=1):
 
     elapsed = timed(steps, warmup, step, None)
     got = sads.cpu().numpy().view(np.uint32)
+    tz = tz_step_record(ctx, blocks)
     ctx.close()
     rng = np.random.default_rng(0x4D4D8000)
     pick = np.sort(rng.choice(len(blocks), size=48, replace=False))
     bit_exact = None
     if not args.no_cpu_baseline:
         from oracle.oracle import Oracle
-        want = Oracle(params, [(W.CUR_POC, -1, W.GED_EPIPOLE_Q24)]).sad_window(
-            W.CUR_POC, blocks[pick], W.ME_RANGE, 16, {poc: r[0] for poc, r in refs.items()}, org)
+        orc = Oracle(params, [(W.CUR_POC, -1, W.GED_EPIPOLE_Q24)])
+        want = orc.sad_window(W.CUR_POC, blocks[pick], W.ME_RANGE, 16, {poc: r[0] for poc, r in refs.items()}, org)
         bit_exact = bool(np.array_equal(got[pick], want))
+        tz_pick = (pick[:, None] * 8 + np.arange(8)[None, :]).ravel()
+        tz_want = orc.sad_window(W.CUR_POC, tz.pop("_blocks")[tz_pick], 0, 16,
+                                 {poc: r[0] for poc, r in refs.items()}, org)
+        tz["bit_exact"] = bool(np.array_equal(tz.pop("_sads")[tz_pick], tz_want))
+        tz["bit_exact_sample"] = f"{len(pick)} seeded blocks x 8 candidates vs the oracle"
+    else:
+        tz.pop("_blocks")
+        tz.pop("_sads")
     bound = None  # the committed PMC profile of this very library, if any (tools/c5_pmc_json.py)
     lib_sha = hashlib.sha256(open(mm360.LIB_PATH, "rb").read()).hexdigest()
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_c5_pmc.json")), reverse=True):
@@ -825,11 +875,45 @@ def c5_record(args, steps=3, warmup=1):
             break
     n_cand = len(blocks) * C
     return {"workload": f"C5: {cfg.description}", "blocks": int(len(blocks)), "candidates": int(n_cand),
+            "tz_step": tz,
             "value": round(n_cand * steps / elapsed / 1e6, 2), "unit": "Mcandidates/s",
             "ms_per_window_set": round(elapsed / steps * 1e3, 3),
             "kernel_ms": round(float(np.mean(kms[warmup:])), 3),
             "bit_exact": bit_exact, "bit_exact_sample": f"{len(pick)} seeded blocks x {C} candidates vs the oracle",
             "bound": bound}
+
+
+TZ_SQUARE = ((-1, -1), (0, -1), (1, -1), (-1, 0), (1, 0), (-1, 1), (0, 1), (1, 1))  # InterSearch.cpp:492-526
+
+
+def tz_step_record(ctx, blocks, dist=2, reps=5):
+    """The encoder's dependent call pattern (InterSearch.cpp:474-526, xTZ8PointSquareSearch via
+    xTZSearchHelp): ONE TZ 8-point square step at distance `dist` around every block's current best
+    (here the C5 window centre) for every PU x model of the C5 picture -- 8 range-0 candidates per
+    block through mm_sad_window -- as one device round trip including the host's wait for the SADs
+    (the next step's start points depend on them).  Time per step, and the steps an encoder could
+    afford per picture in a 30 fps budget."""
+    b8 = np.repeat(blocks, 8)
+    off = np.tile(np.array(TZ_SQUARE, dtype=np.int32), (len(blocks), 1)) * (16 * dist)
+    b8["mv_hor"] += off[:, 0]
+    b8["mv_ver"] += off[:, 1]
+    out = torch.zeros((len(b8), 1), dtype=torch.int32, device="cuda")
+    ctx.sad_window(W.CUR_POC, b8, 0, 16, out=out)  # warm-up (buffers)
+    res = out.cpu()
+    t = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        ctx.sad_window(W.CUR_POC, b8, 0, 16, out=out)
+        res = out.cpu()  # the host needs the SADs to pick the next step's start points
+        t.append(time.perf_counter() - t0)
+    ms = float(np.median(t)) * 1e3
+    return {"candidates": int(len(b8)), "blocks": int(len(blocks)), "distance": dist,
+            "ms_per_step": round(ms, 3), "device_ms": round(ctx.last_timing_ms(), 3),
+            "steps_per_33ms": int(33.3 / ms),
+            "note": "one xTZ8PointSquareSearch step for every PU x model of the picture as one mm_sad_window "
+                    "call of range-0 blocks + the SAD copy to the host, median of the calls; steps_per_33ms: "
+                    "dependent steps a 30 fps encoder could afford per picture on this path alone",
+            "_blocks": b8, "_sads": res.numpy().view(np.uint32).ravel()}
 
 
 def bench_me(args, cfg, params, rank, world, local, dist):

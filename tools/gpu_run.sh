@@ -62,6 +62,9 @@ for step in "$@"; do
     pmc=*)  # pmc=<tag>=<counter,counter,...>: one rocprofv3 --pmc pass over a short bench run
       tag=$(echo "$step" | cut -d= -f2); ctrs=$(echo "$step" | cut -d= -f3 | tr ',' ' ')
       run "pmc_$tag" 600 rocprofv3 --pmc $ctrs -d "gpurun_out/pmc_$tag" -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 --no-mvp --no-c5 --no-dmvr --no-multi ;;
+    pmcv=*)  # pmcv=<tag>=<counter,...>=<v1,v2,...>: one rocprofv3 --pmc pass per library variant (default = in-tree)
+      tag=$(echo "$step" | cut -d= -f2); ctrs=$(echo "$step" | cut -d= -f3 | tr ',' ' '); vs=$(echo "$step" | cut -d= -f4 | tr ',' ' ')
+      run "pmcv_$tag" 600 bash tools/pmc_variant.sh "$tag" "$ctrs" $vs ;;
     pmcd=*)  # pmcd=<tag>=<counter,...>: one rocprofv3 --pmc pass over a short C3 run with a 30 % MM-DMVR share
       tag=$(echo "$step" | cut -d= -f2); ctrs=$(echo "$step" | cut -d= -f3 | tr ',' ' ')
       run "pmcd_$tag" 600 rocprofv3 --pmc $ctrs -d "gpurun_out/pmcd_$tag" -o run --output-format csv -- python3 bench.py --dmvr-share 0.3 --steps 3 --warmup 1 --no-cpu-baseline --kernel-steps 1 --no-mvp --no-c5 ;;
