@@ -580,13 +580,48 @@ def bench_c4(args, cfg, params, rank, world, local, dist):
     bufs = [torch.zeros(lay.total, dtype=torch.int16, device="cuda") for _ in range(n_bufs)]
     ptrs = [lay.dst_pointers(b.data_ptr(), rank) for b in bufs]
     area = W.luma_area(pus)
+    # packed transport (include/mm360.h): each rank packs its int16 segment (3 samples per word at 10
+    # bits), the all-gather moves 2/3 of the bytes, and every rank unpacks a gathered picture straight
+    # into a reference pool slot (margins included) when a picture that references it is predicted --
+    # the decoder's "reconstructed picture becomes a reference" step, so its cost is in the loop
+    pack = bool(args.c4_pack) and world > 1
+    nw = ctx.stripe_packed_dwords(world)
+    pbufs = [torch.zeros(world * nw, dtype=torch.int32, device="cuda") for _ in range(n_bufs)] if pack else []
+    ref_fifo = []  # POCs of the gathered pictures uploaded as references (released after 6)
 
     def mc_only(s):
         ctx.run_raw(*ptrs[s % 2])
 
+    class Gathered:
+        """a packed all-gather in flight: waiting for it also unpacks it into the pool, once"""
+        serial = [0]
+
+        def __init__(self, h, b):
+            self.h, self.b, self.done = h, b, False
+
+        def wait(self):
+            if self.h is not None:
+                self.h.wait()
+            if not self.done:
+                self.done = True
+                Gathered.serial[0] += 1
+                poc = 100000 + Gathered.serial[0]
+                ctx.upload_ref_packed(poc, pbufs[self.b], world)
+                ref_fifo.append(poc)
+                if len(ref_fifo) > 6:
+                    ctx.release_ref(ref_fifo.pop(0))
+
     def gather(b):
         if world == 1:
             return None  # the whole picture is already here
+        if pack:
+            ctx.pack_samples(bufs[b][rank * lay.seg:(rank + 1) * lay.seg], pbufs[b][rank * nw:(rank + 1) * nw])
+            if args.dist_backend == "nccl":
+                return Gathered(P.allgather_packed(pbufs[b], lay, async_op=True), b)
+            host = pbufs[b].cpu()  # gloo rehearsal: host staging, synchronous
+            P.allgather_packed(host, lay)
+            pbufs[b].copy_(host)
+            return Gathered(None, b)
         if args.dist_backend == "nccl":
             return P.allgather_packed(bufs[b], lay, async_op=True)
         host = bufs[b].cpu()  # gloo rehearsal: host staging, synchronous
@@ -644,6 +679,8 @@ def bench_c4(args, cfg, params, rank, world, local, dist):
         h.wait()
     torch.cuda.synchronize()
     ctx.synchronize()
+    gathered_pic = (P.unpack_picture(pbufs[0].cpu().numpy().view(np.uint32), lay, params.bit_depth) if pack
+                    else lay.unpack(bufs[0].cpu().numpy()))
     # stage timing of this rank's stripe
     ctx.set_stage_timing(True)
     stages = []
@@ -660,10 +697,10 @@ def bench_c4(args, cfg, params, rank, world, local, dist):
         from oracle.oracle import Oracle
         orc = Oracle(params, [(cur, -1, W.GED_EPIPOLE_Q24)])
         want = orc.predict_padded(orc.padded_refs(refs), cur, pus, cfg.width, cfg.height, cpu_threads())
-        got = lay.unpack(bufs[0].cpu().numpy())  # (buffer 0 was last written by the gathered check picture)
-        bit_exact = all(np.array_equal(g, w) for g, w in zip(got, want))
+        # buffer 0 was last written by the gathered check picture
+        bit_exact = all(np.array_equal(g, w) for g, w in zip(gathered_pic, want))
     if rank == 0:
-        ag_bytes = (world - 1) * lay.seg * 2
+        ag_bytes = (world - 1) * (nw * 4 if pack else lay.seg * 2)
         per = lambda t: {"value": round(area * args.steps / t / 1e6, 2), "ms_per_step": round(t / args.steps * 1e3, 4)}
         print(json.dumps({
             "metric": METRIC, "value": round(area * args.steps / t_e2e / 1e6, 2), "unit": "Mpixels/s",
@@ -680,6 +717,9 @@ def bench_c4(args, cfg, params, rank, world, local, dist):
                        "width": cfg.width, "height": cfg.height,
                        "pus": int(len(pus)), "pus_rank0": int(len(mine)), "luma_area": int(area),
                        "stripe_ctu_rows": lay.rows // 128, "allgather_bytes_in_per_rank": int(ag_bytes),
+                       "transport": ("packed: 3 samples per 32-bit word (mm_pack_samples), unpacked into the "
+                                     "reference pool on every rank when a picture references it "
+                                     "(mm_upload_ref_packed)" if pack else "int16 samples"),
                        "gop": "ra32", "timed_pictures": "decode-order pictures 0..steps-1 of a GOP",
                        "plan_ahead": bool(args.plan_ahead), "parallelism": f"ctu-row stripes x{world}"},
             "ra_gop8": dict(per(results["ra8"]), note="same loop, dyadic hierarchical-B GOP-8 decode order"),
@@ -745,15 +785,47 @@ def bench_c4_emulate(args, cfg, params):
         mc = worst * 1e3
         dep = {f"{g}{'_all' if every else ''}_{k}": round(G.schedule(64, mc, a * 1e3, g, every)["ms_per_picture"], 4)
                for g in ("ra32", "ra8") for every in (False, True) for k, a in (("ring", ring), ("mesh", mesh))}
+        # packed transport: measured pack (one rank's segment) and unpack-into-the-pool (the gathered
+        # picture) kernels on this GPU, around the modelled all-gather of the packed segments
+        lay = P.StripeLayout(cfg.width, cfg.height, n)
+        nw = ctx.stripe_packed_dwords(n)
+        seg = torch.zeros(lay.seg, dtype=torch.int16, device="cuda")
+        pk = torch.zeros(n * nw, dtype=torch.int32, device="cuda")
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ctx.pack_samples(seg, pk[:nw])
+        ctx.upload_ref_packed(999, pk, n)
+        e0.record()
+        for _ in range(10):
+            ctx.pack_samples(seg, pk[:nw])
+        e1.record()
+        e1.synchronize()
+        pack_ms = e0.elapsed_time(e1) / 10
+        e0.record()
+        for _ in range(10):
+            ctx.upload_ref_packed(999, pk, n)
+        e1.record()
+        e1.synchronize()
+        unpack_ms = e0.elapsed_time(e1) / 10
+        ctx.release_ref(999)
+        ag_p = (n - 1) * nw * 4
+        ring_p = pack_ms + ag_p / link * 1e3 + unpack_ms
+        mesh_p = pack_ms + ag_p / (7 * link) * 1e3 + unpack_ms
+        dep_p = {f"ra32_packed_{k}": round(G.schedule(64, mc, a, "ra32")["ms_per_picture"], 4)
+                 for k, a in (("ring", ring_p), ("mesh", mesh_p))} if n > 1 else {}
         out["n"][n] = {"mc_ms": round(mc, 4), "host_issue_ms": round(issue * 1e3, 4),
                        "allgather_ms": {"ring": round(ring * 1e3, 4), "mesh": round(mesh * 1e3, 4)},
+                       "packed": {"pack_ms": round(pack_ms, 4), "unpack_into_pool_ms": round(unpack_ms, 4),
+                                  "allgather_bytes_in": int(ag_p), "int16_bytes_in": int(ag),
+                                  "transfer_ms": {"ring": round(ring_p, 4), "mesh": round(mesh_p, 4)},
+                                  "note": "pack + modelled all-gather of the packed segments + unpack into the "
+                                          "reference pool, the dependent picture's wait"},
                        "pred_ms_per_picture": {"hidden_ring": round(max(worst, ring) * 1e3, 4),
                                                "hidden_mesh": round(max(worst, mesh) * 1e3, 4),
-                                               "serial_ring": round((worst + ring) * 1e3, 4), **dep},
+                                               "serial_ring": round((worst + ring) * 1e3, 4), **dep, **dep_p},
                        "pred_mpix_s": {"hidden_ring": round(area / max(worst, ring) / 1e6, 1),
                                        "hidden_mesh": round(area / max(worst, mesh) / 1e6, 1),
                                        "mc_only": round(area / worst / 1e6, 1),
-                                       **{k: round(area / (v * 1e-3) / 1e6, 1) for k, v in dep.items()}}}
+                                       **{k: round(area / (v * 1e-3) / 1e6, 1) for k, v in {**dep, **dep_p}.items()}}}
     # Independent pictures (one temporal layer of the RA GOP) in flight together: k contexts, each
     # with its own stream and resident references, predicting rank 0's stripe concurrently, so that
     # several 1/N-picture launch chains share the GPU.  ms per stripe = elapsed / (steps x k).
@@ -801,7 +873,8 @@ def bench_c4_emulate(args, cfg, params):
         ratio = multi[n][2] / multi[n][1]
         e = out["n"][n]
         mc = e["mc_ms"]
-        for k, a in (("ring", e["allgather_ms"]["ring"]), ("mesh", e["allgather_ms"]["mesh"])):
+        for k, a in (("ring", e["allgather_ms"]["ring"]), ("mesh", e["allgather_ms"]["mesh"]),
+                     ("packed_ring", e["packed"]["transfer_ms"]["ring"]), ("packed_mesh", e["packed"]["transfer_ms"]["mesh"])):
             v = round(G.schedule(64, mc, a, "ra32", batch_ms={2: mc * ratio})["ms_per_picture"], 4)
             e["pred_ms_per_picture"][f"ra32_batched_{k}"] = v
             e["pred_mpix_s"][f"ra32_batched_{k}"] = round(area / (v * 1e-3) / 1e6, 1)
@@ -860,7 +933,7 @@ def c5_record(args, steps=3, warmup=1):
         tz_pick = (pick[:, None] * 8 + np.arange(8)[None, :]).ravel()
         tz_want = orc.sad_window(W.CUR_POC, tz.pop("_blocks")[tz_pick], 0, 16,
                                  {poc: r[0] for poc, r in refs.items()}, org)
-        tz["bit_exact"] = bool(np.array_equal(tz.pop("_sads")[tz_pick], tz_want))
+        tz["bit_exact"] = bool(np.array_equal(tz.pop("_sads")[tz_pick], np.asarray(tz_want).view(np.uint32).ravel()))
         tz["bit_exact_sample"] = f"{len(pick)} seeded blocks x 8 candidates vs the oracle"
     else:
         tz.pop("_blocks")
@@ -1014,6 +1087,9 @@ def main():
                          "inside the picture's launch sequence (mm_set_dmvr, MM_PUF_DMVR)")
     ap.add_argument("--uniform-model", type=int, default=None,
                     help="per-model workload: all PUs 16x16 with this MotionModelID (SURVEY 8(d))")
+    ap.add_argument("--c4-pack", type=int, default=1, choices=(0, 1),
+                    help="C4: all-gather the stripe-packed picture (3 samples per word) and unpack it into the "
+                         "reference pool (1), or move int16 samples (0)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (RCCL over xGMI, default) or gloo (rehearsal of N ranks on one GPU: the "
                          "all-gather then stages through host memory)")

@@ -223,6 +223,24 @@ int mm_upload_ref(mm_ctx* ctx, int poc, const int16_t* y, ptrdiff_t stride_y, co
                   const int16_t* cr, ptrdiff_t stride_c, int src_is_device);
 int mm_release_ref(mm_ctx* ctx, int poc);
 
+/* C4 transport (CTU-row stripes across GPUs, one all-gather per referenced picture): the packed
+ * stripe-major picture.  The int16 stripe-major picture of `world` ranks (mm360/parallel.py
+ * StripeLayout: segment r = the luma rows of stripe r, then its Cb rows, then its Cr rows, every
+ * segment sized for the largest stripe of CTU rows of `ctu` luma rows: rows x W + 2 x (rows/2) x
+ * (W/2) samples) is carried with K = 32 / bit_depth samples per dword (3 at 10 bits, so 2/3 of the
+ * int16 bytes): sample j of a segment sits in bits (j % K) * bit_depth of dword j / K of the
+ * segment's mm_stripe_packed_dwords(...) dwords.  Samples must lie in [0, 2^bit_depth) (predicted
+ * samples do).  (No reference counterpart: the reference decodes on one CPU.)
+ *   mm_stripe_packed_dwords: dwords per packed segment.
+ *   mm_pack_samples: n int16 samples (device) -> ceil(n / K) dwords (device), on the context stream;
+ *     a rank packs its own int16 segment into its packed segment before the all-gather.
+ *   mm_upload_ref_packed: the gathered packed picture (device, world segments) becomes reference
+ *     `poc`, unpacked straight into the context's padded reference copy -- margins included, as
+ *     mm_upload_ref pads -- on the context stream. */
+int64_t mm_stripe_packed_dwords(mm_ctx* ctx, int world, int ctu);
+int mm_pack_samples(mm_ctx* ctx, const int16_t* d_src, int64_t n, uint32_t* d_dst);
+int mm_upload_ref_packed(mm_ctx* ctx, int poc, const uint32_t* d_packed, int world, int ctu);
+
 /* Parity API: n blocks, results written to out_xy (host memory) as int32 pairs
  * [X0, Y0, X1, Y1, ...] block after block, N_b = (w/sbw)*(h/sbh) pairs per block.  Blocks are at
  * most 128 x 128 in component units (VVC's MAX_CU_SIZE; MM_ERR_ARG beyond). */

@@ -13,7 +13,7 @@ from helpers import ROOT
 
 def _header_functions():
     text = open(os.path.join(ROOT, "include", "mm360.h")).read()
-    return sorted(set(re.findall(r"^(?:int|void|const char\*|mm_epipole_list\*)\s+(mm_\w+)\(", text, re.M)))
+    return sorted(set(re.findall(r"^(?:int|int64_t|void|const char\*|mm_epipole_list\*)\s+(mm_\w+)\(", text, re.M)))
 
 
 def test_header_and_binding_agree():

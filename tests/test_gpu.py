@@ -171,6 +171,48 @@ def test_pred_extreme_motion_zeroing():
     # large motions wrap around the sphere instead.
 
 
+@pytest.mark.parametrize("world", [1, 3, 8])
+def test_c4_packed_transport_uploads_the_same_reference(world):
+    """C4 transport (mm360.h, stripe-packed pictures): every rank's int16 segment packed by
+    mm_pack_samples == the host definition (mm360.parallel.pack_segment), and the packed picture
+    made a reference by mm_upload_ref_packed (unpacked straight into the padded pool copy) predicts
+    what the oracle predicts from the same planes -- with large motion, so windows reach the
+    margins the unpack fills."""
+    from mm360 import parallel as P
+    cfg = W.CONFIGS["C2"]
+    params = mm360.seq_params(cfg.width, cfg.height, cfg.models)
+    refs = {poc: W.ref_planes(cfg.width, cfg.height, poc) for poc in W.REF_POCS}
+    pus = W.pu_list(cfg, frame=4)
+    rng = np.random.default_rng(17)
+    pus["mv"] = rng.integers(-(1 << 13), 1 << 13, size=pus["mv"].shape)
+    lay = P.StripeLayout(cfg.width, cfg.height, world)
+    buf = np.zeros(lay.total, dtype=np.int16)
+    for r in range(world):
+        lay.pack(refs[W.REF_POCS[1]], r, buf)
+    nw = P.packed_words(lay, 10)
+    want_words = np.zeros(world * nw, dtype=np.uint32)
+    for r in range(world):
+        P.pack_segment(buf, lay, r, 10, want_words)
+    want = Oracle(params, EPI).predict(W.CUR_POC, pus, refs, cfg.width, cfg.height)
+    with _ctx(params) as ctx:
+        assert ctx.stripe_packed_dwords(world) == nw
+        d_buf = torch.from_numpy(buf).cuda()
+        packed = torch.full((world * nw,), -1, dtype=torch.int32, device="cuda")
+        for r in range(world):
+            ctx.pack_samples(d_buf[r * lay.seg:(r + 1) * lay.seg], packed[r * nw:(r + 1) * nw])
+        torch.cuda.synchronize()
+        assert np.array_equal(packed.cpu().numpy().view(np.uint32), want_words)
+        y, cb, cr = refs[W.REF_POCS[0]]
+        ctx.upload_ref(W.REF_POCS[0], torch.from_numpy(y).cuda(), torch.from_numpy(cb).cuda(), torch.from_numpy(cr).cuda())
+        ctx.upload_ref_packed(W.REF_POCS[1], packed, world)
+        out = _planes(cfg, -1)
+        ctx.predict_device(W.CUR_POC, mm360.pus_to_device(pus), *out)
+        ctx.synchronize()
+        for name, t, x in zip(("y", "cb", "cr"), out, want):
+            got = t.cpu().numpy()
+            assert np.array_equal(got, x), plane_mismatch(name, got, x)
+
+
 @pytest.mark.parametrize("max_cu", [8, 32, 64])
 def test_pred_small_max_cu_padded_margins(max_cu):
     """The reference pool's edge-replicated margins are sized from maxCU (mm_kernels.hip

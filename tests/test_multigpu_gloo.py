@@ -79,6 +79,33 @@ def test_stripe_layout_pointers_and_unpack():
             assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("bd", [8, 10, 12])
+def test_packed_transport_roundtrip(bd):
+    """The stripe-packed C4 transport (include/mm360.h): K = 32 // bd samples per word, every
+    bd-bit sample survives pack -> unpack, and a packed picture of every world size unpacks to the
+    planes (C3 geometry at 1, 2, 3, 8 ranks; 10 bits: 2/3 of the int16 bytes)."""
+    rng = np.random.default_rng(bd)
+    v = rng.integers(0, 1 << bd, size=1001).astype(np.int16)
+    w = P.pack_samples(v, bd)
+    assert len(w) == -(-1001 // (32 // bd)) and w.dtype == np.uint32
+    assert np.array_equal(P.unpack_samples(w, 1001, bd), v)
+    cfg = W.CONFIGS["C3"]
+    planes = [rng.integers(0, 1 << bd, size=(cfg.height, cfg.width)).astype(np.int16),
+              rng.integers(0, 1 << bd, size=(cfg.height // 2, cfg.width // 2)).astype(np.int16),
+              rng.integers(0, 1 << bd, size=(cfg.height // 2, cfg.width // 2)).astype(np.int16)]
+    for world in (1, 2, 3, 8):
+        lay = P.StripeLayout(cfg.width, cfg.height, world)
+        buf = np.zeros(lay.total, dtype=np.int16)
+        words = np.zeros(world * P.packed_words(lay, bd), dtype=np.uint32)
+        for r in range(world):
+            lay.pack(planes, r, buf)
+            P.pack_segment(buf, lay, r, bd, words)
+        for a, b in zip(P.unpack_picture(words, lay, bd), planes):
+            assert np.array_equal(a, b)
+        if bd == 10:
+            assert abs(words.nbytes / buf.nbytes - 2 / 3) < 1e-3
+
+
 def test_stripes_partition_pus():
     cfg = W.CONFIGS["C3"]
     pus = W.pu_list(cfg)
@@ -130,10 +157,12 @@ def _chain_pus(k, poc, refs):
     return pus
 
 
-def _chain_worker(rank, world, port, n_pictures, out_dir, batch=1):
+def _chain_worker(rank, world, port, n_pictures, out_dir, batch=1, packed=False):
     """One rank of the C4 decode-order loop (mm360.gop.DependencyLoop) on CPU: every picture is
     predicted FROM the gathered pictures it references, so a missing or early reference wait
-    would show up as a wrong picture."""
+    would show up as a wrong picture.  packed: the all-gather carries the stripe-packed picture
+    (10-bit samples, three per word: mm360.parallel.pack_segment / unpack_picture, the host
+    definition of mm_pack_samples / mm_upload_ref_packed)."""
     import sys
     for p in (os.path.join(ROOT, "vvc-extension-mm_amd"), ROOT, os.path.join(ROOT, "tests", "native")):
         sys.path.insert(0, p)
@@ -170,9 +199,16 @@ def _chain_worker(rank, world, port, n_pictures, out_dir, batch=1):
 
     def gather(b):
         poc = buf_poc.get(b, cur.get("poc")) if batch > 1 else cur["poc"]
-        t = torch.from_numpy(bufs[b])
-        P.allgather_packed(t, lay)
-        decoded[poc] = lay.unpack(t.numpy())
+        if packed:
+            words = np.zeros(world * P.packed_words(lay, 10), dtype=np.uint32)
+            P.pack_segment(bufs[b], lay, rank, 10, words)
+            t = torch.from_numpy(words.view(np.int32))
+            P.allgather_packed(t, lay)
+            decoded[poc] = P.unpack_picture(t.numpy().view(np.uint32), lay, 10)
+        else:
+            t = torch.from_numpy(bufs[b])
+            P.allgather_packed(t, lay)
+            decoded[poc] = lay.unpack(t.numpy())
         return ("gathered", poc)
 
     waits = []
@@ -240,17 +276,18 @@ def test_schedule_model():
         assert abs(cheap - (64 - 0.5 * n_batched) / 64) < 1e-9, (cheap, n_batched)
 
 
-@pytest.mark.parametrize("batch", [1, 2])
-def test_gloo_decode_order_chain(tmp_path, batch):
+@pytest.mark.parametrize("batch,packed", [(1, False), (2, False), (1, True), (2, True)])
+def test_gloo_decode_order_chain(tmp_path, batch, packed):
     """C4 decode-order loop, world 2: each picture of an RA GOP-8 sequence is predicted from its
     gathered references; only referenced pictures are all-gathered (every rank then holds exactly
     the unsharded picture), unreferenced ones stay sharded (each rank holds its stripe of it), and
     each picture waited for the all-gathers of all its references decoded in the sequence.
     batch 2: independent consecutive pictures (the leaves 1 and 3) are predicted together in one
-    multi-picture call (DependencyLoop.step_batch, mm_pred_device_multi's CPU twin)."""
+    multi-picture call (DependencyLoop.step_batch, mm_pred_device_multi's CPU twin).
+    packed: the all-gathers carry the stripe-packed pictures (2/3 of the int16 bytes)."""
     n = 6
     port = _free_port()
-    mp.spawn(_chain_worker, args=(2, port, n, str(tmp_path), batch), nprocs=2, join=True)
+    mp.spawn(_chain_worker, args=(2, port, n, str(tmp_path), batch, packed), nprocs=2, join=True)
     if batch > 1:
         seq_b = G.decode_sequence(n, "ra8")
         loop = G.DependencyLoop("ra8", 2, None, None, None)

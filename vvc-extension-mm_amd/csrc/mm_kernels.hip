@@ -837,8 +837,21 @@ __global__ void __launch_bounds__(DMVR_SEARCH_WG) __attribute__((amdgpu_waves_pe
     // 1. this lane's positions, and the in-range box of its list
     int32_t pfx[DMVR_LANE_OFFS] = {}, pfy[DMVR_LANE_OFFS] = {};
     int xmin = INT_MAX, xmax = INT_MIN, ymin = INT_MAX, ymax = INT_MIN;
-    dmvr_positions_offsets(sc, u, l, e, cache, [&](int j) -> const BlockSetup& { return L.set[part * n_offs + j][l]; },
-                           n_offs, [&](int j, int32_t fx, int32_t fy) {
+#if defined(MM_DMVR_PROBE_NOTAIL)  // timing probe (wrong results): translational positions, no model
+    auto positions = [&](auto out) {
+      const int col = e / u.rows, row = e - col * u.rows, sg = l ? -1 : 1;
+      for (int j = 0; j < n_offs; j++) {
+        const int o = dmvr_outer_offset(part * n_offs + j);
+        out(j, 16 * (u.x + 4 * col) + u.mv[l][0] + sg * 16 * mmdmvr::off_x(o), 16 * (u.y + 4 * row) + u.mv[l][1] + sg * 16 * mmdmvr::off_y(o));
+      }
+    };
+#else
+    auto positions = [&](auto out) {
+      dmvr_positions_offsets(sc, u, l, e, cache, [&](int j) -> const BlockSetup& { return L.set[part * n_offs + j][l]; },
+                             n_offs, out);
+    };
+#endif
+    positions([&](int j, int32_t fx, int32_t fy) {
 #pragma unroll
                              for (int q = 0; q < DMVR_LANE_OFFS; q++)
                                if (q == j) {
@@ -909,10 +922,18 @@ __global__ void __launch_bounds__(DMVR_SEARCH_WG) __attribute__((amdgpu_waves_pe
         const uint32_t* ht = s_taps.lh[fx & 15][(xPos - 3) & 1];
         const uint32_t* vt = s_taps.lv[fy & 15];
         const int x0 = (xPos - 3) & ~1;
+#if defined(MM_DMVR_PROBE_NOFILTER)  // timing probe (wrong results): one window word, no filter
+        if (wstaged) {
+          const uint32_t q = win[(yPos - 3 - wby0) * DMVR_WIN_STRIDE + ((x0 - wbx0) >> 1)] ^ ht[0] ^ vt[0];
+#pragma unroll
+          for (int i = 0; i < 8; i++) p[i] = (int16_t)(q >> i);
+        } else {
+#else
         if (wstaged) {
           const LdsRows rows{&win[(yPos - 3 - wby0) * DMVR_WIN_STRIDE + ((x0 - wbx0) >> 1)], DMVR_WIN_STRIDE};
           predict_rows02(rows, ht, vt, geo.bd, p);
         } else {
+#endif
           const PtrRows rows{pool.base + woff + (long)((yPos - 3) * wstride + x0) * 2, wstride * 2};
           predict_rows02(rows, ht, vt, geo.bd, p);
         }
@@ -1814,6 +1835,103 @@ static int pad_plane(mm_ctx* c, int16_t* origin, const PlaneLayout& l, int w, in
   return MM_OK;
 }
 
+// ---- C4 transport: stripe-packed pictures (mm_pack_samples, mm_upload_ref_packed) -------------
+// The stripe-major picture of mm360/parallel.py StripeLayout, K = 32 / bd samples per dword
+// (mm360.h).  Packing reads the rank's int16 segment once; unpacking fills a pool slot's padded
+// planes position by position from the clamped source sample -- the interior and the margins in one
+// pass each (k_pad_plane's and k_pad_chroma_il's edge replication), so the gathered picture is
+// never materialised as int16 planes.
+constexpr int MAX_STRIPES = 64;
+struct StripePack {
+  int W, H, world, rows;  // rows: luma rows per segment (the largest stripe)
+  int K, bd;
+  long seg, seg_dw;  // int16 samples / packed dwords per segment
+  int y0[MAX_STRIPES + 1];  // first luma row of stripe r; y0[world] = H
+};
+// StripeLayout's stripes: CTU rows split evenly, r gets [n_ctu r / world, n_ctu (r + 1) / world)
+static StripePack stripe_pack(const mm_ctx* c, int world, int ctu) {
+  StripePack s{};
+  s.W = c->geo.W;
+  s.H = c->geo.H;
+  s.world = world;
+  s.bd = c->geo.bd;
+  s.K = 32 / s.bd;
+  const int n_ctu = (s.H + ctu - 1) / ctu;
+  for (int r = 0; r <= world; r++) s.y0[r] = std::min(s.H, (n_ctu * r / world) * ctu);
+  for (int r = 0; r < world; r++) s.rows = std::max(s.rows, s.y0[r + 1] - s.y0[r]);
+  s.seg = (long)s.rows * s.W + 2L * (s.rows / 2) * (s.W / 2);
+  s.seg_dw = (s.seg + s.K - 1) / s.K;
+  return s;
+}
+
+__global__ void __launch_bounds__(256) k_pack_samples(const uint16_t* __restrict__ src, long n,
+                                                      uint32_t* __restrict__ dst, int K, int bd) {
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;  // one output dword
+  const long i0 = t * K;
+  if (i0 >= n) return;
+  const uint32_t mask = (1u << bd) - 1u;
+  uint32_t w = 0;
+  for (int k = 0; k < K; k++)
+    if (i0 + k < n) w |= ((uint32_t)src[i0 + k] & mask) << (k * bd);
+  dst[t] = w;
+}
+
+// sample j of segment r of the packed picture
+__device__ __forceinline__ uint32_t packed_sample(const uint32_t* __restrict__ p, const StripePack& s, int r, long j) {
+  const long q = j / s.K;
+  return (p[r * s.seg_dw + q] >> ((int)(j - q * s.K) * s.bd)) & ((1u << s.bd) - 1u);
+}
+// the stripe holding luma row y (uniform loop over the table)
+__device__ __forceinline__ int stripe_of(const StripePack& s, int y) {
+  int r = 0;
+  for (int k = 1; k < s.world; k++) r += y >= s.y0[k] ? 1 : 0;
+  return r;
+}
+
+// One 4-sample chunk of the padded luma plane per thread: (x, y) over [-mx, W + mx) x [-my, H + my)
+__global__ void __launch_bounds__(256) k_unpack_luma(int16_t* __restrict__ o, int stride, int mx, int my,
+                                                     const uint32_t* __restrict__ p, StripePack s) {
+  typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+  const int fq = (s.W + 2 * mx) >> 2;
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long)fq * (s.H + 2 * my)) return;
+  const int row = (int)(t / fq);
+  const int x = 4 * (int)(t - (long)row * fq) - mx, y = row - my;
+  const int yc = y < 0 ? 0 : (y >= s.H ? s.H - 1 : y);
+  const int r = stripe_of(s, yc);
+  const long base = (long)(yc - s.y0[r]) * s.W;
+  uint32_t v[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int xc = x + k < 0 ? 0 : (x + k >= s.W ? s.W - 1 : x + k);
+    v[k] = packed_sample(p, s, r, base + xc);
+  }
+  *reinterpret_cast<u2*>(o + (long)y * stride + x) = u2{v[0] | (v[1] << 16), v[2] | (v[3] << 16)};
+}
+
+// One 4-position chunk of the padded interleaved chroma plane (Cb | Cr << 16) per thread
+__global__ void __launch_bounds__(256) k_unpack_chroma_il(uint32_t* __restrict__ o, int stride, int mx, int my,
+                                                          const uint32_t* __restrict__ p, StripePack s) {
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  const int w = s.W / 2, h = s.H / 2;
+  const int fq = (w + 2 * mx) >> 2;
+  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (long)fq * (h + 2 * my)) return;
+  const int row = (int)(t / fq);
+  const int x = 4 * (int)(t - (long)row * fq) - mx, y = row - my;
+  const int yc = y < 0 ? 0 : (y >= h ? h - 1 : y);
+  const int r = stripe_of(s, 2 * yc);  // chroma rows [y0 / 2, y1 / 2) of stripe r (y0 even)
+  const long luma = (long)s.rows * s.W, chroma = (long)(s.rows / 2) * w;
+  const long base = luma + (long)(yc - s.y0[r] / 2) * w;
+  uint32_t v[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int xc = x + k < 0 ? 0 : (x + k >= w ? w - 1 : x + k);
+    v[k] = packed_sample(p, s, r, base + xc) | (packed_sample(p, s, r, base + chroma + xc) << 16);
+  }
+  *reinterpret_cast<u4*>(o + (long)y * stride + x) = u4{v[0], v[1], v[2], v[3]};
+}
+
 // A free picture slot of the reference pool; grows the pool (copying the resident pictures) when
 // full.  The copy and the old allocation's release are ordered behind the context's queued work on
 // its own streams (dev_free), so no launch still reads the old allocation and nothing waits on the
@@ -1927,6 +2045,47 @@ int mm_release_ref(mm_ctx* c, int poc) {
   if (it == c->refs.end()) return fail(c, MM_ERR_NOREF, "reference POC not uploaded");
   c->pool_free.push_back(it->second.slot);  // stream-ordered: later uploads into the slot follow
   c->refs.erase(it);                        // every launch already queued on the context stream
+  return MM_OK;
+}
+
+int64_t mm_stripe_packed_dwords(mm_ctx* c, int world, int ctu) {
+  if (!c || world < 1 || world > MAX_STRIPES || ctu < 8 || (ctu & 7)) return -1;
+  return stripe_pack(c, world, ctu).seg_dw;
+}
+
+int mm_pack_samples(mm_ctx* c, const int16_t* d_src, int64_t n, uint32_t* d_dst) {
+  if (!c || n < 0 || (n > 0 && (!d_src || !d_dst))) return MM_ERR_ARG;
+  if (n == 0) return MM_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  const int K = 32 / c->geo.bd;
+  const long nd = (long)((n + K - 1) / K);
+  hipLaunchKernelGGL(k_pack_samples, dim3((unsigned)((nd + 255) / 256)), dim3(256), 0, c->stream,
+                     reinterpret_cast<const uint16_t*>(d_src), (long)n, d_dst, K, c->geo.bd);
+  HIPCHK(c, hipGetLastError());
+  return MM_OK;
+}
+
+int mm_upload_ref_packed(mm_ctx* c, int poc, const uint32_t* d_packed, int world, int ctu) {
+  if (!c || !d_packed || world < 1 || world > MAX_STRIPES || ctu < 8 || (ctu & 7)) return MM_ERR_ARG;
+  if (!c->geo.chroma) return fail(c, MM_ERR_ARG, "the stripe-packed picture is 4:2:0");
+  HIPCHK(c, hipSetDevice(c->device));
+  if (!c->refs.count(poc)) {
+    int slot = -1;
+    RCCHK(take_pool_slot(c, &slot));
+    RefHost& r = c->refs[poc];
+    r.slot = slot;
+    place_ref(c, r);
+  }
+  const RefHost& r = c->refs[poc];
+  const StripePack s = stripe_pack(c, world, ctu);
+  const PlaneLayout ly = luma_layout(c), lc = chroma_layout(c);
+  const long nl = (long)((s.W + 2 * ly.mx) >> 2) * (s.H + 2 * ly.my);
+  const long nc = (long)((s.W / 2 + 2 * lc.mx) >> 2) * (s.H / 2 + 2 * lc.my);
+  hipLaunchKernelGGL(k_unpack_luma, dim3((unsigned)((nl + 255) / 256)), dim3(256), 0, c->stream, r.y, ly.stride, ly.mx,
+                     ly.my, d_packed, s);
+  hipLaunchKernelGGL(k_unpack_chroma_il, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, c->stream,
+                     reinterpret_cast<uint32_t*>(r.cb), lc.stride, lc.mx, lc.my, d_packed, s);
+  HIPCHK(c, hipGetLastError());
   return MM_OK;
 }
 

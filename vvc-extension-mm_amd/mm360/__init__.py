@@ -59,6 +59,7 @@ EXPORTED_SYMBOLS = (
     "mm_epipole_list_destroy", "mm_get_epipole_list", "mm_epipole_add", "mm_epipole_make_available", "mm_epipole_has",
     "mm_epipole_find", "mm_epipole_derive_predictor", "mm_epipole_count", "mm_mvp_convert_device", "mm_mvp_status", "mm_set_dmvr",
     "mm_set_mvp_stream", "mm_mvp_convert_host", "mm_pred_device_multi", "mm_set_kernel_timing", "mm_kernel_times",
+    "mm_stripe_packed_dwords", "mm_pack_samples", "mm_upload_ref_packed",
 )
 
 BCW_DEFAULT = 2  # CommonDef.h:348-349; g_BcwWeights = {-2, 3, 4, 5, 10} (Rom.cpp:203)
@@ -187,6 +188,9 @@ def load_library() -> ctypes.CDLL:
         "mm_sad_window": (c_int, [vp, c_int, vp, c_int, c_int, c_int, vp]),
         "mm_last_stage_timing": (c_int, [vp, POINTER(c_float)]),
         "mm_set_kernel_timing": (c_int, [vp, c_int]),
+        "mm_stripe_packed_dwords": (ctypes.c_int64, [vp, c_int, c_int]),
+        "mm_pack_samples": (c_int, [vp, vp, ctypes.c_int64, vp]),
+        "mm_upload_ref_packed": (c_int, [vp, c_int, vp, c_int, c_int]),
         "mm_kernel_times": (c_int, [vp, POINTER(c_float), c_int, POINTER(c_int)]),
         "mm_set_stripes": (c_int, [vp, c_int]),
         "mm_set_plan_ahead": (c_int, [vp, c_int]),
@@ -572,6 +576,24 @@ class MMContext:
         ms = (c_float * 4)()
         self._check(self.lib.mm_last_stage_timing(self.h, ms))
         return tuple(float(v) for v in ms)
+
+    # -- C4 transport (mm360.h: stripe-packed pictures) --------------------------------------
+    def stripe_packed_dwords(self, world: int, ctu: int = 128) -> int:
+        """mm_stripe_packed_dwords: dwords per packed segment of a `world`-rank stripe picture."""
+        n = int(self.lib.mm_stripe_packed_dwords(self.h, world, ctu))
+        if n < 0:
+            raise MMError(MM_ERR_ARG, "mm_stripe_packed_dwords")
+        return n
+
+    def pack_samples(self, src, dst):
+        """mm_pack_samples: the int16 CUDA tensor `src` (all of it) into the int32 CUDA tensor `dst`
+        (ceil(numel / K) words, K = 32 // bit_depth), on the context stream."""
+        self._check(self.lib.mm_pack_samples(self.h, c_void_p(_ptr(src)), src.numel(), c_void_p(_ptr(dst))))
+
+    def upload_ref_packed(self, poc: int, packed, world: int, ctu: int = 128):
+        """mm_upload_ref_packed: the gathered stripe-packed picture (int32 CUDA tensor, `world`
+        segments) becomes reference `poc`, unpacked into the padded reference copy on the device."""
+        self._check(self.lib.mm_upload_ref_packed(self.h, poc, c_void_p(_ptr(packed)), world, ctu))
 
     def set_kernel_timing(self, on: bool):
         """mm_set_kernel_timing: k_mc_dev launches bracketed by kernel-bound events while on."""

@@ -89,10 +89,57 @@ class StripeLayout:
         return y, cb, cr
 
 
+def samples_per_word(bit_depth: int) -> int:
+    """K of the packed C4 transport (include/mm360.h): bit_depth-bit samples per 32-bit word."""
+    return 32 // bit_depth
+
+
+def packed_words(layout: StripeLayout, bit_depth: int) -> int:
+    """32-bit words per packed segment (mm_stripe_packed_dwords)."""
+    k = samples_per_word(bit_depth)
+    return (layout.seg + k - 1) // k
+
+
+def pack_samples(samples: np.ndarray, bit_depth: int) -> np.ndarray:
+    """Host restatement of mm_pack_samples (the format's definition, used by the CPU tests and the
+    gloo rehearsal): sample j in bits (j % K) * bit_depth of word j // K, K = 32 // bit_depth."""
+    k = samples_per_word(bit_depth)
+    v = samples.astype(np.int64).ravel() & ((1 << bit_depth) - 1)
+    v = np.concatenate([v, np.zeros((-len(v)) % k, dtype=np.int64)]).reshape(-1, k)
+    w = np.zeros(len(v), dtype=np.uint64)
+    for i in range(k):
+        w |= (v[:, i].astype(np.uint64) << np.uint64(i * bit_depth))
+    return w.astype(np.uint32)
+
+
+def unpack_samples(words: np.ndarray, n: int, bit_depth: int) -> np.ndarray:
+    """The inverse: the first n samples of packed words, as int16."""
+    k = samples_per_word(bit_depth)
+    w = words.astype(np.uint64).ravel()
+    cols = [((w >> np.uint64(i * bit_depth)) & np.uint64((1 << bit_depth) - 1)) for i in range(k)]
+    return np.stack(cols, axis=1).ravel()[:n].astype(np.int16)
+
+
+def pack_segment(buf: np.ndarray, layout: StripeLayout, rank: int, bit_depth: int, out: np.ndarray) -> None:
+    """Pack rank's int16 segment of the stripe-major picture into its segment of the packed buffer
+    `out` (uint32, world x packed_words)."""
+    nw = packed_words(layout, bit_depth)
+    out[rank * nw:(rank + 1) * nw] = pack_samples(buf[rank * layout.seg:(rank + 1) * layout.seg], bit_depth)
+
+
+def unpack_picture(words: np.ndarray, layout: StripeLayout, bit_depth: int):
+    """Full (Y, Cb, Cr) planes of a gathered packed picture (what mm_upload_ref_packed reads)."""
+    nw = packed_words(layout, bit_depth)
+    buf = np.concatenate([unpack_samples(words[r * nw:(r + 1) * nw], layout.seg, bit_depth)
+                          for r in range(layout.world)])
+    return layout.unpack(buf)
+
+
 def allgather_packed(buf, layout: StripeLayout, group=None, async_op: bool = False):
     """In place: the one collective of a sharded picture.  `buf` (torch int16, layout.total
-    elements) holds this rank's segment; afterwards every rank holds every segment.  int16 travels
-    bit-exactly as bytes (RCCL and gloo have no int16 type)."""
+    elements -- or the packed form, int32, world x packed_words) holds this rank's segment;
+    afterwards every rank holds every segment.  The samples travel bit-exactly as bytes (RCCL and
+    gloo have no int16 type)."""
     import torch
     import torch.distributed as dist
 
