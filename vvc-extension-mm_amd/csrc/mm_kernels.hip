@@ -1835,6 +1835,8 @@ static int pad_plane(mm_ctx* c, int16_t* origin, const PlaneLayout& l, int w, in
   return MM_OK;
 }
 
+}  // extern "C" (the packing kernels below are templates)
+
 // ---- C4 transport: stripe-packed pictures (mm_pack_samples, mm_upload_ref_packed) -------------
 // The stripe-major picture of mm360/parallel.py StripeLayout, K = 32 / bd samples per dword
 // (mm360.h).  Packing reads the rank's int16 segment once; unpacking fills a pool slot's padded
@@ -1876,10 +1878,12 @@ __global__ void __launch_bounds__(256) k_pack_samples(const uint16_t* __restrict
   dst[t] = w;
 }
 
-// sample j of segment r of the packed picture
-__device__ __forceinline__ uint32_t packed_sample(const uint32_t* __restrict__ p, const StripePack& s, int r, long j) {
-  const long q = j / s.K;
-  return (p[r * s.seg_dw + q] >> ((int)(j - q * s.K) * s.bd)) & ((1u << s.bd) - 1u);
+// sample j of segment r of the packed picture (32-bit indices: a segment holds < 2^31 samples; K a
+// compile-time constant, so j / K is a multiply-high, not a 64-bit division)
+template <int K>
+__device__ __forceinline__ uint32_t packed_sample(const uint32_t* __restrict__ p, const StripePack& s, int r, int j) {
+  const int q = j / K;
+  return (p[(long)r * s.seg_dw + q] >> ((j - q * K) * s.bd)) & ((1u << s.bd) - 1u);
 }
 // the stripe holding luma row y (uniform loop over the table)
 __device__ __forceinline__ int stripe_of(const StripePack& s, int y) {
@@ -1889,48 +1893,52 @@ __device__ __forceinline__ int stripe_of(const StripePack& s, int y) {
 }
 
 // One 4-sample chunk of the padded luma plane per thread: (x, y) over [-mx, W + mx) x [-my, H + my)
+template <int K>
 __global__ void __launch_bounds__(256) k_unpack_luma(int16_t* __restrict__ o, int stride, int mx, int my,
                                                      const uint32_t* __restrict__ p, StripePack s) {
   typedef uint32_t u2 __attribute__((ext_vector_type(2)));
   const int fq = (s.W + 2 * mx) >> 2;
-  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (long)fq * (s.H + 2 * my)) return;
-  const int row = (int)(t / fq);
-  const int x = 4 * (int)(t - (long)row * fq) - mx, y = row - my;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= fq * (s.H + 2 * my)) return;
+  const int row = t / fq;
+  const int x = 4 * (t - row * fq) - mx, y = row - my;
   const int yc = y < 0 ? 0 : (y >= s.H ? s.H - 1 : y);
   const int r = stripe_of(s, yc);
-  const long base = (long)(yc - s.y0[r]) * s.W;
+  const int base = (yc - s.y0[r]) * s.W;
   uint32_t v[4];
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     const int xc = x + k < 0 ? 0 : (x + k >= s.W ? s.W - 1 : x + k);
-    v[k] = packed_sample(p, s, r, base + xc);
+    v[k] = packed_sample<K>(p, s, r, base + xc);
   }
   *reinterpret_cast<u2*>(o + (long)y * stride + x) = u2{v[0] | (v[1] << 16), v[2] | (v[3] << 16)};
 }
 
 // One 4-position chunk of the padded interleaved chroma plane (Cb | Cr << 16) per thread
+template <int K>
 __global__ void __launch_bounds__(256) k_unpack_chroma_il(uint32_t* __restrict__ o, int stride, int mx, int my,
                                                           const uint32_t* __restrict__ p, StripePack s) {
   typedef uint32_t u4 __attribute__((ext_vector_type(4)));
   const int w = s.W / 2, h = s.H / 2;
   const int fq = (w + 2 * mx) >> 2;
-  const long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (long)fq * (h + 2 * my)) return;
-  const int row = (int)(t / fq);
-  const int x = 4 * (int)(t - (long)row * fq) - mx, y = row - my;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= fq * (h + 2 * my)) return;
+  const int row = t / fq;
+  const int x = 4 * (t - row * fq) - mx, y = row - my;
   const int yc = y < 0 ? 0 : (y >= h ? h - 1 : y);
   const int r = stripe_of(s, 2 * yc);  // chroma rows [y0 / 2, y1 / 2) of stripe r (y0 even)
-  const long luma = (long)s.rows * s.W, chroma = (long)(s.rows / 2) * w;
-  const long base = luma + (long)(yc - s.y0[r] / 2) * w;
+  const int luma = s.rows * s.W, chroma = (s.rows / 2) * w;
+  const int base = luma + (yc - s.y0[r] / 2) * w;
   uint32_t v[4];
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     const int xc = x + k < 0 ? 0 : (x + k >= w ? w - 1 : x + k);
-    v[k] = packed_sample(p, s, r, base + xc) | (packed_sample(p, s, r, base + chroma + xc) << 16);
+    v[k] = packed_sample<K>(p, s, r, base + xc) | (packed_sample<K>(p, s, r, base + chroma + xc) << 16);
   }
   *reinterpret_cast<u4*>(o + (long)y * stride + x) = u4{v[0], v[1], v[2], v[3]};
 }
+
+extern "C" {
 
 // A free picture slot of the reference pool; grows the pool (copying the resident pictures) when
 // full.  The copy and the old allocation's release are ordered behind the context's queued work on
@@ -2081,10 +2089,18 @@ int mm_upload_ref_packed(mm_ctx* c, int poc, const uint32_t* d_packed, int world
   const PlaneLayout ly = luma_layout(c), lc = chroma_layout(c);
   const long nl = (long)((s.W + 2 * ly.mx) >> 2) * (s.H + 2 * ly.my);
   const long nc = (long)((s.W / 2 + 2 * lc.mx) >> 2) * (s.H / 2 + 2 * lc.my);
-  hipLaunchKernelGGL(k_unpack_luma, dim3((unsigned)((nl + 255) / 256)), dim3(256), 0, c->stream, r.y, ly.stride, ly.mx,
-                     ly.my, d_packed, s);
-  hipLaunchKernelGGL(k_unpack_chroma_il, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, c->stream,
-                     reinterpret_cast<uint32_t*>(r.cb), lc.stride, lc.mx, lc.my, d_packed, s);
+  auto launch = [&](auto kl, auto kc) {
+    hipLaunchKernelGGL(kl, dim3((unsigned)((nl + 255) / 256)), dim3(256), 0, c->stream, r.y, ly.stride, ly.mx, ly.my,
+                       d_packed, s);
+    hipLaunchKernelGGL(kc, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, c->stream,
+                       reinterpret_cast<uint32_t*>(r.cb), lc.stride, lc.mx, lc.my, d_packed, s);
+  };
+  if (s.K == 4)
+    launch(k_unpack_luma<4>, k_unpack_chroma_il<4>);
+  else if (s.K == 3)
+    launch(k_unpack_luma<3>, k_unpack_chroma_il<3>);
+  else
+    launch(k_unpack_luma<2>, k_unpack_chroma_il<2>);
   HIPCHK(c, hipGetLastError());
   return MM_OK;
 }
