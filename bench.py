@@ -583,7 +583,8 @@ def bench_c4(args, cfg, params, rank, world, local, dist):
     # packed transport (include/mm360.h): each rank packs its int16 segment (3 samples per word at 10
     # bits), the all-gather moves 2/3 of the bytes, and every rank unpacks a gathered picture straight
     # into a reference pool slot (margins included) when a picture that references it is predicted --
-    # the decoder's "reconstructed picture becomes a reference" step, so its cost is in the loop
+    # the decoder's "reconstructed picture becomes a reference" step, so its cost is in the loop (the
+    # int16 transport, --c4-pack 0, uploads from the int16 stripes the same way)
     pack = bool(args.c4_pack) and world > 1
     nw = ctx.stripe_packed_dwords(world)
     pbufs = [torch.zeros(world * nw, dtype=torch.int32, device="cuda") for _ in range(n_bufs)] if pack else []
@@ -606,7 +607,10 @@ def bench_c4(args, cfg, params, rank, world, local, dist):
                 self.done = True
                 Gathered.serial[0] += 1
                 poc = 100000 + Gathered.serial[0]
-                ctx.upload_ref_packed(poc, pbufs[self.b], world)
+                if pack:
+                    ctx.upload_ref_packed(poc, pbufs[self.b], world)
+                else:
+                    ctx.upload_ref_stripes(poc, bufs[self.b], world)
                 ref_fifo.append(poc)
                 if len(ref_fifo) > 6:
                     ctx.release_ref(ref_fifo.pop(0))
@@ -623,11 +627,11 @@ def bench_c4(args, cfg, params, rank, world, local, dist):
             pbufs[b].copy_(host)
             return Gathered(None, b)
         if args.dist_backend == "nccl":
-            return P.allgather_packed(bufs[b], lay, async_op=True)
+            return Gathered(P.allgather_packed(bufs[b], lay, async_op=True), b)
         host = bufs[b].cpu()  # gloo rehearsal: host staging, synchronous
         P.allgather_packed(host, lay)
         bufs[b].copy_(host)
-        return None
+        return Gathered(None, b)
 
     def loop_for(gop_name, ref_waits=True, gather_all=False):
         """A DependencyLoop whose warm-up steps are the tail of the GOP before the timed one, so
@@ -719,7 +723,9 @@ def bench_c4(args, cfg, params, rank, world, local, dist):
                        "stripe_ctu_rows": lay.rows // 128, "allgather_bytes_in_per_rank": int(ag_bytes),
                        "transport": ("packed: 3 samples per 32-bit word (mm_pack_samples), unpacked into the "
                                      "reference pool on every rank when a picture references it "
-                                     "(mm_upload_ref_packed)" if pack else "int16 samples"),
+                                     "(mm_upload_ref_packed)" if pack else
+                                     "int16 samples, uploaded into the reference pool on every rank when a "
+                                     "picture references it (mm_upload_ref_stripes)"),
                        "gop": "ra32", "timed_pictures": "decode-order pictures 0..steps-1 of a GOP",
                        "plan_ahead": bool(args.plan_ahead), "parallelism": f"ctu-row stripes x{world}"},
             "ra_gop8": dict(per(results["ra8"]), note="same loop, dyadic hierarchical-B GOP-8 decode order"),
@@ -806,17 +812,29 @@ def bench_c4_emulate(args, cfg, params):
         e1.record()
         e1.synchronize()
         unpack_ms = e0.elapsed_time(e1) / 10
+        full16 = torch.zeros(lay.total, dtype=torch.int16, device="cuda")
+        ctx.upload_ref_stripes(999, full16, n)
+        e0.record()
+        for _ in range(10):
+            ctx.upload_ref_stripes(999, full16, n)
+        e1.record()
+        e1.synchronize()
+        up16_ms = e0.elapsed_time(e1) / 10
         ctx.release_ref(999)
         ag_p = (n - 1) * nw * 4
         ring_p = pack_ms + ag_p / link * 1e3 + unpack_ms
         mesh_p = pack_ms + ag_p / (7 * link) * 1e3 + unpack_ms
-        dep_p = {f"ra32_packed_{k}": round(G.schedule(64, mc, a, "ra32")["ms_per_picture"], 4)
-                 for k, a in (("ring", ring_p), ("mesh", mesh_p))} if n > 1 else {}
+        ring_u, mesh_u = ring * 1e3 + up16_ms, mesh * 1e3 + up16_ms
+        dep_p = {f"ra32_{t}_{k}": round(G.schedule(64, mc, a, "ra32")["ms_per_picture"], 4)
+                 for t, k, a in (("packed", "ring", ring_p), ("packed", "mesh", mesh_p),
+                                 ("int16_upload", "ring", ring_u), ("int16_upload", "mesh", mesh_u))} if n > 1 else {}
         out["n"][n] = {"mc_ms": round(mc, 4), "host_issue_ms": round(issue * 1e3, 4),
                        "allgather_ms": {"ring": round(ring * 1e3, 4), "mesh": round(mesh * 1e3, 4)},
+                       "int16_upload_into_pool_ms": round(up16_ms, 4),
                        "packed": {"pack_ms": round(pack_ms, 4), "unpack_into_pool_ms": round(unpack_ms, 4),
                                   "allgather_bytes_in": int(ag_p), "int16_bytes_in": int(ag),
                                   "transfer_ms": {"ring": round(ring_p, 4), "mesh": round(mesh_p, 4)},
+                                  "int16_transfer_ms": {"ring": round(ring_u, 4), "mesh": round(mesh_u, 4)},
                                   "note": "pack + modelled all-gather of the packed segments + unpack into the "
                                           "reference pool, the dependent picture's wait"},
                        "pred_ms_per_picture": {"hidden_ring": round(max(worst, ring) * 1e3, 4),
@@ -874,7 +892,9 @@ def bench_c4_emulate(args, cfg, params):
         e = out["n"][n]
         mc = e["mc_ms"]
         for k, a in (("ring", e["allgather_ms"]["ring"]), ("mesh", e["allgather_ms"]["mesh"]),
-                     ("packed_ring", e["packed"]["transfer_ms"]["ring"]), ("packed_mesh", e["packed"]["transfer_ms"]["mesh"])):
+                     ("packed_ring", e["packed"]["transfer_ms"]["ring"]), ("packed_mesh", e["packed"]["transfer_ms"]["mesh"]),
+                     ("int16_upload_ring", e["packed"]["int16_transfer_ms"]["ring"]),
+                     ("int16_upload_mesh", e["packed"]["int16_transfer_ms"]["mesh"])):
             v = round(G.schedule(64, mc, a, "ra32", batch_ms={2: mc * ratio})["ms_per_picture"], 4)
             e["pred_ms_per_picture"][f"ra32_batched_{k}"] = v
             e["pred_mpix_s"][f"ra32_batched_{k}"] = round(area / (v * 1e-3) / 1e6, 1)

@@ -236,10 +236,12 @@ int mm_release_ref(mm_ctx* ctx, int poc);
  *     a rank packs its own int16 segment into its packed segment before the all-gather.
  *   mm_upload_ref_packed: the gathered packed picture (device, world segments) becomes reference
  *     `poc`, unpacked straight into the context's padded reference copy -- margins included, as
- *     mm_upload_ref pads -- on the context stream. */
+ *     mm_upload_ref pads -- on the context stream.
+ *   mm_upload_ref_stripes: the same from the int16 stripe-major picture (the unpacked transport). */
 int64_t mm_stripe_packed_dwords(mm_ctx* ctx, int world, int ctu);
 int mm_pack_samples(mm_ctx* ctx, const int16_t* d_src, int64_t n, uint32_t* d_dst);
 int mm_upload_ref_packed(mm_ctx* ctx, int poc, const uint32_t* d_packed, int world, int ctu);
+int mm_upload_ref_stripes(mm_ctx* ctx, int poc, const int16_t* d_stripes, int world, int ctu);
 
 /* Parity API: n blocks, results written to out_xy (host memory) as int32 pairs
  * [X0, Y0, X1, Y1, ...] block after block, N_b = (w/sbw)*(h/sbh) pairs per block.  Blocks are at

@@ -175,9 +175,9 @@ def test_pred_extreme_motion_zeroing():
 def test_c4_packed_transport_uploads_the_same_reference(world):
     """C4 transport (mm360.h, stripe-packed pictures): every rank's int16 segment packed by
     mm_pack_samples == the host definition (mm360.parallel.pack_segment), and the packed picture
-    made a reference by mm_upload_ref_packed (unpacked straight into the padded pool copy) predicts
-    what the oracle predicts from the same planes -- with large motion, so windows reach the
-    margins the unpack fills."""
+    made a reference by mm_upload_ref_packed (unpacked straight into the padded pool copy) -- or the
+    int16 stripe-major picture by mm_upload_ref_stripes -- predicts what the oracle predicts from the
+    same planes, with large motion, so windows reach the margins the unpack fills."""
     from mm360 import parallel as P
     cfg = W.CONFIGS["C2"]
     params = mm360.seq_params(cfg.width, cfg.height, cfg.models)
@@ -204,13 +204,19 @@ def test_c4_packed_transport_uploads_the_same_reference(world):
         assert np.array_equal(packed.cpu().numpy().view(np.uint32), want_words)
         y, cb, cr = refs[W.REF_POCS[0]]
         ctx.upload_ref(W.REF_POCS[0], torch.from_numpy(y).cuda(), torch.from_numpy(cb).cuda(), torch.from_numpy(cr).cuda())
-        ctx.upload_ref_packed(W.REF_POCS[1], packed, world)
-        out = _planes(cfg, -1)
-        ctx.predict_device(W.CUR_POC, mm360.pus_to_device(pus), *out)
-        ctx.synchronize()
-        for name, t, x in zip(("y", "cb", "cr"), out, want):
-            got = t.cpu().numpy()
-            assert np.array_equal(got, x), plane_mismatch(name, got, x)
+        d_pus = mm360.pus_to_device(pus)
+        for transport in ("packed", "int16"):  # mm_upload_ref_packed, then mm_upload_ref_stripes
+            if transport == "packed":
+                ctx.upload_ref_packed(W.REF_POCS[1], packed, world)
+            else:
+                ctx.release_ref(W.REF_POCS[1])
+                ctx.upload_ref_stripes(W.REF_POCS[1], d_buf, world)
+            out = _planes(cfg, -1)
+            ctx.predict_device(W.CUR_POC, d_pus, *out)
+            ctx.synchronize()
+            for name, t, x in zip(("y", "cb", "cr"), out, want):
+                got = t.cpu().numpy()
+                assert np.array_equal(got, x), (transport, plane_mismatch(name, got, x))
 
 
 @pytest.mark.parametrize("max_cu", [8, 32, 64])

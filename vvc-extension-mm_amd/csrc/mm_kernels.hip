@@ -468,6 +468,9 @@ constexpr bool PLAN_AHEAD_HOST_WAIT = MM_PLAN_HOST_WAIT;
 #ifndef MM_REPROJ_AHEAD
 #define MM_REPROJ_AHEAD 1  // see launch_stripe
 #endif
+#ifndef MM_MC_LDS
+#define MM_MC_LDS 0  // A/B knob: dynamic LDS per k_mc_dev workgroup, to cap its workgroups per CU
+#endif
 #ifndef MM_REPROJ_LDS
 #define MM_REPROJ_LDS 0  // A/B knob: dynamic LDS per k_reproj_dev workgroup, to cap its workgroups per CU
 #endif
@@ -1880,10 +1883,15 @@ __global__ void __launch_bounds__(256) k_pack_samples(const uint16_t* __restrict
 
 // sample j of segment r of the packed picture (32-bit indices: a segment holds < 2^31 samples; K a
 // compile-time constant, so j / K is a multiply-high, not a 64-bit division)
+// K == 1: the int16 stripe-major picture itself (mm_upload_ref_stripes)
 template <int K>
 __device__ __forceinline__ uint32_t packed_sample(const uint32_t* __restrict__ p, const StripePack& s, int r, int j) {
-  const int q = j / K;
-  return (p[(long)r * s.seg_dw + q] >> ((j - q * K) * s.bd)) & ((1u << s.bd) - 1u);
+  if constexpr (K == 1) {
+    return (uint32_t)reinterpret_cast<const uint16_t*>(p)[(long)r * s.seg + j];
+  } else {
+    const int q = j / K;
+    return (p[(long)r * s.seg_dw + q] >> ((j - q * K) * s.bd)) & ((1u << s.bd) - 1u);
+  }
 }
 // the stripe holding luma row y (uniform loop over the table)
 __device__ __forceinline__ int stripe_of(const StripePack& s, int y) {
@@ -2073,7 +2081,8 @@ int mm_pack_samples(mm_ctx* c, const int16_t* d_src, int64_t n, uint32_t* d_dst)
   return MM_OK;
 }
 
-int mm_upload_ref_packed(mm_ctx* c, int poc, const uint32_t* d_packed, int world, int ctu) {
+// k: the samples per word of the source (1: the int16 stripe-major picture, mm_upload_ref_stripes)
+static int upload_ref_stripes(mm_ctx* c, int poc, const uint32_t* d_packed, int world, int ctu, bool int16) {
   if (!c || !d_packed || world < 1 || world > MAX_STRIPES || ctu < 8 || (ctu & 7)) return MM_ERR_ARG;
   if (!c->geo.chroma) return fail(c, MM_ERR_ARG, "the stripe-packed picture is 4:2:0");
   HIPCHK(c, hipSetDevice(c->device));
@@ -2085,7 +2094,8 @@ int mm_upload_ref_packed(mm_ctx* c, int poc, const uint32_t* d_packed, int world
     place_ref(c, r);
   }
   const RefHost& r = c->refs[poc];
-  const StripePack s = stripe_pack(c, world, ctu);
+  StripePack s = stripe_pack(c, world, ctu);
+  if (int16) s.K = 1;
   const PlaneLayout ly = luma_layout(c), lc = chroma_layout(c);
   const long nl = (long)((s.W + 2 * ly.mx) >> 2) * (s.H + 2 * ly.my);
   const long nc = (long)((s.W / 2 + 2 * lc.mx) >> 2) * (s.H / 2 + 2 * lc.my);
@@ -2095,7 +2105,9 @@ int mm_upload_ref_packed(mm_ctx* c, int poc, const uint32_t* d_packed, int world
     hipLaunchKernelGGL(kc, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, c->stream,
                        reinterpret_cast<uint32_t*>(r.cb), lc.stride, lc.mx, lc.my, d_packed, s);
   };
-  if (s.K == 4)
+  if (s.K == 1)
+    launch(k_unpack_luma<1>, k_unpack_chroma_il<1>);
+  else if (s.K == 4)
     launch(k_unpack_luma<4>, k_unpack_chroma_il<4>);
   else if (s.K == 3)
     launch(k_unpack_luma<3>, k_unpack_chroma_il<3>);
@@ -2103,6 +2115,12 @@ int mm_upload_ref_packed(mm_ctx* c, int poc, const uint32_t* d_packed, int world
     launch(k_unpack_luma<2>, k_unpack_chroma_il<2>);
   HIPCHK(c, hipGetLastError());
   return MM_OK;
+}
+int mm_upload_ref_packed(mm_ctx* c, int poc, const uint32_t* d_packed, int world, int ctu) {
+  return upload_ref_stripes(c, poc, d_packed, world, ctu, false);
+}
+int mm_upload_ref_stripes(mm_ctx* c, int poc, const int16_t* d_stripes, int world, int ctu) {
+  return upload_ref_stripes(c, poc, reinterpret_cast<const uint32_t*>(d_stripes), world, ctu, true);
 }
 
 int mm_reproject(mm_ctx* c, const mm_block_desc* blocks, int n, int32_t* out_xy) {
@@ -2313,9 +2331,9 @@ static int launch_stripe(mm_ctx* c, PlanSlot& S, hipStream_t st, const PicTables
     c->kt_n++;
   }
   if (geo.hp)
-    hipExtLaunchKernelGGL(k_mc_dev<true>, dim3(gm), dim3(256), 0, st, start, stop, 0, geo, S.meta.p, mc, t, dst);
+    hipExtLaunchKernelGGL(k_mc_dev<true>, dim3(gm), dim3(256), MM_MC_LDS, st, start, stop, 0, geo, S.meta.p, mc, t, dst);
   else
-    hipExtLaunchKernelGGL(k_mc_dev<false>, dim3(gm), dim3(256), 0, st, start, stop, 0, geo, S.meta.p, mc, t, dst);
+    hipExtLaunchKernelGGL(k_mc_dev<false>, dim3(gm), dim3(256), MM_MC_LDS, st, start, stop, 0, geo, S.meta.p, mc, t, dst);
   if (mc_done && (c->kt_on || !KERNEL_EVENTS)) {
     if (c->kt_on && gate_out)
       *gate_out = stop;  // bound to this k_mc_dev: no marker packet in the timed loop

@@ -59,7 +59,7 @@ EXPORTED_SYMBOLS = (
     "mm_epipole_list_destroy", "mm_get_epipole_list", "mm_epipole_add", "mm_epipole_make_available", "mm_epipole_has",
     "mm_epipole_find", "mm_epipole_derive_predictor", "mm_epipole_count", "mm_mvp_convert_device", "mm_mvp_status", "mm_set_dmvr",
     "mm_set_mvp_stream", "mm_mvp_convert_host", "mm_pred_device_multi", "mm_set_kernel_timing", "mm_kernel_times",
-    "mm_stripe_packed_dwords", "mm_pack_samples", "mm_upload_ref_packed",
+    "mm_stripe_packed_dwords", "mm_pack_samples", "mm_upload_ref_packed", "mm_upload_ref_stripes",
 )
 
 BCW_DEFAULT = 2  # CommonDef.h:348-349; g_BcwWeights = {-2, 3, 4, 5, 10} (Rom.cpp:203)
@@ -191,6 +191,7 @@ def load_library() -> ctypes.CDLL:
         "mm_stripe_packed_dwords": (ctypes.c_int64, [vp, c_int, c_int]),
         "mm_pack_samples": (c_int, [vp, vp, ctypes.c_int64, vp]),
         "mm_upload_ref_packed": (c_int, [vp, c_int, vp, c_int, c_int]),
+        "mm_upload_ref_stripes": (c_int, [vp, c_int, vp, c_int, c_int]),
         "mm_kernel_times": (c_int, [vp, POINTER(c_float), c_int, POINTER(c_int)]),
         "mm_set_stripes": (c_int, [vp, c_int]),
         "mm_set_plan_ahead": (c_int, [vp, c_int]),
@@ -594,6 +595,11 @@ class MMContext:
         """mm_upload_ref_packed: the gathered stripe-packed picture (int32 CUDA tensor, `world`
         segments) becomes reference `poc`, unpacked into the padded reference copy on the device."""
         self._check(self.lib.mm_upload_ref_packed(self.h, poc, c_void_p(_ptr(packed)), world, ctu))
+
+    def upload_ref_stripes(self, poc: int, stripes, world: int, ctu: int = 128):
+        """mm_upload_ref_stripes: the int16 stripe-major picture (CUDA tensor, StripeLayout.total
+        samples) becomes reference `poc` (the unpacked C4 transport)."""
+        self._check(self.lib.mm_upload_ref_stripes(self.h, poc, c_void_p(_ptr(stripes)), world, ctu))
 
     def set_kernel_timing(self, on: bool):
         """mm_set_kernel_timing: k_mc_dev launches bracketed by kernel-bound events while on."""
