@@ -15,7 +15,7 @@
 // centre setups and the centre cost of every sub-PU (k_dmvr_setup_dev, k_dmvr_centre_dev; a sub-PU
 // whose centre ends the search keeps its merge MVs), then for the surviving sub-PUs only --
 // compacted into a list -- the 24 other offsets' setups, positions and the search, all inside one
-// workgroup per survivor (k_dmvr_search_dev): the planner (mm_devplan.h) places every sub-PU of an MM_PUF_DMVR PU as a bi PU
+// wave per survivor (k_dmvr_search_dev): the planner (mm_devplan.h) places every sub-PU of an MM_PUF_DMVR PU as a bi PU
 // with its reprojection jobs and a SubPuDev record pointing at them, the search runs on the
 // records, and the search writes the refined MVs into those jobs before k_setup reads them --
 // step 4 is then the ordinary setup / reprojection / interpolation of the picture.

@@ -2392,7 +2392,7 @@ static int launch_pictures(mm_ctx* c, const mm_pic_job* pics, int n_pics, int on
       if (!(vy && vc)) geo.vec_store = 0;
     }
   }
-  // one stripe under stage timing, with DMVR (its setup / cost buffers are the context's) and for
+  // one stripe under stage timing, with DMVR (its setup / cost buffers are per plan slot, one picture's) and for
   // several pictures
   const int K = (c->stage_timing || dmvr || n_pics > 1)
                     ? 1
@@ -2795,8 +2795,9 @@ int mm_mvp_convert_device(mm_ctx* c, const mm_mvp_query* d_q, int n, int32_t* d_
   // queries are converted in input order.
   const bool sort = n >= MVP_SORT_MIN;
   if (sort) {
-    // the sort buffers are shared by the calls of the context: growing them drains the device
-    // (DevBuf::ensure), so a conversion still running on the MVP stream keeps its buffers
+    // the sort buffers are shared by the calls of the context: growing them frees the old ones in
+    // stream order behind the queued work (DevBuf::ensure -> dev_free), so a conversion still running
+    // on the MVP stream keeps its buffers
     HIPCHK(c, c->d_mvp_local.ensure(c, n));
     HIPCHK(c, c->d_mvp_perm.ensure(c, n));
   }
