@@ -1893,6 +1893,28 @@ __device__ __forceinline__ uint32_t packed_sample(const uint32_t* __restrict__ p
     return (p[(long)r * s.seg_dw + q] >> ((j - q * K) * s.bd)) & ((1u << s.bd) - 1u);
   }
 }
+// Samples j0 .. j0 + 3 of segment r (one run inside a plane row): with K >= 3 they lie in two
+// consecutive dwords, so an interior chunk takes two loads and one division instead of four each
+template <int K>
+__device__ __forceinline__ void packed_run4(const uint32_t* __restrict__ p, const StripePack& s, int r, int j0,
+                                            uint32_t* v) {
+  if constexpr (K < 3) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) v[k] = packed_sample<K>(p, s, r, j0 + k);
+  } else {
+    const int q = j0 / K, o = j0 - q * K;
+    const uint32_t* w = p + (long)r * s.seg_dw + q;
+    const uint32_t d0 = w[0];
+    const uint32_t d1 = o + 3 >= K ? w[1] : 0u;  // dword q + 1 only when sample j0 + 3 lies in it
+    const uint32_t mask = (1u << s.bd) - 1u;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int t = o + k;  // 0 .. 2K - 1
+      v[k] = ((t < K ? d0 : d1) >> ((t < K ? t : t - K) * s.bd)) & mask;
+    }
+  }
+}
+
 // the stripe holding luma row y (uniform loop over the table)
 __device__ __forceinline__ int stripe_of(const StripePack& s, int y) {
   int r = 0;
@@ -1914,10 +1936,14 @@ __global__ void __launch_bounds__(256) k_unpack_luma(int16_t* __restrict__ o, in
   const int r = stripe_of(s, yc);
   const int base = (yc - s.y0[r]) * s.W;
   uint32_t v[4];
+  if (x >= 0 && x + 3 < s.W) {
+    packed_run4<K>(p, s, r, base + x, v);
+  } else {
 #pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const int xc = x + k < 0 ? 0 : (x + k >= s.W ? s.W - 1 : x + k);
-    v[k] = packed_sample<K>(p, s, r, base + xc);
+    for (int k = 0; k < 4; k++) {
+      const int xc = x + k < 0 ? 0 : (x + k >= s.W ? s.W - 1 : x + k);
+      v[k] = packed_sample<K>(p, s, r, base + xc);
+    }
   }
   *reinterpret_cast<u2*>(o + (long)y * stride + x) = u2{v[0] | (v[1] << 16), v[2] | (v[3] << 16)};
 }
@@ -1938,10 +1964,18 @@ __global__ void __launch_bounds__(256) k_unpack_chroma_il(uint32_t* __restrict__
   const int luma = s.rows * s.W, chroma = (s.rows / 2) * w;
   const int base = luma + (yc - s.y0[r] / 2) * w;
   uint32_t v[4];
+  if (x >= 0 && x + 3 < w) {
+    uint32_t b[4], c[4];
+    packed_run4<K>(p, s, r, base + x, b);
+    packed_run4<K>(p, s, r, base + chroma + x, c);
 #pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const int xc = x + k < 0 ? 0 : (x + k >= w ? w - 1 : x + k);
-    v[k] = packed_sample<K>(p, s, r, base + xc) | (packed_sample<K>(p, s, r, base + chroma + xc) << 16);
+    for (int k = 0; k < 4; k++) v[k] = b[k] | (c[k] << 16);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int xc = x + k < 0 ? 0 : (x + k >= w ? w - 1 : x + k);
+      v[k] = packed_sample<K>(p, s, r, base + xc) | (packed_sample<K>(p, s, r, base + chroma + xc) << 16);
+    }
   }
   *reinterpret_cast<u4*>(o + (long)y * stride + x) = u4{v[0], v[1], v[2], v[3]};
 }
