@@ -55,6 +55,7 @@ extern "C" {
 #define MM_ERR_NOEPIPOLE 4  /* no epipole for (curPOC, refPOC) -- EpipoleList.cpp:31 CHECK */
 #define MM_ERR_MODEL 5      /* motion model not active / CLASSIC passed to reprojection */
 #define MM_ERR_NODEV 6      /* no HIP device */
+#define MM_ERR_BITSTREAM 7  /* malformed / truncated syntax (mm_*_read, mm_motion_model_decode) */
 
 /* MotionModelID, SRC/TypeDef.h:865-879 */
 enum mm_model_id {
@@ -462,6 +463,82 @@ int mm_set_dmvr(mm_ctx* ctx, int on);
  * stage timing; results do not depend on the setting.  (No reference counterpart: VTM decodes a
  * picture's PUs inside its own CTU loop.) */
 int mm_set_plan_ahead(mm_ctx* ctx, int on);
+
+/* ---------------------------------------------------------------- bitstream side (host only)
+ * The MM syntax a decoder parses around the hot path; bit-serial host code,
+ * no context and no GPU.  Bit positions are MSB-first bit offsets into caller buffers, so the
+ * fragments can be spliced into a caller's SPS / PH RBSP.
+ *   mm_sps_mm_write / _read        <- VLCWriter.cpp:1110-1142 / VLCReader.cpp:1920-1980
+ *                                     (sps_mpa_enabled_flag .. sps_global_epipole_i)
+ *   mm_ph_epipole_write / _read    <- VLCWriter.cpp:2096-2109 / VLCReader.cpp:3354-3372
+ *   mm_motion_model_candidates     <- the candidate order of CABACReader::motion_model
+ *                                     (CABACReader.cpp:2179-2296, MMConfig.cpp:7-39)
+ *   mm_motion_model_encode / _decode <- CABACWriter::motion_model / CABACReader::motion_model
+ *                                     (CABACWriter.cpp:1984-2000, CABACReader.cpp:2300-2322) on
+ *                                     VVC's CABAC engine (BinEncoder.cpp, BinDecoder.cpp) with the
+ *                                     MotionModel contexts (Contexts.cpp:420-426) */
+#define MM_MAX_CALIB_COEFFS 16   /* CALIBRATED_PROJECTION_MAX_NUM_COEFFS (CommonDef.h:442) */
+#define MM_NUM_MODEL_IDS 11      /* MotionModelID CLASSIC .. GEODESIC_CAMPOSE (TypeDef.h:865-879) */
+
+/* MMConfig's coded fields (CommonLib/MMConfig.h:15-30) */
+typedef struct mm_sps_mm {
+  int32_t mpa, t3d, tan, rot, ged, geda;  /* sps_{mpa,3dt,tan,rot,ged,geda}_enabled_flag */
+  int32_t ged_flavor;                     /* sps_ged_flavor, coded iff ged || geda */
+  int32_t mmmvp;                          /* sps_mmmvp_enabled_flag */
+  int32_t mm_offset_4x4;                  /* sps_mm_offset_4x4, 0..4 */
+  int32_t projection_fct;                 /* 0 EQUISOLID, 1 CALIBRATED, 2 EQUIRECTANGULAR */
+  uint32_t focal_length_px, optical_center_x_px, optical_center_y_px;  /* EQUISOLID / CALIBRATED */
+  uint32_t num_calibrated_coeffs;         /* CALIBRATED, <= MM_MAX_CALIB_COEFFS */
+  int32_t calibrated_coeffs[MM_MAX_CALIB_COEFFS];  /* coded ue(v), stored int (VLCReader.cpp:1970) */
+  int32_t global_epipole[3];              /* se(v), coded iff ged */
+} mm_sps_mm;
+
+/* Write the fragment at *bit_pos into buf (cap_bytes long; bits outside the fragment are left as
+ * they are), advancing *bit_pos.  Every syntax element is written; when the multi-model flags are
+ * all 0 only the six flags are.  MM_ERR_ARG: a value the reader rejects (mm_offset_4x4 outside
+ * 0..4, projection_fct outside 0..2, more than 16 calibrated coefficients, a negative ue(v) field,
+ * INT32_MIN epipole) or the buffer is too small. */
+int mm_sps_mm_write(const mm_sps_mm* sps, uint8_t* buf, int64_t cap_bytes, int64_t* bit_pos);
+/* Read the fragment at *bit_pos of a buffer holding nbits bits.  Fields not coded are 0 (the
+ * MMConfig defaults).  MM_ERR_BITSTREAM on a range violation or truncation (*bit_pos unchanged). */
+int mm_sps_mm_read(const uint8_t* buf, int64_t nbits, int64_t* bit_pos, mm_sps_mm* sps);
+/* ph_signal_epipole_delta_flag (+ three se(v)), present iff the SPS enables multi-model AND GED;
+ * the flag is 1 iff the delta is not {0, 0, 0}.  Nothing is written / read otherwise (delta = 0). */
+int mm_ph_epipole_write(const mm_sps_mm* sps, const int32_t delta[3], uint8_t* buf, int64_t cap_bytes,
+                        int64_t* bit_pos);
+int mm_ph_epipole_read(const mm_sps_mm* sps, const uint8_t* buf, int64_t nbits, int64_t* bit_pos,
+                       int32_t delta[3]);
+
+/* The motion_model() candidate list of one PU, in coding order, into cand[MM_NUM_MODEL_IDS]; *n_cand
+ * = the number of active models (getActiveMotionModels order: CLASSIC, MPA x3, 3DT, TAN, ROT,
+ * GEODESIC_CAMPOSE, GEODESIC_X/Y/Z).  pred_type is CABACReader's m_mmPredType: 0 none (the
+ * reference apps' setting, DecApp.cpp:895), 1 centre point, 2 voted, 3 sorted.  For 1-3,
+ * col_models is the collocated picture's motion field on the 4x4 grid, [grid_h][grid_w][2] int8
+ * (motionModel[list], -1 = INVALID), grid covering pic_w x pic_h; col_list = colFromL0Flag for
+ * type 1 and eColRefPicList for 2 / 3 (CABACReader.cpp:2205); (x, y, w, h) the PU's luma area.
+ * A predicted model the list does not hold leaves the order unchanged (the reference's
+ * vector::erase(end()) is undefined there).  Ties: first maximum in model-id order (type 2), a
+ * stable order (type 3).  MM_ERR_ARG on a bad argument or a field value outside -1..10. */
+int mm_motion_model_candidates(const mm_sps_mm* sps, int pred_type, const int8_t* col_models, int grid_w,
+                               int grid_h, int pic_w, int pic_h, int col_list, int x, int y, int w, int h,
+                               int32_t* cand, int32_t* n_cand);
+
+/* CABAC-code the motion_model() of n_pu PUs as one slice-data stream: the contexts initialised
+ * for (slice_qp, init_type = slice type B 0 / P 1 / I 2 after the cabac_init_flag swap), the PUs'
+ * bins in order, then end_of_slice_segment_flag (terminating bin 1), the arithmetic coder's flush
+ * and rbsp trailing bits.  cand: n_pu rows of MM_NUM_MODEL_IDS (mm_motion_model_candidates output;
+ * the first n_cand entries of each row are used), coding_depth = m_mmCodingDepth (the apps use 9).
+ * affine (optional, n_pu bytes): affine PUs code nothing and must be CLASSIC (CABACWriter.cpp:1860).
+ * With no multi-model flag set, no PU codes bins and every model must be CLASSIC.
+ * encode: *nbytes = stream length; MM_ERR_ARG if a model is not in its PU's list or cap is short.
+ * decode: models_out[n_pu]; MM_ERR_BITSTREAM if the stream is malformed, ends early, or does not
+ * end with the terminating bin and the stop pattern exactly at its last byte (BinDecoder.cpp:85-91). */
+int mm_motion_model_encode(const mm_sps_mm* sps, int slice_qp, int init_type, int coding_depth, int n_pu,
+                           const int32_t* cand, const uint8_t* affine, const int32_t* models, uint8_t* out,
+                           int64_t cap_bytes, int64_t* nbytes);
+int mm_motion_model_decode(const mm_sps_mm* sps, int slice_qp, int init_type, int coding_depth, int n_pu,
+                           const int32_t* cand, const uint8_t* affine, const uint8_t* in, int64_t nbytes,
+                           int32_t* models_out);
 
 #ifdef __cplusplus
 }

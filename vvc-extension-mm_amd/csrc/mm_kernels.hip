@@ -32,6 +32,7 @@
 #include "mm_effective.h"
 #include "mm_pipeline.h"
 #include "mm_plan.h"
+#include "mm_syntax.h"
 
 using namespace mmpipe;
 
@@ -2994,6 +2995,126 @@ int mm_filter(mm_ctx* c, int comp, int vertical, const int16_t* src, ptrdiff_t s
   if (e != hipSuccess) return fail(c, MM_ERR_HIP, hipGetErrorString(e));
   for (int r = 0; r < h; r++)
     for (int q = 0; q < w; q++) dst[(long)r * dst_stride + q] = out[(size_t)r * w + q];
+  return MM_OK;
+}
+
+// ------------------------------------------------------------- bitstream side (mm_syntax.h)
+int mm_sps_mm_write(const mm_sps_mm* sps, uint8_t* buf, int64_t cap_bytes, int64_t* bit_pos) {
+  if (!sps || !buf || !bit_pos || cap_bytes < 0 || *bit_pos < 0 || !mmsyn::sps_valid(*sps)) return MM_ERR_ARG;
+  mmsyn::BitWriter w{buf, cap_bytes * 8, *bit_pos};
+  mmsyn::write_sps_mm(w, *sps);
+  if (w.bad) return MM_ERR_ARG;
+  *bit_pos = w.pos;
+  return MM_OK;
+}
+
+int mm_sps_mm_read(const uint8_t* buf, int64_t nbits, int64_t* bit_pos, mm_sps_mm* sps) {
+  if (!buf || !bit_pos || !sps || nbits < 0 || *bit_pos < 0) return MM_ERR_ARG;
+  mmsyn::BitReader r{buf, nbits, *bit_pos};
+  mm_sps_mm s;
+  if (!mmsyn::read_sps_mm(r, s)) return MM_ERR_BITSTREAM;
+  *sps = s;
+  *bit_pos = r.pos;
+  return MM_OK;
+}
+
+int mm_ph_epipole_write(const mm_sps_mm* sps, const int32_t delta[3], uint8_t* buf, int64_t cap_bytes,
+                        int64_t* bit_pos) {
+  if (!sps || !delta || !buf || !bit_pos || cap_bytes < 0 || *bit_pos < 0) return MM_ERR_ARG;
+  mmsyn::BitWriter w{buf, cap_bytes * 8, *bit_pos};
+  mmsyn::write_ph_epipole(w, *sps, delta);
+  if (w.bad) return MM_ERR_ARG;
+  *bit_pos = w.pos;
+  return MM_OK;
+}
+
+int mm_ph_epipole_read(const mm_sps_mm* sps, const uint8_t* buf, int64_t nbits, int64_t* bit_pos, int32_t delta[3]) {
+  if (!sps || !buf || !bit_pos || !delta || nbits < 0 || *bit_pos < 0) return MM_ERR_ARG;
+  mmsyn::BitReader r{buf, nbits, *bit_pos};
+  int32_t d[3];
+  if (!mmsyn::read_ph_epipole(r, *sps, d)) return MM_ERR_BITSTREAM;
+  std::memcpy(delta, d, sizeof d);
+  *bit_pos = r.pos;
+  return MM_OK;
+}
+
+int mm_motion_model_candidates(const mm_sps_mm* sps, int pred_type, const int8_t* col_models, int grid_w,
+                               int grid_h, int pic_w, int pic_h, int col_list, int x, int y, int w, int h,
+                               int32_t* cand, int32_t* n_cand) {
+  if (!sps || !cand || !n_cand || pred_type < 0 || pred_type > 3) return MM_ERR_ARG;
+  const mmsyn::ColField f{col_models, grid_w, grid_h};
+  int n = 0;
+  if (!mmsyn::order_candidates(*sps, pred_type, &f, pic_w, pic_h, col_list, x, y, w, h, cand, &n)) return MM_ERR_ARG;
+  *n_cand = n;
+  return MM_OK;
+}
+
+// the rows' candidate lists: a permutation of the active models, n_cand of them
+static bool mm_cand_rows_ok(const mm_sps_mm& sps, const int32_t* cand, int n_pu, int* n_out) {
+  int32_t act[mmsyn::NUM_MODELS];
+  const int n = mmsyn::active_models(sps, act);
+  for (int p = 0; p < n_pu; ++p) {
+    const int32_t* row = cand + size_t(p) * MM_NUM_MODEL_IDS;
+    uint32_t seen = 0;
+    for (int i = 0; i < n; ++i) {
+      if (row[i] < 0 || row[i] >= mmsyn::NUM_MODELS || (seen >> row[i]) & 1u) return false;
+      if (std::find(act, act + n, row[i]) == act + n) return false;
+      seen |= 1u << row[i];
+    }
+  }
+  *n_out = n;
+  return true;
+}
+
+int mm_motion_model_encode(const mm_sps_mm* sps, int slice_qp, int init_type, int coding_depth, int n_pu,
+                           const int32_t* cand, const uint8_t* affine, const int32_t* models, uint8_t* out,
+                           int64_t cap_bytes, int64_t* nbytes) {
+  if (!sps || n_pu < 0 || (n_pu && (!cand || !models)) || !out || !nbytes || init_type < 0 || init_type > 2 ||
+      coding_depth < 0 || cap_bytes < 0)
+    return MM_ERR_ARG;
+  int n = 0;
+  if (!mm_cand_rows_ok(*sps, cand, n_pu, &n)) return MM_ERR_ARG;
+  const bool mm_on = mmsyn::use_multi_model(*sps);
+  mmsyn::MotionModelCtx ctx;
+  ctx.init(slice_qp, init_type);
+  mmsyn::CabacEncoder e;
+  for (int p = 0; p < n_pu; ++p) {
+    if (!mm_on || (affine && affine[p])) {  // CABACWriter.cpp:1860-1864
+      if (models[p] != mmsyn::CLASSIC) return MM_ERR_ARG;
+      continue;
+    }
+    if (!mmsyn::encode_motion_model(e, ctx, cand + size_t(p) * MM_NUM_MODEL_IDS, n, coding_depth, models[p]))
+      return MM_ERR_ARG;
+  }
+  e.end_of_slice();
+  if (int64_t(e.out.size()) > cap_bytes) return MM_ERR_ARG;
+  std::memcpy(out, e.out.data(), e.out.size());
+  *nbytes = int64_t(e.out.size());
+  return MM_OK;
+}
+
+int mm_motion_model_decode(const mm_sps_mm* sps, int slice_qp, int init_type, int coding_depth, int n_pu,
+                           const int32_t* cand, const uint8_t* affine, const uint8_t* in, int64_t nbytes,
+                           int32_t* models_out) {
+  if (!sps || n_pu < 0 || (n_pu && (!cand || !models_out)) || !in || nbytes < 0 || init_type < 0 ||
+      init_type > 2 || coding_depth < 0)
+    return MM_ERR_ARG;
+  int n = 0;
+  if (!mm_cand_rows_ok(*sps, cand, n_pu, &n)) return MM_ERR_ARG;
+  const bool mm_on = mmsyn::use_multi_model(*sps);
+  mmsyn::MotionModelCtx ctx;
+  ctx.init(slice_qp, init_type);
+  mmsyn::CabacDecoder d{in, nbytes};
+  d.start();
+  for (int p = 0; p < n_pu; ++p) {
+    if (!mm_on || (affine && affine[p])) {  // CABACReader.cpp:2172-2176
+      models_out[p] = mmsyn::CLASSIC;
+      continue;
+    }
+    models_out[p] = mmsyn::decode_motion_model(d, ctx, cand + size_t(p) * MM_NUM_MODEL_IDS, n, coding_depth);
+    if (d.bad || models_out[p] == mmsyn::INVALID) return MM_ERR_BITSTREAM;
+  }
+  if (!d.bin_trm() || !d.finish()) return MM_ERR_BITSTREAM;
   return MM_OK;
 }
 

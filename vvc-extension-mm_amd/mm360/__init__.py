@@ -43,10 +43,11 @@ MODEL_NAMES = {
     GEODESIC_CAMPOSE: "GEODESIC_CAMPOSE",
 }
 
-MM_OK, MM_ERR_ARG, MM_ERR_HIP, MM_ERR_NOREF, MM_ERR_NOEPIPOLE, MM_ERR_MODEL, MM_ERR_NODEV = range(7)
+MM_OK, MM_ERR_ARG, MM_ERR_HIP, MM_ERR_NOREF, MM_ERR_NOEPIPOLE, MM_ERR_MODEL, MM_ERR_NODEV, MM_ERR_BITSTREAM = range(8)
 ERROR_NAMES = {
     MM_ERR_ARG: "MM_ERR_ARG", MM_ERR_HIP: "MM_ERR_HIP", MM_ERR_NOREF: "MM_ERR_NOREF",
     MM_ERR_NOEPIPOLE: "MM_ERR_NOEPIPOLE", MM_ERR_MODEL: "MM_ERR_MODEL", MM_ERR_NODEV: "MM_ERR_NODEV",
+    MM_ERR_BITSTREAM: "MM_ERR_BITSTREAM",
 }
 
 # Every entry point declared in include/mm360.h (checked by the CPU test suite)
@@ -60,6 +61,8 @@ EXPORTED_SYMBOLS = (
     "mm_epipole_find", "mm_epipole_derive_predictor", "mm_epipole_count", "mm_mvp_convert_device", "mm_mvp_status", "mm_set_dmvr",
     "mm_set_mvp_stream", "mm_mvp_convert_host", "mm_pred_device_multi", "mm_set_kernel_timing", "mm_kernel_times",
     "mm_stripe_packed_dwords", "mm_pack_samples", "mm_upload_ref_packed", "mm_upload_ref_stripes",
+    "mm_sps_mm_write", "mm_sps_mm_read", "mm_ph_epipole_write", "mm_ph_epipole_read", "mm_motion_model_candidates",
+    "mm_motion_model_encode", "mm_motion_model_decode",
 )
 
 BCW_DEFAULT = 2  # CommonDef.h:348-349; g_BcwWeights = {-2, 3, 4, 5, 10} (Rom.cpp:203)
@@ -210,6 +213,16 @@ def load_library() -> ctypes.CDLL:
         "mm_epipole_count": (c_int, [vp]),
         "mm_mvp_convert_host": (c_int, [POINTER(SeqParams), vp, vp, c_int, vp, POINTER(c_int)]),
         "mm_pred_device_multi": (c_int, [vp, vp, c_int]),
+        # bitstream side (mm360.syntax); the mm_sps_mm struct is passed as a pointer
+        "mm_sps_mm_write": (c_int, [vp, vp, ctypes.c_int64, POINTER(ctypes.c_int64)]),
+        "mm_sps_mm_read": (c_int, [vp, ctypes.c_int64, POINTER(ctypes.c_int64), vp]),
+        "mm_ph_epipole_write": (c_int, [vp, POINTER(c_int32), vp, ctypes.c_int64, POINTER(ctypes.c_int64)]),
+        "mm_ph_epipole_read": (c_int, [vp, vp, ctypes.c_int64, POINTER(ctypes.c_int64), POINTER(c_int32)]),
+        "mm_motion_model_candidates": (c_int, [vp, c_int, vp, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                               c_int, POINTER(c_int32), POINTER(c_int32)]),
+        "mm_motion_model_encode": (c_int, [vp, c_int, c_int, c_int, c_int, vp, vp, vp, vp, ctypes.c_int64,
+                                           POINTER(ctypes.c_int64)]),
+        "mm_motion_model_decode": (c_int, [vp, c_int, c_int, c_int, c_int, vp, vp, vp, ctypes.c_int64, vp]),
     }
     default_lib = os.path.abspath(LIB_PATH) == os.path.join(os.path.dirname(_HERE), "lib", "libmm360.so")
     for name, (res, args) in sig.items():
