@@ -49,6 +49,13 @@ POC_STRIDE = 32  # picture f: refs (32 f, 32 f + 16), current POC 32 f + 8
 RED_DEVICE = ["cuda"]  # where the timing reductions run: "cpu" under the gloo rehearsal backend
 
 
+def build_provenance():
+    """The measured library's sha256, the tree's source sha256 and whether both match the record
+    __graft_entry__.build() wrote when it last recompiled the library (mm360/provenance.py)."""
+    from mm360 import provenance
+    return provenance.provenance(mm360.LIB_PATH)
+
+
 def measured_traffic(args, config):
     """HBM bytes per k_mc_dev launch from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes
     (profiles/r0N_traffic.json, tools/traffic_json.py), only when that profile was taken with
@@ -330,6 +337,7 @@ def bench_pictures(args, cfg, params, rank, world, local, dist):
                           "reproj": round(float(st[2]), 4), "mc": round(float(st[3]), 4),
                           "pipeline": round(float(st.sum()), 4)},
             "cpu_baseline": cpu,
+            "build": build_provenance(),
         }
         if mvp is not None:
             line["mvp"] = mvp

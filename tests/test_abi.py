@@ -77,3 +77,15 @@ def test_cpp_shim_example_builds_and_fails_loudly_without_gpu():
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 2, r.stdout + r.stderr
     assert "mm360 error 6" in r.stdout
+
+
+def test_build_provenance_record():
+    """bench.py's `build` key: the library's and the sources' sha256 against __graft_entry__.build()'s record."""
+    from mm360 import provenance
+    assert provenance.source_sha256() == provenance.source_sha256()
+    rel = [os.path.relpath(f, ROOT) for f in provenance.source_files()]
+    assert "include/mm360.h" in rel and "vvc-extension-mm_amd/csrc/mm_kernels.hip" in rel
+    if os.path.exists(mm360.LIB_PATH):
+        p = provenance.provenance(mm360.LIB_PATH)
+        assert len(p["lib_sha256"]) == 64 and len(p["src_sha256"]) == 64
+        assert "built_by_build" in p or "build_info" in p
