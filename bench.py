@@ -990,31 +990,42 @@ TZ_SQUARE = ((-1, -1), (0, -1), (1, -1), (-1, 0), (1, 0), (-1, 1), (0, 1), (1, 1
 def tz_step_record(ctx, blocks, dist=2, reps=5):
     """The encoder's dependent call pattern (InterSearch.cpp:474-526, xTZ8PointSquareSearch via
     xTZSearchHelp): ONE TZ 8-point square step at distance `dist` around every block's current best
-    (here the C5 window centre) for every PU x model of the C5 picture -- 8 range-0 candidates per
-    block through mm_sad_window -- as one device round trip including the host's wait for the SADs
-    (the next step's start points depend on them).  Time per step, and the steps an encoder could
-    afford per picture in a 30 fps budget."""
+    (here the C5 window centre) for every PU x model of the C5 picture as one device round trip
+    including the host's wait for the SADs (the next step's start points depend on them).
+    mm_sad_pattern takes the step as one pattern of 8 offsets shared by the blocks (each block's setup
+    and each sub-block's model head once for its 8 candidates); the round-5 form -- 8 range-0 blocks
+    per block through mm_sad_window -- is timed beside it.  Time per step, and the steps an encoder
+    could afford per picture in a 30 fps budget."""
+    off = np.array(TZ_SQUARE, dtype=np.int32) * (16 * dist)
     b8 = np.repeat(blocks, 8)
-    off = np.tile(np.array(TZ_SQUARE, dtype=np.int32), (len(blocks), 1)) * (16 * dist)
-    b8["mv_hor"] += off[:, 0]
-    b8["mv_ver"] += off[:, 1]
-    out = torch.zeros((len(b8), 1), dtype=torch.int32, device="cuda")
-    ctx.sad_window(W.CUR_POC, b8, 0, 16, out=out)  # warm-up (buffers)
-    res = out.cpu()
-    t = []
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        ctx.sad_window(W.CUR_POC, b8, 0, 16, out=out)
-        res = out.cpu()  # the host needs the SADs to pick the next step's start points
-        t.append(time.perf_counter() - t0)
-    ms = float(np.median(t)) * 1e3
+    o8 = np.tile(off, (len(blocks), 1))
+    b8["mv_hor"] += o8[:, 0]
+    b8["mv_ver"] += o8[:, 1]
+    out = torch.zeros((len(blocks), 8), dtype=torch.int32, device="cuda")
+
+    def run(fn):
+        fn()  # warm-up (buffers)
+        res = out.cpu()
+        t = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            res = out.cpu()  # the host needs the SADs to pick the next step's start points
+            t.append(time.perf_counter() - t0)
+        return float(np.median(t)) * 1e3, ctx.last_timing_ms(), res.numpy().view(np.uint32).reshape(len(blocks), 8)
+
+    ms, dev_ms, sads = run(lambda: ctx.sad_pattern(W.CUR_POC, blocks, off, out=out))
+    ms0, dev_ms0, sads0 = run(lambda: ctx.sad_window(W.CUR_POC, b8, 0, 16, out=out.view(-1, 1)))
     return {"candidates": int(len(b8)), "blocks": int(len(blocks)), "distance": dist,
-            "ms_per_step": round(ms, 3), "device_ms": round(ctx.last_timing_ms(), 3),
+            "ms_per_step": round(ms, 3), "device_ms": round(dev_ms, 3),
             "steps_per_33ms": int(33.3 / ms),
-            "note": "one xTZ8PointSquareSearch step for every PU x model of the picture as one mm_sad_window "
-                    "call of range-0 blocks + the SAD copy to the host, median of the calls; steps_per_33ms: "
-                    "dependent steps a 30 fps encoder could afford per picture on this path alone",
-            "_blocks": b8, "_sads": res.numpy().view(np.uint32).ravel()}
+            "range0_blocks": {"ms_per_step": round(ms0, 3), "device_ms": round(dev_ms0, 3),
+                              "equal": bool(np.array_equal(sads, sads0))},
+            "note": "one xTZ8PointSquareSearch step for every PU x model of the picture as one mm_sad_pattern call "
+                    "(8 offsets shared by the blocks) + the SAD copy to the host, median of the calls; "
+                    "range0_blocks: the same step as 8 range-0 blocks per block through mm_sad_window; "
+                    "steps_per_33ms: dependent steps a 30 fps encoder could afford per picture on this path alone",
+            "_blocks": b8, "_sads": sads.ravel()}
 
 
 def bench_me(args, cfg, params, rank, world, local, dist):

@@ -28,6 +28,8 @@
  *                       (UnitTools.cpp:2930-2992, 3134-3167); device batches serve TMVP (:2267-2304)
  *   mm_sad_window    <- InterSearch::xMVReprojectionInterpolation + RdCost::xGetSAD per candidate
  *                       (EncoderLib/InterSearch.cpp:6277-6385, 363-443; SRC/RdCost.cpp:482-517)
+ *   mm_sad_pattern   <- the same over the TZ / refinement candidate patterns (InterSearch.cpp:474-526,
+ *                       6168-6249)
  *   mm_upload_org    <- the original picture (pcPatternKey) the encoder SAD compares against
  *   mm_destroy       <- (MVReprojection / InterPrediction destructors)
  *
@@ -399,6 +401,16 @@ int mm_upload_org(mm_ctx* ctx, int poc, const int16_t* y, ptrdiff_t stride_y, in
  * reference may stop early past its running best (same search decisions). */
 int mm_sad_window(mm_ctx* ctx, int cur_poc, const mm_me_block* blocks, int n, int range, int step,
                   uint32_t* sads);
+/* The same evaluation for a pattern of k candidate offsets shared by every block (1 <= k <= 64,
+ * distinct, |offset| <= 4096 in 1/16 luma): candidate c of block b has
+ * mv = (mv_hor + offsets[2c], mv_ver + offsets[2c+1]) and its SAD goes to sads[b * k + c] (DEVICE
+ * memory).  The encoder's dependent steps -- xTZSearchHelp over the TZ 8-point square / diamond,
+ * 2-point and star patterns (EncoderLib/InterSearch.cpp:474-526, xTZSearch :5350) and the 9-point
+ * fractional refinements of xPatternRefinementProjected (:6168-6249) -- in one call per step for
+ * all blocks: each block's setup work and each sub-block's MV-independent model head and original
+ * samples are done once for its k candidates.  Same results as k range-0 mm_sad_window blocks. */
+int mm_sad_pattern(mm_ctx* ctx, int cur_poc, const mm_me_block* blocks, int n, const int32_t* offsets, int k,
+                   uint32_t* sads);
 
 /* Device time of the last mm_pred_device / mm_pred_run / mm_sad_window / mm_mvp_convert_device
  * launch sequence (HIP events on the context stream around all of its launches), milliseconds.

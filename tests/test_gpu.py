@@ -870,6 +870,48 @@ def test_sad_window_c5_full_window_vs_oracle():
     assert np.array_equal(got.argmin(axis=1), want.argmin(axis=1))
 
 
+TZ_SQUARE = [(-1, -1), (0, -1), (1, -1), (-1, 0), (1, 0), (-1, 1), (0, 1), (1, 1)]  # InterSearch.cpp:492-526
+TZ_DIAMOND = [(0, -2), (-1, -1), (1, -1), (-2, 0), (2, 0), (-1, 1), (1, 1), (0, 2)]
+
+
+@pytest.mark.parametrize("pattern", ["square1", "square8", "diamond4", "refine_half", "star32", "ragged"])
+def test_sad_pattern_vs_oracle(pattern):
+    """mm_sad_pattern (one call per TZ / refinement step, the block's setup and each sub-block's
+    model head shared by its k candidates) == the oracle's range-0 SAD of every (block, offset),
+    bit-exact, all models, edge blocks, 16x16 and ragged block sizes."""
+    from test_me import _case
+    w, h = 256, 128
+    params = mm360.seq_params(w, h, ME_ALL)
+    if pattern.startswith("square"):
+        d = int(pattern[6:])
+        off = [(16 * d * x, 16 * d * y) for x, y in TZ_SQUARE]
+    elif pattern == "diamond4":
+        off = [(32 * x, 32 * y) for x, y in TZ_DIAMOND]
+    elif pattern == "refine_half":  # xPatternRefinementProjected: 9 points, half-pel
+        off = [(8 * x, 8 * y) for y in (-1, 0, 1) for x in (-1, 0, 1)]
+    elif pattern == "star32":
+        off = [(16 * d * x, 16 * d * y) for d in (1, 2, 4, 8, 16, 32) for x, y in TZ_DIAMOND]
+    else:
+        off = [(5, -3), (0, 0), (-37, 12), (64, 64), (-1, 100), (3, 3), (-128, -7)]
+    blocks, refs, org = _case(w, h, ME_ALL, 40, seed=21 + len(off), sub_shift=1 if pattern == "ragged" else 0)
+    if pattern == "ragged":
+        blocks = blocks.copy()
+        blocks["w"] = np.minimum(blocks["w"], 8)
+    k = len(off)
+    rep = np.repeat(blocks, k)
+    o = np.tile(np.asarray(off, np.int32), (len(blocks), 1))
+    rep["mv_hor"] += o[:, 0]
+    rep["mv_ver"] += o[:, 1]
+    want = Oracle(params, EPI).sad_window(W.CUR_POC, rep, 0, 16, refs, org).reshape(len(blocks), k)
+    with _me_ctx(params, w, h) as ctx:
+        got = ctx.sad_pattern(W.CUR_POC, blocks, off).cpu().numpy().view(np.uint32)
+        got0 = ctx.sad_window(W.CUR_POC, rep, 0, 16).cpu().numpy().view(np.uint32).reshape(len(blocks), k)
+        with pytest.raises(mm360.MMError):
+            ctx.sad_pattern(W.CUR_POC, blocks, off + [off[0]])  # repeated offset
+    assert np.array_equal(got, want), np.argwhere(got != want)[:5]
+    assert np.array_equal(got0, want)
+
+
 @pytest.mark.parametrize("w,h", [(256, 128), (1024, 512)])
 def test_pred_dmvr_vs_oracle(w, h):
     """MM-DMVR on the GPU == the oracle: refined per-sub-PU deltas and predicted planes."""

@@ -591,6 +591,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MM_ME_
   const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const bool any = xmin <= xmax;  // some lane of the block has an in-range extreme candidate
   if (!any) xmin = xmax = ymin = ymax = 0;
+  xmin += w.box_lx;  // a pattern's other candidates (0 for a window)
+  xmax += w.box_hx;
+  ymin += w.box_ly;
+  ymax += w.box_hy;
   // columns [bx0, bx0 + 8 cw) hold every window (12 samples from its even start) of a position in
   // [xmin - SLACK, xmax + SLACK]; rows [by0, by0 + rows) every window's rows yPos - 3 .. yPos + 7
   const int bx0 = (xmin - ME_WIN_SLACK - 3) & ~1, by0 = ymin - ME_WIN_SLACK - 3;
@@ -2681,9 +2685,8 @@ int mm_upload_org(mm_ctx* c, int poc, const int16_t* y, ptrdiff_t sy, int src_de
   return MM_OK;
 }
 
-int mm_sad_window(mm_ctx* c, int cur_poc, const mm_me_block* blocks, int n, int range, int step, uint32_t* sads) {
-  if (!c || n < 0 || (n > 0 && (!blocks || !sads)) || range < 0 || range > 64 || step <= 0) return MM_ERR_ARG;
-  if (n == 0) return MM_OK;
+// The candidates of every block (window or pattern, mm_me.h MeWindow) -> sads[n][w.C] on the device
+static int me_run(mm_ctx* c, int cur_poc, const mm_me_block* blocks, int n, const MeWindow& w, uint32_t* sads) {
   HIPCHK(c, hipSetDevice(c->device));
   auto oit = c->orgs.find(cur_poc);
   if (oit == c->orgs.end()) return fail(c, MM_ERR_ARG, "no original picture uploaded for the current POC");
@@ -2694,11 +2697,6 @@ int mm_sad_window(mm_ctx* c, int cur_poc, const mm_me_block* blocks, int n, int 
   int rc = build_pic_tables(seq_info(c->prm), c->epipoles, cur_poc, refs, &t, &err);
   if (rc) return fail(c, rc, err);
   RCCHK(device_tables(c, &t));
-  MeWindow w;
-  w.range = range;
-  w.step = step;
-  w.side = 2 * range + 1;
-  w.C = w.side * w.side;
   std::vector<MeBatch> batches;
   rc = plan_me_window(seq_info(c->prm), t, blocks, n, w, &batches, &err, false);
   if (rc) return fail(c, rc, err);
@@ -2729,6 +2727,51 @@ int mm_sad_window(mm_ctx* c, int cur_poc, const mm_me_block* blocks, int n, int 
   HIPCHK(c, hipEventRecord(c->ev1, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return MM_OK;
+}
+
+int mm_sad_window(mm_ctx* c, int cur_poc, const mm_me_block* blocks, int n, int range, int step, uint32_t* sads) {
+  if (!c || n < 0 || (n > 0 && (!blocks || !sads)) || range < 0 || range > 64 || step <= 0) return MM_ERR_ARG;
+  if (n == 0) return MM_OK;
+  MeWindow w;
+  w.range = range;
+  w.step = step;
+  w.side = 2 * range + 1;
+  w.C = w.side * w.side;
+  return me_run(c, cur_poc, blocks, n, w, sads);
+}
+
+int mm_sad_pattern(mm_ctx* c, int cur_poc, const mm_me_block* blocks, int n, const int32_t* offsets, int k,
+                   uint32_t* sads) {
+  if (!c || n < 0 || (n > 0 && (!blocks || !sads)) || k < 1 || k > ME_MAX_PAT || !offsets) return MM_ERR_ARG;
+  MeWindow w;
+  w.range = 0;
+  w.step = 16;
+  w.side = w.C = w.npat = k;
+  for (int i = 0; i < k; i++) {
+    const int32_t ox = offsets[2 * i], oy = offsets[2 * i + 1];
+    if (ox < -4096 || ox > 4096 || oy < -4096 || oy > 4096) return fail(c, MM_ERR_ARG, "pattern offset beyond +-256 pel");
+    for (int q = 0; q < i; q++)
+      if (offsets[2 * q] == ox && offsets[2 * q + 1] == oy) return fail(c, MM_ERR_ARG, "repeated pattern offset");
+    w.pat[2 * i] = (int16_t)ox;
+    w.pat[2 * i + 1] = (int16_t)oy;
+  }
+  // the staged box: k_me_sad takes it from the first and last candidates' windows; the pattern's
+  // bounding box extends it by these (whole samples, rounded outwards)
+  int lx = 0, hx = 0, ly = 0, hy = 0;
+  const int ax0 = std::min(w.pat[0], w.pat[2 * k - 2]), ax1 = std::max(w.pat[0], w.pat[2 * k - 2]);
+  const int ay0 = std::min(w.pat[1], w.pat[2 * k - 1]), ay1 = std::max(w.pat[1], w.pat[2 * k - 1]);
+  for (int i = 0; i < k; i++) {
+    lx = std::min(lx, (w.pat[2 * i] - ax0) >> 4);
+    hx = std::max(hx, (w.pat[2 * i] - ax1 + 15) >> 4);
+    ly = std::min(ly, (w.pat[2 * i + 1] - ay0) >> 4);
+    hy = std::max(hy, (w.pat[2 * i + 1] - ay1 + 15) >> 4);
+  }
+  w.box_lx = lx;
+  w.box_hx = hx;
+  w.box_ly = ly;
+  w.box_hy = hy;
+  if (n == 0) return MM_OK;
+  return me_run(c, cur_poc, blocks, n, w, sads);
 }
 
 // MM-DMVR of a PU list: every PU is flagged MM_PUF_DMVR and the list runs the device-planned

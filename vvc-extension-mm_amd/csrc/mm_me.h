@@ -31,13 +31,28 @@ struct MeBlockDev {
   int sad_off;         // sads index of candidate 0
 };
 
+// The candidates of a block: a (2 range + 1)^2 window of MVs `step` apart (mm_sad_window; k_me_sad
+// threads per window row), or a pattern of npat MV offsets shared by every block (mm_sad_pattern: the
+// TZ search's 8-point square / diamond, 2-point and star steps and the 9-point refinements,
+// InterSearch.cpp:474-526, 6168-6249; one row of npat candidates per block).
+constexpr int ME_MAX_PAT = 64;
 struct MeWindow {
-  int range, step, side, C;  // side = 2 * range + 1, C = side * side
+  int range, step, side, C;  // window: side = 2 * range + 1, C = side * side; pattern: side = C = npat
   int seg16 = 0;             // device: every block of the batch has 16 sub-blocks (k_me_sad's 16-lane sums)
+  int npat = 0;              // pattern candidates (0: window)
+  // pattern: the staged box's extension beyond the first and last candidates' windows, in samples
+  // (the pattern's bounding box relative to those two; 0 for a window, whose extremes they are)
+  int box_lx = 0, box_hx = 0, box_ly = 0, box_hy = 0;
+  int16_t pat[2 * ME_MAX_PAT] = {};  // pattern offsets (hor, ver), 1/16 luma
 };
 
-// candidate c of the window -> MV offset (row-major over the vertical offset)
+// candidate c of the window (row-major over the vertical offset) or of the pattern -> its MV
 MM_HD void me_candidate_mv(const MeWindow& w, const MeBlockDev& b, int c, int* mvh, int* mvv) {
+  if (w.npat) {
+    *mvh = b.mvh + w.pat[2 * c];
+    *mvv = b.mvv + w.pat[2 * c + 1];
+    return;
+  }
   const int i = c % w.side - w.range, j = c / w.side - w.range;
   *mvh = b.mvh + i * w.step;
   *mvv = b.mvv + j * w.step;
@@ -90,8 +105,8 @@ MM_HD void me_elem_init(int g, int bi, const SeqConst& sc, const MeWindow& w, co
   el->vip = vip ? 1 : 0;
   el->packet = packet_lane(e, b.n) ? 1 : 0;
   const GridSphere pg = grid_point(cache, b.model, (b.x >> 2) + col, (b.y >> 2) + row, el->packet != 0);
-  // the head needs a setup that is not the zero-MV identity: at most one candidate of the window has
-  // a zero MV, so candidate 0 or 1 of the row
+  // the head needs a setup that is not the zero-MV identity: at most one candidate of the window (or of
+  // the pattern, whose offsets are distinct) has a zero MV, so candidate 0 or 1 of the row
   const BlockSetup* s0 = &setups[(long)bi * w.C + (long)j * w.side];
   if (s0->identity && w.side > 1) s0 = s0 + 1;
   el->head = motion_head(sc, *s0, el->gx, el->gy, Math{el->packet != 0}, pg);

@@ -345,7 +345,7 @@ inline int plan_me_window(const SeqInfo& s, const mmdev::PicTables& t, const mm_
     cur.blocks.push_back(d);
     cur.blk_off.push_back(d.elem_off);
     cur.n_jobs += w.C;
-    cur.n_elems += (long)w.side * nsb;  // k_me_sad thread per (window row, sub-block)
+    cur.n_elems += (long)(w.npat ? 1 : w.side) * nsb;  // k_me_sad thread per (window row, sub-block)
   }
   if (!cur.blocks.empty()) batches->push_back(std::move(cur));
   if (host_chunks)

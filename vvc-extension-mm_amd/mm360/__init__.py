@@ -61,7 +61,7 @@ EXPORTED_SYMBOLS = (
     "mm_epipole_find", "mm_epipole_derive_predictor", "mm_epipole_count", "mm_mvp_convert_device", "mm_mvp_status", "mm_set_dmvr",
     "mm_set_mvp_stream", "mm_mvp_convert_host", "mm_pred_device_multi", "mm_set_kernel_timing", "mm_kernel_times",
     "mm_stripe_packed_dwords", "mm_pack_samples", "mm_upload_ref_packed", "mm_upload_ref_stripes",
-    "mm_sps_mm_write", "mm_sps_mm_read", "mm_ph_epipole_write", "mm_ph_epipole_read", "mm_motion_model_candidates",
+    "mm_sad_pattern", "mm_sps_mm_write", "mm_sps_mm_read", "mm_ph_epipole_write", "mm_ph_epipole_read", "mm_motion_model_candidates",
     "mm_motion_model_encode", "mm_motion_model_decode",
 )
 
@@ -189,6 +189,7 @@ def load_library() -> ctypes.CDLL:
         "mm_set_mvp_stream": (c_int, [vp, vp]),
         "mm_pred_dmvr": (c_int, [vp, c_int, vp, c_int, vp, ctypes.c_ssize_t, vp, vp, ctypes.c_ssize_t, vp]),
         "mm_sad_window": (c_int, [vp, c_int, vp, c_int, c_int, c_int, vp]),
+        "mm_sad_pattern": (c_int, [vp, c_int, vp, c_int, vp, c_int, vp]),
         "mm_last_stage_timing": (c_int, [vp, POINTER(c_float)]),
         "mm_set_kernel_timing": (c_int, [vp, c_int]),
         "mm_stripe_packed_dwords": (ctypes.c_int64, [vp, c_int, c_int]),
@@ -641,6 +642,18 @@ class MMContext:
             out = torch.zeros((len(blocks), C), dtype=torch.int32, device=f"cuda:{self.device}")
         self._check(self.lib.mm_sad_window(self.h, cur_poc, c_void_p(blocks.ctypes.data), len(blocks), range_, step,
                                            c_void_p(_ptr(out))))
+        return out
+
+    def sad_pattern(self, cur_poc: int, blocks: np.ndarray, offsets, out=None):
+        """SADs of every block at mv + offsets[c] (1/16 luma, shared pattern of k candidates): a torch
+        uint32-as-int32 CUDA tensor [n_blocks, k] (mm_sad_pattern)."""
+        import torch
+        blocks = np.ascontiguousarray(blocks, dtype=ME_BLOCK_DTYPE)
+        off = np.ascontiguousarray(np.asarray(offsets, dtype=np.int32).reshape(-1, 2))
+        if out is None:
+            out = torch.zeros((len(blocks), len(off)), dtype=torch.int32, device=f"cuda:{self.device}")
+        self._check(self.lib.mm_sad_pattern(self.h, cur_poc, c_void_p(blocks.ctypes.data), len(blocks),
+                                            c_void_p(off.ctypes.data), len(off), c_void_p(_ptr(out))))
         return out
 
     # -- InterpolationFilter -----------------------------------------------------------------
