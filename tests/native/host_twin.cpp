@@ -392,10 +392,9 @@ extern "C" long twin_packed_taps_selftest(int trials) {
 }
 
 // Encoder candidate windows (mm_sad_window) through the product's planner and per-thread bodies.
-extern "C" int twin_sad_window(const mm_seq_params* p, int n_epi, const int32_t* epi, int cur_poc,
-                               const mm_me_block* blocks, int n, int range, int step, int n_refs, const int32_t* pocs,
-                               const int16_t* const* ys, int stride_y, const int16_t* org, int org_stride,
-                               uint32_t* sads) {
+static int twin_me(const mm_seq_params* p, int n_epi, const int32_t* epi, int cur_poc, const mm_me_block* blocks,
+                   int n, const mmme::MeWindow& w, int n_refs, const int32_t* pocs, const int16_t* const* ys,
+                   int stride_y, const int16_t* org, int org_stride, uint32_t* sads) {
   using namespace mmdev;
   using namespace mmme;
   Twin t;
@@ -408,7 +407,6 @@ extern "C" int twin_sad_window(const mm_seq_params* p, int n_epi, const int32_t*
   std::string err;
   int rc = build_pic_tables(seq_info(*p), em, cur_poc, refs, &tab, &err);
   if (rc) return rc;
-  MeWindow w{range, step, 2 * range + 1, (2 * range + 1) * (2 * range + 1)};
   std::vector<MeBatch> batches;
   rc = plan_me_window(seq_info(*p), tab, blocks, n, w, &batches, &err);
   if (rc) return rc;
@@ -434,6 +432,28 @@ extern "C" int twin_sad_window(const mm_seq_params* p, int n_epi, const int32_t*
     }
   }
   return 0;
+}
+
+extern "C" int twin_sad_window(const mm_seq_params* p, int n_epi, const int32_t* epi, int cur_poc,
+                               const mm_me_block* blocks, int n, int range, int step, int n_refs, const int32_t* pocs,
+                               const int16_t* const* ys, int stride_y, const int16_t* org, int org_stride,
+                               uint32_t* sads) {
+  mmme::MeWindow w{range, step, 2 * range + 1, (2 * range + 1) * (2 * range + 1)};
+  return twin_me(p, n_epi, epi, cur_poc, blocks, n, w, n_refs, pocs, ys, stride_y, org, org_stride, sads);
+}
+
+// mm_sad_pattern's host logic: one pattern of k offsets shared by the blocks (mm_me.h MeWindow::npat)
+extern "C" int twin_sad_pattern(const mm_seq_params* p, int n_epi, const int32_t* epi, int cur_poc,
+                                const mm_me_block* blocks, int n, const int32_t* offsets, int k, int n_refs,
+                                const int32_t* pocs, const int16_t* const* ys, int stride_y, const int16_t* org,
+                                int org_stride, uint32_t* sads) {
+  if (k < 1 || k > mmme::ME_MAX_PAT) return MM_ERR_ARG;
+  mmme::MeWindow w;
+  w.range = 0;
+  w.step = 16;
+  w.side = w.C = w.npat = k;
+  for (int i = 0; i < 2 * k; i++) w.pat[i] = (int16_t)offsets[i];
+  return twin_me(p, n_epi, epi, cur_poc, blocks, n, w, n_refs, pocs, ys, stride_y, org, org_stride, sads);
 }
 
 // MM-DMVR (mm_pred_dmvr): every PU flagged MM_PUF_DMVR through the device-planned path (the

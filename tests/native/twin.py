@@ -37,6 +37,8 @@ def load():
                                     c_int]
     lib.twin_sad_window.argtypes = [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
                                     c_void_p, c_int, c_void_p, c_int, c_void_p]
+    lib.twin_sad_pattern.argtypes = [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int,
+                                     c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p]
     lib.twin_pred_multi.argtypes = [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p,
                                     c_int, c_int]
@@ -150,6 +152,27 @@ def sad_window(params, cur_poc, blocks, range_, step, refs, org, epipoles=()):
                              c_void_p(out.ctypes.data))
     if rc:
         raise RuntimeError(f"twin sad_window failed: {rc}")
+    return out
+
+
+def sad_pattern(params, cur_poc, blocks, offsets, refs, org, epipoles=()):
+    """mm_sad_pattern's host twin: uint32 SADs [n_blocks, k] at mv + offsets[c]."""
+    lib = load()
+    blocks = np.ascontiguousarray(blocks)
+    off = np.ascontiguousarray(np.asarray(offsets, dtype=np.int32).reshape(-1, 2))
+    pocs = sorted(refs)
+    ys = [np.ascontiguousarray(refs[p]) for p in pocs]
+    ptrs = (c_void_p * len(pocs))(*[a.ctypes.data for a in ys])
+    org = np.ascontiguousarray(org, dtype=np.int16)
+    out = np.zeros((len(blocks), len(off)), dtype=np.uint32)
+    pa = np.array(pocs, dtype=np.int32)
+    n_epi, ea = _epi(epipoles)
+    rc = lib.twin_sad_pattern(ctypes.addressof(params), n_epi, c_void_p(ea.ctypes.data), cur_poc,
+                              c_void_p(blocks.ctypes.data), len(blocks), c_void_p(off.ctypes.data), len(off), len(pocs),
+                              c_void_p(pa.ctypes.data), ptrs, ys[0].shape[1], c_void_p(org.ctypes.data), org.shape[1],
+                              c_void_p(out.ctypes.data))
+    if rc:
+        raise RuntimeError(f"twin sad_pattern failed: {rc}")
     return out
 
 

@@ -49,6 +49,33 @@ def test_twin_sad_window_matches_oracle(w, h, models, step, sub_shift):
     assert np.array_equal(got, want), np.argwhere(got != want)[:5]
 
 
+@pytest.mark.parametrize("pattern", ["square2", "diamond8", "refine_quarter", "scattered"])
+def test_twin_sad_pattern_matches_oracle(pattern):
+    """mm_sad_pattern's host logic (planner with one thread row per block, pattern offsets, the head
+    shared by the block's candidates) == the oracle's range-0 SAD of every (block, offset)."""
+    w, h = 256, 128
+    params = mm360.seq_params(w, h, ALL)
+    sq = [(-1, -1), (0, -1), (1, -1), (-1, 0), (1, 0), (-1, 1), (0, 1), (1, 1)]
+    if pattern == "square2":
+        off = [(32 * x, 32 * y) for x, y in sq]
+    elif pattern == "diamond8":
+        off = [(0, -128), (-64, -64), (64, -64), (-128, 0), (128, 0), (-64, 64), (64, 64), (0, 128)]
+    elif pattern == "refine_quarter":
+        off = [(4 * x, 4 * y) for y in (-1, 0, 1) for x in (-1, 0, 1)]
+    else:
+        off = [(3, 0), (0, 0), (-40, 17), (100, -90), (7, 7)]
+    blocks, refs, org = _case(w, h, ALL, 50, seed=31 + len(off), sub_shift=int(pattern == "scattered"))
+    k = len(off)
+    rep = np.repeat(blocks, k)
+    o = np.tile(np.asarray(off, np.int32), (len(blocks), 1))
+    rep["mv_hor"] += o[:, 0]
+    rep["mv_ver"] += o[:, 1]
+    want = Oracle(params, EPI).sad_window(W.CUR_POC, rep, 0, 16, refs, org).reshape(len(blocks), k)
+    got = twin.sad_pattern(params, W.CUR_POC, blocks, off, refs, org, EPI)
+    assert want.max() > 0
+    assert np.array_equal(got, want), np.argwhere(got != want)[:5]
+
+
 def test_sad_window_centre_equals_uni_prediction_sad():
     """Window centre of an interior block == SAD of the decoder-path uni prediction (the two
     differ only in the out-of-range margin, which interior blocks with small motion never hit)."""
