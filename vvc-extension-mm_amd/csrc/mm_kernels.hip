@@ -823,7 +823,11 @@ __global__ void __launch_bounds__(DMVR_SEARCH_WG) __attribute__((amdgpu_waves_pe
     lds_put(reinterpret_cast<uint4*>(&s_taps)[tid], reinterpret_cast<const uint4*>(&c_packed_taps)[tid], make_uint4(~0u, ~0u, ~0u, ~0u));
   stage_arg_words<sizeof(s_ged) / 4>(reinterpret_cast<const uint32_t*>(t.ged), reinterpret_cast<uint32_t*>(s_ged));
   __syncthreads();  // s_taps, s_ged: the only LDS the waves share
+#if defined(MM_DMVR_PROBE_NOSEARCH)  // timing probe (wrong results): no survivor is searched
+  const int n_surv = 0;
+#else
   const int n_surv = (int)*w.count;
+#endif
   const RefPool pool = t.pool;
   for (int k = blockIdx.x * DMVR_WAVES + wv; k < n_surv; k += gridDim.x * DMVR_WAVES) {
     const int s = w.surv_s[k];
@@ -891,6 +895,9 @@ __global__ void __launch_bounds__(DMVR_SEARCH_WG) __attribute__((amdgpu_waves_pe
       by0[ll] = bymin - 3;
       const int cw = (bxmax + 9 - bx0[ll] + 7) >> 3, rows = bymax - bymin + 11;  // 16-byte chunks per row, rows
       staged[ll] = bxmin <= bxmax && cw * 8 <= DMVR_WIN_W && rows <= DMVR_WIN_H;
+#if defined(MM_DMVR_PROBE_NOSTAGE)  // A/B: no union window in LDS, every row from the pool (same results)
+      staged[ll] = false;
+#endif
       if (staged[ll]) {
         const char* src = pool.base + off_y[ll] + (long)(by0[ll] * stride_y[ll] + bx0[ll]) * 2;
         for (int c4 = lane; c4 < rows * cw; c4 += 64) {
