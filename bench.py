@@ -255,11 +255,13 @@ def bench_pictures(args, cfg, params, rank, world, local, dist):
     # bracketed by kernel-bound events (mm_set_kernel_timing: no marker packets; under plan-ahead
     # the stop event is the slot's gate), so its duration includes the overlap with the next
     # picture's planning and reprojection on the auxiliary queue
-    ctx.set_kernel_timing(True)
-    replay = timed(args.steps, args.warmup, step, None)
-    loop_k = ctx.kernel_times_ms()[-args.steps:]
-    ctx.set_kernel_timing(False)
-    loop_kernel_ms = float(np.mean(loop_k))
+    loop_k, replay = [], float("nan")
+    if hasattr(ctx.lib, "mm_set_kernel_timing"):  # an A/B library (--lib) of an older round may lack it
+        ctx.set_kernel_timing(True)
+        replay = timed(args.steps, args.warmup, step, None)
+        loop_k = ctx.kernel_times_ms()[-args.steps:]
+        ctx.set_kernel_timing(False)
+    loop_kernel_ms = float(np.mean(loop_k)) if len(loop_k) else None
     steps_area = sum(area[s % P_] for s in range(args.steps))
     total_area = float(steps_area)
     if dist:
@@ -278,6 +280,8 @@ def bench_pictures(args, cfg, params, rank, world, local, dist):
     alg_step = float(np.mean([alg[s % P_] for s in range(args.kernel_steps)]))
     alg_loop = float(np.mean([alg[s % P_] for s in range(args.steps)]))
     achieved_iso = alg_step / (kernel_ms * 1e-3) / 1e9
+    if loop_kernel_ms is None:
+        loop_kernel_ms = kernel_ms
     achieved = alg_loop / (loop_kernel_ms * 1e-3) / 1e9
     traffic, traffic_src = measured_traffic(args, args.config)
     mvp = None
