@@ -5,9 +5,13 @@
 // Builds a 256x128 ERP sequence context with the MPA models, uploads two synthetic reference
 // pictures, reprojects one block (MVReprojection call shape) and predicts a picture's PU list
 // four times -- host list (mm_pred), device-resident list (mm_pred_device) and two pictures in one
-// launch chain (mm_pred_device_multi) -- and checks that all predictions agree.  Exit 0 and "OK" on success; exit 2 when no HIP device is present.
+// launch chain (mm_pred_device_multi) -- and checks that all predictions agree.  The sequence
+// parameters come from an SPS MM fragment written and parsed back (mm360::MMSyntax), and the PUs'
+// motion models make a CABAC motion_model() round trip.  Exit 0 and "OK" on success; exit 2 when no
+// HIP device is present.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <vector>
@@ -16,9 +20,24 @@
 
 int main() {
   const int W = 256, H = 128;
-  mm_seq_params prm{W, H, 1, 10, 128, 128, 1, 1, (1u << MM_CLASSIC) | (1u << MM_MPA_FRONT_BACK) |
-                                                      (1u << MM_MPA_LEFT_RIGHT) | (1u << MM_MPA_TOP_BOTTOM)};
   try {
+    // the SPS as an encoder writes it and a decoder parses it (VLCWriter.cpp:1110-1142 /
+    // VLCReader.cpp:1920-1980): MPA on, MMOffset4x4 code 1, ERP projection
+    mm_sps_mm sps{};
+    sps.mpa = 1;
+    sps.mm_offset_4x4 = 1;
+    sps.ged_flavor = 1;
+    sps.projection_fct = 2;
+    std::vector<uint8_t> rbsp;
+    int64_t wpos = 5;  // inside a larger SPS: any bit offset
+    mm360::MMSyntax::writeSPS(sps, rbsp, wpos);
+    int64_t rpos = 5;
+    const mm_sps_mm parsed = mm360::MMSyntax::readSPS(rbsp.data(), wpos, rpos);
+    if (rpos != wpos || parsed.mpa != 1 || parsed.mm_offset_4x4 != 1) return 1;
+    const mm_seq_params prm = mm360::MMSyntax::seqParams(parsed, W, H, 1, 10, 128, 128);
+    if (prm.active_models != ((1u << MM_CLASSIC) | (1u << MM_MPA_FRONT_BACK) | (1u << MM_MPA_LEFT_RIGHT) |
+                              (1u << MM_MPA_TOP_BOTTOM)))
+      return 1;
     mm360::Context ctx(prm, 0);
     std::vector<int16_t> y(W * H), c((W / 2) * (H / 2));
     for (int poc : {0, 16}) {
@@ -55,6 +74,26 @@ int main() {
         const int model[2] = {MM_MPA_FRONT_BACK + (bx / 16) % 3, MM_MPA_TOP_BOTTOM};
         pred.addPU(bx, by, 16, 16, mv, ref, model);
       }
+    // the PUs' motion_model() through CABAC and back (CABACWriter / CABACReader::motion_model,
+    // m_mmCodingDepth 9, m_mmPredType 0 as the apps set them)
+    {
+      const std::vector<int32_t> act = mm360::MMSyntax::activeModels(parsed);
+      const std::vector<mm_pu_desc>& pus = pred.pus();
+      std::vector<int32_t> cand(pus.size() * MM_NUM_MODEL_IDS, -1), models(pus.size()), back(pus.size());
+      for (size_t i = 0; i < pus.size(); i++) {
+        std::copy(act.begin(), act.end(), cand.begin() + i * MM_NUM_MODEL_IDS);
+        models[i] = pus[i].model[0];
+      }
+      std::vector<uint8_t> stream(64 + 4 * pus.size());
+      int64_t nbytes = 0;
+      mm360::check(nullptr, mm_motion_model_encode(&parsed, 32, 0, 9, (int)pus.size(), cand.data(), nullptr, models.data(),
+                                                   stream.data(), (int64_t)stream.size(), &nbytes),
+                   "mm_motion_model_encode");
+      mm360::check(nullptr, mm_motion_model_decode(&parsed, 32, 0, 9, (int)pus.size(), cand.data(), nullptr, stream.data(),
+                                                   nbytes, back.data()),
+                   "mm_motion_model_decode");
+      if (back != models) return 1;
+    }
     int16_t *dy[4], *dc[4][2];
     for (int k = 0; k < 4; k++) {
       if (hipMalloc(&dy[k], W * H * 2) != hipSuccess || hipMalloc(&dc[k][0], W * H / 2) != hipSuccess ||

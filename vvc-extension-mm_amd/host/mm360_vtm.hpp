@@ -10,6 +10,9 @@
 //                              effective blocks of decoded PUs (motionCompensation's splits,
 //                              SRC/InterPrediction.cpp:1681-1810)
 //   mm360::EpipoleList         EpipoleList (SRC/EpipoleList.{h,cpp}) incl. derivePredictor
+//   mm360::MMSyntax            the MM syntax of VLCReader / VLCWriter (SPS, PH) and of
+//                              CABACReader / CABACWriter::motion_model, and the mm_seq_params a
+//                              parsed SPS gives (DecLib.cpp:2013-2050's MM initialisation)
 //
 // Status codes become exceptions, like the reference's CHECK -> Exception (SRC/TypeDef.h:1120-1135).
 // NaN reprojections (zero motion) and out-of-range sub-blocks (zero samples) are results, as in
@@ -266,5 +269,40 @@ class InterPredictionMM {
   Context* ctx_;
   std::vector<mm_pu_desc> pus_, dmvr_;
 };
+
+// ---------------------------------------------------------------------------------------------
+// The bitstream side (host only).  Bit positions are MSB-first offsets into the caller's RBSP.
+namespace MMSyntax {
+inline mm_sps_mm readSPS(const uint8_t* rbsp, int64_t nbits, int64_t& bitPos) {
+  mm_sps_mm s;
+  check(nullptr, mm_sps_mm_read(rbsp, nbits, &bitPos, &s), "mm_sps_mm_read");
+  return s;
+}
+// appends at bitPos, growing the buffer as needed
+inline void writeSPS(const mm_sps_mm& s, std::vector<uint8_t>& rbsp, int64_t& bitPos) {
+  if ((int64_t)rbsp.size() * 8 < bitPos + 2048) rbsp.resize((size_t)((bitPos + 2048 + 7) / 8), 0);
+  check(nullptr, mm_sps_mm_write(&s, rbsp.data(), (int64_t)rbsp.size(), &bitPos), "mm_sps_mm_write");
+}
+inline void readEpipoleDelta(const mm_sps_mm& s, const uint8_t* rbsp, int64_t nbits, int64_t& bitPos, int32_t delta[3]) {
+  check(nullptr, mm_ph_epipole_read(&s, rbsp, nbits, &bitPos, delta), "mm_ph_epipole_read");
+}
+// MMConfig::getActiveMotionModels order (the coding order of motion_model with m_mmPredType 0)
+inline std::vector<int32_t> activeModels(const mm_sps_mm& s) {
+  int32_t c[MM_NUM_MODEL_IDS];
+  int32_t n = 0;
+  check(nullptr, mm_motion_model_candidates(&s, 0, nullptr, 0, 0, 0, 0, 0, 0, 0, 0, 0, c, &n),
+        "mm_motion_model_candidates");
+  return std::vector<int32_t>(c, c + n);
+}
+// The sequence parameters of the MM path from a parsed SPS fragment plus the SPS's picture fields
+// (DecLib.cpp:2013-2050 builds MVReprojection from the same values)
+inline mm_seq_params seqParams(const mm_sps_mm& s, int width, int height, int chromaFormat, int bitDepth,
+                               int maxCuWidth, int maxCuHeight) {
+  uint32_t mask = 0;
+  for (int32_t m : activeModels(s)) mask |= 1u << m;
+  return mm_seq_params{width, height, chromaFormat, bitDepth, maxCuWidth, maxCuHeight, s.mm_offset_4x4,
+                       s.ged_flavor, mask};
+}
+}  // namespace MMSyntax
 
 }  // namespace mm360
