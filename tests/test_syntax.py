@@ -264,3 +264,29 @@ def test_motion_model_no_multi_model_codes_nothing():
     assert stream == O.encode_models({}, [0] * 50, [[0]] * 50)
     assert stream == b"\xfe\x80"  # end_of_slice + flush + stop bit only
     assert S.decode_motion_models(s, stream, [[0]] * 50) == [0] * 50
+
+
+def test_malformed_input_never_crashes():
+    """Random bytes into the readers: a status, never a crash or an out-of-range model (the
+    reference would read past its buffers or vectors on some of these)."""
+    rng = random.Random(99)
+    d = dict(mpa=1, t3d=1, tan=1, rot=1, ged=1, geda=1)
+    s = S.sps_mm(**d)
+    act = O.active_models(d)
+    for _ in range(300):
+        data = bytes(rng.getrandbits(8) for _ in range(rng.randint(0, 40)))
+        arr = np.frombuffer(data or b"\0", np.uint8).copy()
+        try:
+            S.read_sps_mm(arr, 8 * len(data))
+        except MMError as e:
+            assert e.code == MM_ERR_BITSTREAM
+        try:
+            S.read_ph_epipole(s, arr, 8 * len(data))
+        except MMError as e:
+            assert e.code == MM_ERR_BITSTREAM
+        n = rng.randint(0, 30)
+        try:
+            got = S.decode_motion_models(s, data, [act] * n, coding_depth=rng.choice([0, 2, 9]))
+            assert all(m in act for m in got)
+        except MMError as e:
+            assert e.code == MM_ERR_BITSTREAM
