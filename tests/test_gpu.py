@@ -912,6 +912,25 @@ def test_sad_pattern_vs_oracle(pattern):
     assert np.array_equal(got0, want)
 
 
+@pytest.mark.parametrize("step", [16, 4])
+def test_sad_pattern_grid_equals_window_at_c5_size(step):
+    """At the C5 geometry (2048x1024, every model, the whole 16x16 PU grid = 57,344 blocks): the
+    pattern entry point with the 5x5 grid pattern equals the range-2 window (same candidate order),
+    and the TZ square at distance 2 equals that window's corner / edge-centre candidates."""
+    w, h = 2048, 1024
+    params = mm360.seq_params(w, h, ME_ALL)
+    blocks = W.me_blocks(w, h, ME_ALL, grid=16, seed=13)
+    grid = [(step * i, step * j) for j in range(-2, 3) for i in range(-2, 3)]
+    sq = [(2 * step * x, 2 * step * y) for x, y in TZ_SQUARE]
+    with _me_ctx(params, w, h) as ctx:
+        win = ctx.sad_window(W.CUR_POC, blocks, 2, step).cpu().numpy().view(np.uint32)
+        pat = ctx.sad_pattern(W.CUR_POC, blocks, grid).cpu().numpy().view(np.uint32)
+        sqr = ctx.sad_pattern(W.CUR_POC, blocks, sq).cpu().numpy().view(np.uint32)
+    assert np.array_equal(pat, win)
+    idx = [(y + 2) * 5 + (x + 2) for x, y in [(2 * a, 2 * b) for a, b in TZ_SQUARE]]
+    assert np.array_equal(sqr, win[:, idx])
+
+
 @pytest.mark.parametrize("w,h", [(256, 128), (1024, 512)])
 def test_pred_dmvr_vs_oracle(w, h):
     """MM-DMVR on the GPU == the oracle: refined per-sub-PU deltas and predicted planes."""
