@@ -8,6 +8,7 @@
 // identical to the reference's edge-replicated margin (Picture.cpp:988-1048) for every
 // position the out-of-range rule lets through (|reach| <= maxCU + 3 < margin 288).
 #pragma once
+#include <cstddef>
 #include <stdint.h>
 #include "mm_numerics.h"
 
@@ -59,6 +60,13 @@ struct PackedTaps {
   uint32_t ch[32][2][6];   // chroma H [phase][parity][even 3 | odd 3]
   uint32_t cv[32][5];      // chroma V [phase][even 2 | odd 3]
 };
+// The luma members of PackedTaps, which lead the struct: an LDS copy of its first bytes (k_me_sad)
+struct PackedLumaTaps {
+  uint32_t lh[16][2][10];
+  uint32_t lv[16][9];
+};
+static_assert(sizeof(PackedLumaTaps) % 16 == 0 && offsetof(PackedTaps, lv) == offsetof(PackedLumaTaps, lv),
+              "PackedLumaTaps is the leading part of PackedTaps");
 constexpr uint32_t tap_pair_(int lo, int hi) { return ((uint32_t)lo & 0xffffu) | ((uint32_t)hi << 16); }
 template <int NT>
 constexpr void pair_sets_(const int8_t* f, uint32_t* A, uint32_t* B, uint32_t* C) {

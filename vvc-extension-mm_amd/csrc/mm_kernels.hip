@@ -395,7 +395,12 @@ __global__ void __launch_bounds__(256) k_reproj_dev(SeqConst sc, const PlanMeta*
   if (g - (int)__lane_id() >= n_elems) return;  // whole wave past the end
   const int ji = wave_find_item(job_offsets, chunk_start, g, meta->n_jobs);
   if (g >= n_elems) return;
+#if MM_REPROJ_BYVAL
+  const BlockSetup su = setups[ji];
+  reproj_thread_mc(g, ji, sc, jobs, job_offsets, su, cache, mc);
+#else
   reproj_thread_mc(g, ji, sc, jobs, job_offsets, setups[ji], cache, mc);
+#endif
 }
 
 // The tap-pair tables (4 KB) are copied into LDS once per workgroup: every lane indexes them by
@@ -535,7 +540,11 @@ __device__ __forceinline__ void wave_lds_sync() {
 constexpr int ME_WIN_W = 88, ME_WIN_H = 48;           // staged box per wave: samples x rows
 constexpr int ME_WIN_STRIDE = ME_WIN_W / 2 + 1;       // dwords per LDS row (odd: rows start on different banks)
 [[maybe_unused]] constexpr int ME_WIN_SLACK = 2;
-static_assert(MM_ME_WAVES * (4 * ME_WIN_H * ME_WIN_STRIDE * 4 + MAX_SLOTS * (int)sizeof(RefDev)) <= 160 * 1024,
+#ifndef MM_ME_LDS_TAPS
+#define MM_ME_LDS_TAPS 1  // the packed tap pairs in LDS (each candidate's tap rows are position-dependent loads)
+#endif
+static_assert(MM_ME_WAVES * (4 * ME_WIN_H * ME_WIN_STRIDE * 4 + MAX_SLOTS * (int)sizeof(RefDev) +
+                             (MM_ME_LDS_TAPS ? (int)sizeof(PackedLumaTaps) : 0)) <= 160 * 1024,
               "the workgroups of one CU fit its LDS");
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MM_ME_WAVES))) k_me_sad(SeqConst sc, Geometry geo, MeWindow w,
                                                 const MeBlockDev* __restrict__ blocks, int n_blocks,
@@ -548,13 +557,25 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MM_ME_
   __shared__ uint32_t s_win[4][ME_WIN_H * ME_WIN_STRIDE];  // per wave
 #endif
   stage_ref_table<MAX_SLOTS>(t.pool_slot4, t.pool, s_ref);
+#if MM_ME_LDS_TAPS && defined(__HIP_DEVICE_COMPILE__)
+  // every candidate reads its (phase, parity) luma tap rows at a position-dependent address: from
+  // LDS instead of a dependent constant-memory load ahead of each candidate's filter
+  __shared__ PackedLumaTaps s_lt;
+  static_assert(sizeof(PackedLumaTaps) / 16 <= 256, "one 16-byte word per thread");
+  if (threadIdx.x < sizeof(PackedLumaTaps) / 16)
+    lds_put(reinterpret_cast<uint4*>(&s_lt)[threadIdx.x], reinterpret_cast<const uint4*>(&c_packed_taps)[threadIdx.x],
+            make_uint4(~0u, ~0u, ~0u, ~0u));
+  [[maybe_unused]] const PackedLumaTaps* lt = &s_lt;
+#else
+  [[maybe_unused]] const PackedLumaTaps* lt = reinterpret_cast<const PackedLumaTaps*>(&c_packed_taps);  // its leading members
+#endif
   __syncthreads();
   const int g = xcd_block() * blockDim.x + threadIdx.x;
   const int lane = __lane_id();
   if (g - lane >= n_elems) return;  // whole wave past the end
   const int bi = wave_find_item(blk_off, chunk, g, n_blocks);
   const bool active = g < n_elems;
-  const Taps taps{c_luma_taps, c_chroma_taps, &c_packed_taps, t.pool};
+  [[maybe_unused]] const Taps taps{c_luma_taps, c_chroma_taps, &c_packed_taps, t.pool};  // MM_ME_LDS 0 / host
   MeElem el;
   int j = 0, key = -1 - lane;  // inactive lanes: distinct keys that never merge
   if (active) {
@@ -617,12 +638,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MM_ME_
   wave_lds_sync();
   const MeWin win{s_win[wv], ME_WIN_STRIDE, bx0, by0, bx0 + 8 * cw, by0 + rows};
   const bool use_win = staged && mine;
+  const RefDev rme = s_ref[active ? blocks[bi].slot : 0];
+  const int sub_shift = active ? blocks[bi].sub_shift : 0;
 #endif
 #pragma unroll 1
   for (int i = 0; i < w.side; i++) {  // uniform trip count (shuffles below)
     uint32_t v = 0;
 #if MM_ME_LDS && defined(__HIP_DEVICE_COMPILE__)
-    if (active) v = me_cand_sad_win(el, i, j, bi, sc, geo, taps, w, blocks, setups, s_ref, win, use_win);
+    if (active) {
+      // the whole setup by value: its seven 8-byte words are loaded together ahead of the tail (as a
+      // reference into global memory the fields were loaded where used: C5 1,194 vs 1,228 Mcand/s)
+      const BlockSetup su = setups[(long)bi * w.C + (long)j * w.side + i];
+      v = me_cand_sad_win(el, su, i, j, sc, geo, t.pool, lt, rme, sub_shift, win, use_win);
+    }
 #else
     if (active) v = me_cand_sad(el, i, j, bi, sc, geo, taps, w, blocks, setups, s_ref);
 #endif

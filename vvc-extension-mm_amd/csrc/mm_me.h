@@ -115,10 +115,9 @@ MM_HD void me_elem_init(int g, int bi, const SeqConst& sc, const MeWindow& w, co
     for (int k = 0; k < 4; k++) el->org[r * 4 + k] = o[(long)r * org_stride + k];
 }
 
-// The element's reprojected position (1/16 luma) for candidate i of its row j.
-MM_HD void me_cand_pos(const MeElem& el, int i, int j, int bi, const SeqConst& sc, const MeWindow& w,
-                       const BlockSetup* setups, int32_t* fx, int32_t* fy) {
-  const BlockSetup& s = setups[(long)bi * w.C + (long)j * w.side + i];
+// The element's reprojected position (1/16 luma) for candidate i of its row j, whose setup is s.
+MM_HD void me_cand_pos_s(const MeElem& el, const BlockSetup& s, int i, int j, const SeqConst& sc, int32_t* fx,
+                         int32_t* fy) {
   float mx, my;
 #if defined(MM_PROBE_ME_NOTAIL)  // timing probe (wrong results): a candidate-dependent position without the model tail
   mx = el.gx + 0.37f * (float)i + s.mvx * 1e-9f;
@@ -127,6 +126,10 @@ MM_HD void me_cand_pos(const MeElem& el, int i, int j, int bi, const SeqConst& s
   motion_tail(sc, s, el.head, el.gx, el.gy, Math{el.packet != 0}, el.mpa != 0, el.px, el.py, el.vip != 0, &mx, &my);
 #endif
   reproject_finish(sc, el.gx, el.gy, mx, my, el.packet != 0, 0, fx, fy);
+}
+MM_HD void me_cand_pos(const MeElem& el, int i, int j, int bi, const SeqConst& sc, const MeWindow& w,
+                       const BlockSetup* setups, int32_t* fx, int32_t* fy) {
+  me_cand_pos_s(el, setups[(long)bi * w.C + (long)j * w.side + i], i, j, sc, fx, fy);
 }
 
 // RdCost::xGetSAD over this sub-block's rows of the block (rows 4*row + r; subShift 1 keeps the even
@@ -192,31 +195,30 @@ struct MeWin {
   int stride, x0, y0, x1, y1;
 };
 // me_cand_sad with the window rows read from the staged window when `use` and the candidate's window
-// lies inside it; otherwise from the pool as me_cand_sad does (same integer sums either way).
-__device__ __forceinline__ uint32_t me_cand_sad_win(const MeElem& el, int i, int j, int bi, const SeqConst& sc,
-                                                    const Geometry& geo, const Taps& taps, const MeWindow& w,
-                                                    const MeBlockDev* blocks, const BlockSetup* setups,
-                                                    const RefDev* refs, const MeWin& win, bool use) {
-  const MeBlockDev& b = blocks[bi];
+// lies inside it; otherwise from the pool as me_cand_sad does (same integer sums either way).  The
+// candidate's setup `s` and the luma tap pairs come from the caller (LDS in k_me_sad).
+__device__ __forceinline__ uint32_t me_cand_sad_win(const MeElem& el, const BlockSetup& s, int i, int j,
+                                                    const SeqConst& sc, const Geometry& geo, const RefPool& pool,
+                                                    const PackedLumaTaps* lt, const RefDev& r, int sub_shift,
+                                                    const MeWin& win, bool use) {
   int32_t fx, fy;
-  me_cand_pos(el, i, j, bi, sc, w, setups, &fx, &fy);
+  me_cand_pos_s(el, s, i, j, sc, &fx, &fy);
   const int xPos = fx >> 4, yPos = fy >> 4, xFrac = fx & 15, yFrac = fy & 15;
   int16_t p[16];
   if (me_out_of_range(xPos, yPos, geo)) {
     for (int k = 0; k < 16; k++) p[k] = 0;
   } else {
-    const uint32_t* ht = taps.packed->lh[xFrac][(xPos - 3) & 1];
-    const uint32_t* vt = taps.packed->lv[yFrac];
+    const uint32_t* ht = lt->lh[xFrac][(xPos - 3) & 1];
+    const uint32_t* vt = lt->lv[yFrac];
     const int xw = (xPos - 3) & ~1;  // the window's dword-aligned rows: 12 samples from xw, rows yPos - 3 .. yPos + 7
     if (use && xw >= win.x0 && xw + 12 <= win.x1 && yPos - 3 >= win.y0 && yPos + 8 <= win.y1) {
       const LdsRows rows{win.lds + (yPos - 3 - win.y0) * win.stride + ((xw - win.x0) >> 1), win.stride};
       predict_rows<8, 4, 4>(rows, ht, vt, false, geo.bd, p);
     } else {
-      const RefDev r = refs[b.slot];
-      predict_subblock_pool<8, 4, 4>(taps.pool, r.off_y, 0, r.stride_y, xPos, yPos, ht, vt, false, geo.bd, p);
+      predict_subblock_pool<8, 4, 4>(pool, r.off_y, 0, r.stride_y, xPos, yPos, ht, vt, false, geo.bd, p);
     }
   }
-  return me_sad_of(el, b.sub_shift, p);
+  return me_sad_of(el, sub_shift, p);
 }
 #endif
 

@@ -295,9 +295,16 @@ MM_HD void mpa_cache_thread(int t, const SeqConst& sc, int plane, int cols, int 
 }
 
 // The reprojection of one element of a device-planned job, stored in k_mc's record layout.
+#ifndef MM_REPROJ_BYVAL
+#define MM_REPROJ_BYVAL 1  // k_reproj_dev copies its job record and setup by value (loads issued together)
+#endif
 MM_HD void reproj_thread_mc(int g, int ji, const SeqConst& sc, const JobDev* jobs, const int* job_offsets,
                             const BlockSetup& setup, const MpaCache& cache, const McRec& mc) {
+#if MM_REPROJ_BYVAL
+  const JobDev j = jobs[ji];
+#else
   const JobDev& j = jobs[ji];
+#endif
   // Elements are enumerated row-major over the block (the records k_mc reads and the frame-cache
   // entries are then contiguous across lanes); Eigen's column-major index still decides packet
   // vs tail.  pu_cols = cw / sbw for luma and for 4:2:0 chroma alike.
