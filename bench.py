@@ -1006,27 +1006,33 @@ def tz_step_record(ctx, blocks, dist=2, reps=5):
     b8["mv_hor"] += o8[:, 0]
     b8["mv_ver"] += o8[:, 1]
     out = torch.zeros((len(blocks), 8), dtype=torch.int32, device="cuda")
+    host = torch.empty((len(blocks), 8), dtype=torch.int32, pin_memory=True)  # an encoder's SAD buffer
 
     def run(fn):
         fn()  # warm-up (buffers)
-        res = out.cpu()
-        t = []
+        host.copy_(out)
+        t, tc = [], []
         for _ in range(reps):
             t0 = time.perf_counter()
-            fn()
-            res = out.cpu()  # the host needs the SADs to pick the next step's start points
+            fn()  # synchronous: returns with the SADs in HBM
+            t1 = time.perf_counter()
+            host.copy_(out)  # the host needs the SADs to pick the next step's start points
             t.append(time.perf_counter() - t0)
-        return float(np.median(t)) * 1e3, ctx.last_timing_ms(), res.numpy().view(np.uint32).reshape(len(blocks), 8)
+            tc.append(time.perf_counter() - t1)
+        return (float(np.median(t)) * 1e3, ctx.last_timing_ms(), float(np.median(tc)) * 1e3,
+                host.numpy().copy().view(np.uint32).reshape(len(blocks), 8))
 
-    ms, dev_ms, sads = run(lambda: ctx.sad_pattern(W.CUR_POC, blocks, off, out=out))
-    ms0, dev_ms0, sads0 = run(lambda: ctx.sad_window(W.CUR_POC, b8, 0, 16, out=out.view(-1, 1)))
+    ms, dev_ms, copy_ms, sads = run(lambda: ctx.sad_pattern(W.CUR_POC, blocks, off, out=out))
+    ms0, dev_ms0, _, sads0 = run(lambda: ctx.sad_window(W.CUR_POC, b8, 0, 16, out=out.view(-1, 1)))
     return {"candidates": int(len(b8)), "blocks": int(len(blocks)), "distance": dist,
-            "ms_per_step": round(ms, 3), "device_ms": round(dev_ms, 3),
+            "ms_per_step": round(ms, 3), "device_ms": round(dev_ms, 3), "sad_copy_ms": round(copy_ms, 3),
+            "host_ms": round(ms - dev_ms - copy_ms, 3),
             "steps_per_33ms": int(33.3 / ms),
             "range0_blocks": {"ms_per_step": round(ms0, 3), "device_ms": round(dev_ms0, 3),
                               "equal": bool(np.array_equal(sads, sads0))},
             "note": "one xTZ8PointSquareSearch step for every PU x model of the picture as one mm_sad_pattern call "
-                    "(8 offsets shared by the blocks) + the SAD copy to the host, median of the calls; "
+                    "(8 offsets shared by the blocks) + the SAD copy to a pinned host buffer, median of the calls; "
+                    "device_ms: the call's stream time (block uploads + kernels), host_ms: planning and call overhead; "
                     "range0_blocks: the same step as 8 range-0 blocks per block through mm_sad_window; "
                     "steps_per_33ms: dependent steps a 30 fps encoder could afford per picture on this path alone",
             "_blocks": b8, "_sads": sads.ravel()}
