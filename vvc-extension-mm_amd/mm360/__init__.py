@@ -10,6 +10,10 @@ Mirrors the reference's C++ call surface for this path:
       same, PU list resident in HBM               -> MMContext.predict_device (mm_pred_device)
     InterPrediction::xPredInterBlkMM, one list    -> MMContext.predict_list  (mm_pred_list)
     InterpolationFilter::filterHor / filterVer    -> MMContext.filter_hor / filter_ver
+    InterSearch::xMVReprojectionInterpolation + RdCost::xGetSAD (encoder)
+                                                  -> MMContext.sad_window (dense windows) /
+                                                     MMContext.sad_pattern (TZ / refinement steps)
+    VLCReader / CABACReader MM syntax             -> mm360.syntax (host only)
 
 Everything runs through the HIP C-ABI library ``lib/libmm360.so`` (include/mm360.h).  There is
 no CPU fallback: constructing a context without the library or without a GPU raises.
