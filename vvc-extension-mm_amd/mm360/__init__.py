@@ -321,6 +321,13 @@ def mvp_convert_host(params: SeqParams, queries: np.ndarray, epipoles: Optional[
     return out[:len(q)]
 
 
+def _check_sad_out(out, n: int) -> None:
+    """The SAD output the library writes n uint32 into: a contiguous 4-byte CUDA tensor that large
+    (the C-ABI takes a bare device pointer and cannot check it)."""
+    if not getattr(out, "is_cuda", False) or out.element_size() != 4 or not out.is_contiguous() or out.numel() < n:
+        raise MMError(MM_ERR_ARG, f"SAD output must be a contiguous 4-byte CUDA tensor of >= {n} elements")
+
+
 def _ptr(a) -> int:
     """Address of a numpy array or a torch tensor (host or device)."""
     if isinstance(a, np.ndarray):
@@ -644,6 +651,7 @@ class MMContext:
         C = (2 * range_ + 1) ** 2
         if out is None:
             out = torch.zeros((len(blocks), C), dtype=torch.int32, device=f"cuda:{self.device}")
+        _check_sad_out(out, len(blocks) * C)
         self._check(self.lib.mm_sad_window(self.h, cur_poc, c_void_p(blocks.ctypes.data), len(blocks), range_, step,
                                            c_void_p(_ptr(out))))
         return out
@@ -656,6 +664,7 @@ class MMContext:
         off = np.ascontiguousarray(np.asarray(offsets, dtype=np.int32).reshape(-1, 2))
         if out is None:
             out = torch.zeros((len(blocks), len(off)), dtype=torch.int32, device=f"cuda:{self.device}")
+        _check_sad_out(out, len(blocks) * len(off))
         self._check(self.lib.mm_sad_pattern(self.h, cur_poc, c_void_p(blocks.ctypes.data), len(blocks),
                                             c_void_p(off.ctypes.data), len(off), c_void_p(_ptr(out))))
         return out
