@@ -434,6 +434,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MM_MC_
   static_assert(sizeof(PackedTaps) % 16 == 0 && sizeof(PackedTaps) / 16 <= 256, "one 16-byte word per thread");
   const int first = b0 + (int)(blockIdx.x >> 3) * 256;
   if (first >= b1) return;  // whole workgroup past the band's end
+#if defined(MM_MC_PRIO) && defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_s_setprio(MM_MC_PRIO);  // A/B: issue priority over the next picture's reprojection waves
+#endif
   if (threadIdx.x < sizeof(PackedTaps) / 16)
     lds_put(reinterpret_cast<uint4*>(&s_taps)[threadIdx.x], reinterpret_cast<const uint4*>(&c_packed_taps)[threadIdx.x], make_uint4(~0u, ~0u, ~0u, ~0u));
   stage_ref_table<MAX_SLOTS>(t.pool_slot4, t.pool, s_ref);
